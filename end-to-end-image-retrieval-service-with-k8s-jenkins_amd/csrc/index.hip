@@ -1,0 +1,510 @@
+// index.hip — the in-HBM exact cosine index that replaces Pinecone
+// (reference: get_index ingesting/utils.py:23-38, upsert ingesting/main.py:156-158,
+//  query retriever/utils.py:59-66, fetch retriever/main.py:142).
+//
+// HBM layout: rows [capacity][ld] in the storage dtype (f32 / f16 / bf16),
+// L2-normalised at upsert, ld = 128 * nch (zero-padded), plus norms [capacity] f32.
+//
+// Search (single / few queries) is one streaming pass over the rows:
+//   scan_topk_kernel: 16 lanes per row, 16-B loads, f32 FMA against the
+//     query held in registers, DPP reduction across the 16 lanes, then a
+//     wavefront top-k (ballot-filtered append against a running threshold +
+//     register bitonic sort) per wave, merged per block → partial keys;
+//   merge_partials_kernel: per query, top-k over all blocks' partial lists.
+// Algorithmic HBM bytes per query pass: n_rows * ld * sizeof(T).
+#include <algorithm>
+#include <vector>
+
+#include "index_common.h"
+
+namespace rc {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string &m) { g_last_error = m; }
+
+// ------------------------------------------------------- upsert / fetch --
+// One wave per vector: norm in f32, normalise, cast, scatter to its row slot.
+template <typename T>
+__global__ __launch_bounds__(256) void upsert_kernel(T *__restrict__ rows, float *__restrict__ norms, int64_t ld, int dim,
+                                                    const float *__restrict__ vecs, const int64_t *__restrict__ slot,
+                                                    int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= n) return;
+    const float *src = vecs + v * dim;
+    float ss = 0.f;
+    for (int c = lane; c < dim; c += 64) ss = fmaf(src[c], src[c], ss);
+    ss = wave_sum(ss);
+    const float nrm = sqrtf(ss);
+    const float inv = nrm > 0.f ? 1.0f / nrm : 0.f;
+    const int64_t r = slot[v];
+    T *dst = rows + r * ld;
+    for (int c = lane; c < ld; c += 64) dst[c] = Elem<T>::cast(c < dim ? src[c] * inv : 0.f);
+    if (lane == 0) norms[r] = nrm;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void fetch_kernel(const T *__restrict__ rows, const float *__restrict__ norms, int64_t ld,
+                                                   int dim, const int64_t *__restrict__ slot, int64_t n,
+                                                   float *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= n) return;
+    const int64_t r = slot[v];
+    const float nrm = norms ? norms[r] : 1.0f;
+    for (int c = lane; c < dim; c += 64) out[v * dim + c] = Elem<T>::load(rows, r * ld + c) * nrm;
+}
+
+// splitmix64 finaliser: the synthetic-row generator (reproducible in numpy).
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ float synth_value(uint64_t seed, int64_t row, int dim, int c) {
+    const uint64_t h = splitmix64(seed * 0xD1342543DE82EF95ull + (uint64_t)row * (uint64_t)dim + (uint64_t)c);
+    return (float)(int32_t)(h >> 40) * (1.0f / 8388608.0f) - 1.0f;  // 24-bit uniform in [-1, 1)
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void fill_random_kernel(T *__restrict__ rows, float *__restrict__ norms, int64_t ld,
+                                                         int dim, uint64_t seed, int64_t row0, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < n; v += nw) {
+        const int64_t r = row0 + v;
+        float ss = 0.f;
+        for (int c = lane; c < dim; c += 64) {
+            const float x = synth_value(seed, r, dim, c);
+            ss = fmaf(x, x, ss);
+        }
+        ss = wave_sum(ss);
+        const float nrm = sqrtf(ss);
+        const float inv = 1.0f / nrm;
+        T *dst = rows + r * ld;
+        for (int c = lane; c < ld; c += 64) dst[c] = Elem<T>::cast(c < dim ? synth_value(seed, r, dim, c) * inv : 0.f);
+        if (lane == 0) norms[r] = nrm;
+    }
+}
+
+// queries [nq, dim] f32 → normalised, zero-padded [nq, ld]
+// rows >= nq (padding up to a multiple of the scan's queries-per-pass) are zero.
+__global__ __launch_bounds__(64) void normalize_queries_kernel(const float *__restrict__ q, int nq, int dim, int64_t ld,
+                                                              float *__restrict__ qn) {
+    const int lane = threadIdx.x;
+    const bool valid = (int)blockIdx.x < nq;
+    const float *src = q + (int64_t)(valid ? blockIdx.x : 0) * dim;
+    float ss = 0.f;
+    for (int c = lane; c < dim; c += 64) ss = valid ? fmaf(src[c], src[c], ss) : 0.f;
+    ss = wave_sum(ss);
+    const float inv = ss > 0.f ? 1.0f / sqrtf(ss) : 0.f;
+    for (int c = lane; c < ld; c += 64) qn[(int64_t)blockIdx.x * ld + c] = (valid && c < dim) ? src[c] * inv : 0.f;
+}
+
+// One block per query: top-k over nlist sorted partial lists of k keys each.
+template <int CAP>
+__global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__restrict__ partial, int nlist,
+                                                            int nq_total, int k, int64_t row_base,
+                                                            float *__restrict__ out_scores,
+                                                            int64_t *__restrict__ out_rows) {
+    __shared__ uint64_t lds[4][CAP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qi = blockIdx.x;
+    WaveTopK<CAP> tk;
+    tk.init(as_lds(&lds[wave][0]), k);
+    const int64_t total = (int64_t)nlist * k;
+    for (int64_t j0 = (int64_t)wave * 64; j0 < total; j0 += 256) {
+        const int64_t j = j0 + lane;
+        uint64_t key = KEY_EMPTY;
+        if (j < total) {
+            const int64_t l = j / k, t = j - l * k;
+            key = partial[(l * nq_total + qi) * k + t];
+        }
+        tk.reserve(64);
+        tk.push(key != KEY_EMPTY, key);
+    }
+    tk.compact();
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < 4; ++w)
+            for (int j = 0; j < k; j += 64) {
+                const uint64_t key = (j + lane < k) ? as_lds(&lds[w][0])[j + lane] : KEY_EMPTY;
+                tk.reserve(64);
+                tk.push(key != KEY_EMPTY, key);
+            }
+        tk.compact();
+        for (int j = lane; j < k; j += 64) {
+            const uint64_t key = tk.buf[j];
+            const bool ok = key != KEY_EMPTY;
+            out_scores[(int64_t)qi * k + j] = ok ? key_score(key) : -INFINITY;
+            out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) : -1;
+        }
+    }
+}
+
+// Cross-shard merge: nlists lists of (score, row) per query, each sorted
+// (score desc, row asc), lists in ascending row-range order.  The key's low
+// word is the candidate's position l*k_in + t, which orders equal scores
+// exactly as the global row does.
+template <int CAP>
+__global__ __launch_bounds__(256) void merge_lists_kernel(const float *__restrict__ scores,
+                                                         const int64_t *__restrict__ rows, int nlists, int nq,
+                                                         int k_in, int k, float *__restrict__ out_scores,
+                                                         int64_t *__restrict__ out_rows) {
+    __shared__ uint64_t lds[4][CAP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qi = blockIdx.x;
+    WaveTopK<CAP> tk;
+    tk.init(as_lds(&lds[wave][0]), k);
+    const int64_t total = (int64_t)nlists * k_in;
+    for (int64_t j0 = (int64_t)wave * 64; j0 < total; j0 += 256) {
+        const int64_t j = j0 + lane;
+        uint64_t key = KEY_EMPTY;
+        bool ok = false;
+        if (j < total) {
+            const int64_t l = j / k_in, t = j - l * k_in;
+            const int64_t src = (l * nq + qi) * k_in + t;
+            ok = rows[src] >= 0;
+            key = make_key(scores[src], (uint32_t)j);
+        }
+        tk.reserve(64);
+        tk.push(ok, key);
+    }
+    tk.compact();
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < 4; ++w)
+            for (int j = 0; j < k; j += 64) {
+                const uint64_t key = (j + lane < k) ? as_lds(&lds[w][0])[j + lane] : KEY_EMPTY;
+                tk.reserve(64);
+                tk.push(key != KEY_EMPTY, key);
+            }
+        tk.compact();
+        for (int j = lane; j < k; j += 64) {
+            const uint64_t key = tk.buf[j];
+            const bool ok = key != KEY_EMPTY;
+            int64_t src = 0;
+            if (ok) {
+                const int64_t p = key_idx(key), l = p / k_in, t = p - l * k_in;
+                src = (l * nq + qi) * k_in + t;
+            }
+            out_scores[(int64_t)qi * k + j] = ok ? scores[src] : -INFINITY;
+            out_rows[(int64_t)qi * k + j] = ok ? rows[src] : -1;
+        }
+    }
+}
+
+}  // namespace rc
+
+// ================================================================= host ====
+using namespace rc;
+
+struct rc_index {
+    std::mutex mu;
+    int device = 0;
+    int dim = 0;
+    int dtype = RC_F32;
+    int nch = 1;  // ld = 128 * nch
+    int64_t ld = 0;
+    int64_t capacity = 0;
+    int64_t row_base = 0;
+    void *rows = nullptr;
+    float *norms = nullptr;
+    // search workspace
+    int ws_nq = 0, ws_k = 0, ws_nblk = 0;
+    float *qn = nullptr;
+    uint64_t *partial = nullptr;
+    KernelTimer timer;
+};
+
+namespace {
+
+constexpr int kNchSet[] = {1, 2, 3, 4, 6, 8, 12, 16};
+constexpr int kMaxBlocks = 2048;
+
+int pick_nch(int dim) {
+    const int need = (dim + 127) / 128;
+    for (int n : kNchSet)
+        if (n >= need) return n;
+    return -1;
+}
+
+void ensure_workspace(rc_index *h, int nq, int k) {
+    if (nq <= h->ws_nq && k <= h->ws_k) return;
+    const int nq2 = std::max(nq, h->ws_nq), k2 = std::max(k, h->ws_k);
+    dfree(h->qn);
+    dfree(h->partial);
+    h->qn = nullptr;
+    h->partial = nullptr;
+    h->qn = (float *)dmalloc((size_t)nq2 * h->ld * sizeof(float));
+    h->partial = (uint64_t *)dmalloc((size_t)kMaxBlocks * nq2 * k2 * sizeof(uint64_t));
+    h->ws_nq = nq2;
+    h->ws_k = k2;
+}
+
+template <typename T>
+void launch_upsert(rc_index *h, const float *vecs, int64_t n, const int64_t *slots, hipStream_t s) {
+    const unsigned grid = (unsigned)((n + 3) / 4);
+    hipLaunchKernelGGL(upsert_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, vecs, slots, n);
+    RC_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_fetch(rc_index *h, const int64_t *slots, int64_t n, float *out, bool stored, hipStream_t s) {
+    const unsigned grid = (unsigned)((n + 3) / 4);
+    hipLaunchKernelGGL(fetch_kernel<T>, dim3(grid), dim3(256), 0, s, (const T *)h->rows, stored ? nullptr : h->norms, h->ld,
+                       h->dim, slots, n, out);
+    RC_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_fill(rc_index *h, uint64_t seed, int64_t row0, int64_t n, hipStream_t s) {
+    const int64_t waves = (n + 0) ;
+    unsigned grid = (unsigned)std::min<int64_t>((waves + 3) / 4, 256 * 32);
+    if (grid == 0) return;
+    hipLaunchKernelGGL(fill_random_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, seed, row0, n);
+    RC_LAUNCH_CHECK();
+}
+
+void launch_scan(rc_index *h, const ScanArgs &a) {
+    switch (h->dtype) {
+        case RC_F32: return launch_scan_f32(a);
+        case RC_F16: return launch_scan_f16(a);
+        case RC_BF16: return launch_scan_bf16(a);
+        default: throw Error(RC_ERR_INVALID, "unknown dtype");
+    }
+}
+
+template <int CAP>
+void launch_merge_partials_t(rc_index *h, int nlist, int nq, int nq_stride, int k, float *scores, int64_t *rows, hipStream_t s) {
+    hipLaunchKernelGGL(merge_partials_kernel<CAP>, dim3(nq), dim3(256), 0, s, h->partial, nlist, nq_stride, k, h->row_base, scores, rows);
+    RC_LAUNCH_CHECK();
+}
+
+void launch_merge_partials(rc_index *h, int nlist, int nq, int nq_stride, int k, float *scores, int64_t *rows, hipStream_t s) {
+    const int cap = topk_cap(k);
+    if (cap <= 128) return launch_merge_partials_t<128>(h, nlist, nq, nq_stride, k, scores, rows, s);
+    if (cap <= 256) return launch_merge_partials_t<256>(h, nlist, nq, nq_stride, k, scores, rows, s);
+    return launch_merge_partials_t<512>(h, nlist, nq, nq_stride, k, scores, rows, s);
+}
+
+template <typename F>
+void dispatch_dtype(int dtype, F &&f) {
+    switch (dtype) {
+        case RC_F32: f(float{}); break;
+        case RC_F16: f(f16_t{}); break;
+        case RC_BF16: f(bf16_t{}); break;
+        default: throw Error(RC_ERR_INVALID, "unknown dtype");
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rc_last_error(void) { return g_last_error.c_str(); }
+int rc_abi_version(void) { return RC_ABI_VERSION; }
+
+int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t row_base, rc_index **out) {
+    return guard([&] {
+        RC_REQUIRE(out != nullptr, RC_ERR_INVALID, "out is NULL");
+        RC_REQUIRE(dim > 0, RC_ERR_INVALID, "dimension must be positive");
+        RC_REQUIRE(dtype == RC_F32 || dtype == RC_F16 || dtype == RC_BF16, RC_ERR_INVALID, "dtype must be RC_F32/RC_F16/RC_BF16");
+        RC_REQUIRE(capacity > 0 && capacity < (int64_t(1) << 32), RC_ERR_INVALID, "capacity must be in [1, 2^32)");
+        const int nch = pick_nch(dim);
+        RC_REQUIRE(nch > 0, RC_ERR_UNSUPPORTED, "dimension > 2048 is not supported");
+        DeviceScope ds(device);
+        auto *h = new rc_index();
+        h->device = device;
+        h->dim = dim;
+        h->dtype = dtype;
+        h->nch = nch;
+        h->ld = 128LL * nch;
+        h->capacity = capacity;
+        h->row_base = row_base;
+        try {
+            h->rows = dmalloc((size_t)capacity * h->ld * dtype_size(dtype));
+            h->norms = (float *)dmalloc((size_t)capacity * sizeof(float));
+            RC_HIP(hipMemset(h->rows, 0, (size_t)capacity * h->ld * dtype_size(dtype)));
+            RC_HIP(hipMemset(h->norms, 0, (size_t)capacity * sizeof(float)));
+            ensure_workspace(h, 4, 16);
+        } catch (...) {
+            dfree(h->rows);
+            dfree(h->norms);
+            dfree(h->qn);
+            dfree(h->partial);
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int rc_index_destroy(rc_index *h) {
+    return guard([&] {
+        if (!h) return;
+        DeviceScope ds(h->device);
+        h->timer.destroy();
+        dfree(h->rows);
+        dfree(h->norms);
+        dfree(h->qn);
+        dfree(h->partial);
+        delete h;
+    });
+}
+
+int rc_index_info(const rc_index *h, int *dim, int *dtype, int64_t *capacity, int64_t *ld) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        if (dim) *dim = h->dim;
+        if (dtype) *dtype = h->dtype;
+        if (capacity) *capacity = h->capacity;
+        if (ld) *ld = h->ld;
+    });
+}
+
+int rc_index_data(const rc_index *h, void **rows_dev, float **norms_dev) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        if (rows_dev) *rows_dev = h->rows;
+        if (norms_dev) *norms_dev = h->norms;
+    });
+}
+
+int rc_index_reserve(rc_index *h, int max_nq, int max_k) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(max_nq > 0 && max_k > 0 && max_k <= RC_TOPK_MAX, RC_ERR_INVALID, "bad reserve sizes");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        ensure_workspace(h, max_nq, max_k);
+    });
+}
+
+int rc_index_upsert(rc_index *h, const float *vecs, int64_t n, const int64_t *rows, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
+        if (n == 0) return;
+        RC_REQUIRE(vecs && rows, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        dispatch_dtype(h->dtype, [&](auto t) { launch_upsert<decltype(t)>(h, vecs, n, rows, (hipStream_t)stream); });
+    });
+}
+
+int rc_index_fetch(rc_index *h, const int64_t *rows, int64_t n, float *out, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
+        if (n == 0) return;
+        RC_REQUIRE(rows && out, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        dispatch_dtype(h->dtype, [&](auto t) { launch_fetch<decltype(t)>(h, rows, n, out, false, (hipStream_t)stream); });
+    });
+}
+
+int rc_index_fetch_stored(rc_index *h, const int64_t *rows, int64_t n, float *out, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
+        if (n == 0) return;
+        RC_REQUIRE(rows && out, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        dispatch_dtype(h->dtype, [&](auto t) { launch_fetch<decltype(t)>(h, rows, n, out, true, (hipStream_t)stream); });
+    });
+}
+
+int rc_index_fill_random(rc_index *h, uint64_t seed, int64_t row0, int64_t n, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(row0 >= 0 && n >= 0 && row0 + n <= h->capacity, RC_ERR_INVALID, "rows out of capacity");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        dispatch_dtype(h->dtype, [&](auto t) { launch_fill<decltype(t)>(h, seed, row0, n, (hipStream_t)stream); });
+    });
+}
+
+int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores, int64_t *out_rows,
+                    void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(nq >= 0, RC_ERR_INVALID, "negative query count");
+        RC_REQUIRE(k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "top_k must be in [1, 256]");
+        RC_REQUIRE(n_rows >= 0 && n_rows <= h->capacity, RC_ERR_INVALID, "n_rows out of range");
+        if (nq == 0) return;
+        RC_REQUIRE(queries && scores && out_rows, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        hipStream_t s = (hipStream_t)stream;
+        // queries per scan pass: a power of two the kernel is instantiated for (1, 2, 4)
+        int qb = 1;
+        while (qb * 2 <= std::min(nq, scan_max_qb(h->nch, k))) qb *= 2;
+        const int nq_pad = (nq + qb - 1) / qb * qb;  // every scan pass runs qb real-or-zero query slots
+        ensure_workspace(h, nq_pad, k);
+        hipLaunchKernelGGL(normalize_queries_kernel, dim3(nq_pad), dim3(64), 0, s, queries, nq, h->dim, h->ld, h->qn);
+        RC_LAUNCH_CHECK();
+        int nblk = (int)std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (n_rows + 511) / 512));
+        int64_t rpb = (n_rows + nblk - 1) / nblk;
+        rpb = ((rpb + 31) / 32) * 32;
+        if (rpb == 0) rpb = 32;
+        nblk = (int)std::max<int64_t>(1, (n_rows + rpb - 1) / rpb);
+        const double bytes = (double)n_rows * h->ld * dtype_size(h->dtype);
+        if (h->timer.enabled) h->timer.create();
+        for (int q0 = 0; q0 < nq_pad; q0 += qb) {
+            const int slot = h->timer.begin(s);
+            ScanArgs a{h->rows, h->ld, h->nch, n_rows, rpb, nblk, h->qn, q0, qb, nq_pad, k, h->partial, s};
+            launch_scan(h, a);
+            h->timer.end(slot, s, bytes);
+        }
+        launch_merge_partials(h, nblk, nq, nq_pad, k, scores, out_rows, s);
+    });
+}
+
+int rc_topk_merge(const float *scores, const int64_t *rows, int nlists, int nq, int k_in, int k, float *out_scores,
+                  int64_t *out_rows, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(nlists >= 1 && nq >= 0 && k_in >= 1 && k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "bad merge sizes");
+        RC_REQUIRE((int64_t)nlists * k_in < (int64_t(1) << 32), RC_ERR_INVALID, "too many candidates");
+        if (nq == 0) return;
+        hipStream_t s = (hipStream_t)stream;
+        const int cap = topk_cap(k);
+        if (cap <= 128)
+            hipLaunchKernelGGL(merge_lists_kernel<128>, dim3(nq), dim3(256), 0, s, scores, rows, nlists, nq, k_in, k, out_scores, out_rows);
+        else if (cap <= 256)
+            hipLaunchKernelGGL(merge_lists_kernel<256>, dim3(nq), dim3(256), 0, s, scores, rows, nlists, nq, k_in, k, out_scores, out_rows);
+        else
+            hipLaunchKernelGGL(merge_lists_kernel<512>, dim3(nq), dim3(256), 0, s, scores, rows, nlists, nq, k_in, k, out_scores, out_rows);
+        RC_LAUNCH_CHECK();
+    });
+}
+
+int rc_index_timing(rc_index *h, int enable) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        if (enable) h->timer.create();
+        h->timer.enabled = enable != 0;
+    });
+}
+
+int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *bytes) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        h->timer.flush();
+        if (total_ms) *total_ms = h->timer.total_ms;
+        if (launches) *launches = h->timer.launches;
+        if (bytes) *bytes = h->timer.work;
+        h->timer.total_ms = 0;
+        h->timer.launches = 0;
+        h->timer.work = 0;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+// index_common.h — storage dtypes and the single-query streaming scan
+// (HBM-bound GEMV + fused wavefront top-k) of the exact cosine index.
+// The scan is instantiated per storage dtype in scan_{f32,f16,bf16}.hip so
+// the three translation units compile in parallel.
+#pragma once
+
+#include "rc_common.h"
+#include "topk.h"
+
+namespace rc {
+
+struct f16_t { uint16_t b; };
+struct bf16_t { uint16_t b; };
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+    __device__ static float load(const float *p, int64_t i) { return p[i]; }
+    __device__ static float cast(float x) { return x; }
+};
+template <> struct Elem<f16_t> {
+    __device__ static float load(const f16_t *p, int64_t i) { return f16_to_f32(p[i].b); }
+    __device__ static f16_t cast(float x) { return f16_t{f32_to_f16(x)}; }
+};
+template <> struct Elem<bf16_t> {
+    __device__ static float load(const bf16_t *p, int64_t i) { return bf16_to_f32(p[i].b); }
+    __device__ static bf16_t cast(float x) { return bf16_t{f32_to_bf16(x)}; }
+};
+
+inline size_t dtype_size(int dtype) { return dtype == RC_F32 ? 4 : 2; }
+
+// unpack one 16-B chunk into its 4 (f32) or 8 (f16/bf16) values
+template <typename T>
+__device__ __forceinline__ void unpack16(const uint4 &x, float *out);
+template <>
+__device__ __forceinline__ void unpack16<float>(const uint4 &x, float *o) {
+    o[0] = __uint_as_float(x.x);
+    o[1] = __uint_as_float(x.y);
+    o[2] = __uint_as_float(x.z);
+    o[3] = __uint_as_float(x.w);
+}
+template <>
+__device__ __forceinline__ void unpack16<f16_t>(const uint4 &x, float *o) {
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = f16_to_f32((uint16_t)(w[i] & 0xffffu));
+        o[2 * i + 1] = f16_to_f32((uint16_t)(w[i] >> 16));
+    }
+}
+template <>
+__device__ __forceinline__ void unpack16<bf16_t>(const uint4 &x, float *o) {
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+
+inline int topk_cap(int k) {
+    int kp = 16;
+    while (kp < k) kp <<= 1;
+    return kp * 2 < 128 ? 128 : kp * 2;
+}
+
+struct ScanArgs {
+    const void *rows;
+    int64_t ld;
+    int nch;
+    int64_t n_rows;
+    int64_t rows_per_block;
+    int nblk;
+    const float *qn;
+    int q0;
+    int qb;
+    int nq_total;
+    int k;
+    uint64_t *partial;
+    hipStream_t stream;
+};
+
+// largest queries-per-pass for a row width: query registers per lane = QB*nch*8 floats <= 64
+inline int scan_max_qb(int nch, int k) {
+    if (k > 128) return 1;
+    return nch <= 2 ? 4 : (nch <= 4 ? 2 : 1);
+}
+
+void launch_scan_f32(const ScanArgs &a);
+void launch_scan_f16(const ScanArgs &a);
+void launch_scan_bf16(const ScanArgs &a);
+
+#if defined(SCAN_INSTANTIATE)
+// qn holds nq_total (a multiple of QB) query rows, zero beyond the caller's
+// queries, so every slot is computed and stored unconditionally.
+// Block = 4 waves over a contiguous row range.  Lane = (row-in-group rg = lane>>4,
+// position sub = lane&15); 16-B chunk j = sub + 16 i of a row holds elements
+// [j*EPC, (j+1)*EPC).  SCAN_U row-groups are loaded before any is consumed.
+constexpr int SCAN_U = 2;
+
+template <typename T, int NCH, int QB, int CAP>
+__global__ __launch_bounds__(256) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
+                                                       int64_t rows_per_block, const float *__restrict__ qn, int q0,
+                                                       int nq_total, int k, uint64_t *__restrict__ partial) {
+    constexpr int EPC = 16 / sizeof(T);
+    constexpr int CPL = NCH * 128 / (16 * EPC);
+    __shared__ uint64_t lds[4][QB][CAP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 15, rg = lane >> 4;
+
+    float q[QB][CPL][EPC];
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int i = 0; i < CPL; ++i)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                q[b][i][e] = qn[(int64_t)(q0 + b) * ld + (sub + 16 * i) * EPC + e];
+            }
+
+    WaveTopK<CAP> tk[QB];
+    static_for<QB>([&](auto bc) { tk[bc.value].init(as_lds(&lds[wave][bc.value][0]), k); });
+
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(n_rows, r0 + rows_per_block);
+    const uint4 *base4 = reinterpret_cast<const uint4 *>(rows);
+    const int64_t ld4 = ld / EPC;  // row stride in 16-B chunks
+
+    for (int64_t g = r0 + wave * 4 * SCAN_U; g < r1; g += 16 * SCAN_U) {
+        uint4 x[SCAN_U][CPL];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; ++u) {
+            const int64_t r = g + u * 4 + rg;
+            const int64_t rr = r < r1 ? r : r0;  // clamp to a valid row; result discarded below
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) x[u][i] = base4[rr * ld4 + sub + 16 * i];
+        }
+#pragma unroll
+        for (int u = 0; u < SCAN_U; ++u) {
+            const int64_t r = g + u * 4 + rg;
+            float acc[QB];
+#pragma unroll
+            for (int b = 0; b < QB; ++b) acc[b] = 0.f;
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) {
+                float f[EPC];
+                unpack16<T>(x[u][i], f);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e)
+#pragma unroll
+                    for (int b = 0; b < QB; ++b) acc[b] = fmaf(f[e], q[b][i][e], acc[b]);
+            }
+            static_for<QB>([&](auto bc) {
+                constexpr int b = bc.value;
+                const float s = sum16(acc[b]);
+                tk[b].reserve(4);
+                tk[b].push(sub == 0 && r < r1, make_key(s, (uint32_t)r));
+            });
+        }
+    }
+
+    // per-wave final selection, then wave 0 merges the other three waves' lists
+    static_for<QB>([&](auto bc) { tk[bc.value].compact(); });
+    __syncthreads();
+    if (wave == 0) {
+        static_for<QB>([&](auto bc) {
+            constexpr int b = bc.value;
+            const int qi = q0 + b;
+            for (int w = 1; w < 4; ++w) {
+                const lds_u64 *src = as_lds(&lds[w][b][0]);
+                for (int j = 0; j < k; j += 64) {
+                    const uint64_t key = (j + lane < k) ? src[j + lane] : KEY_EMPTY;
+                    tk[b].reserve(64);
+                    tk[b].push(key != KEY_EMPTY, key);
+                }
+            }
+            tk[b].compact();
+            uint64_t *dst = partial + ((int64_t)blockIdx.x * nq_total + qi) * k;
+            for (int j = lane; j < k; j += 64) dst[j] = tk[b].buf[j];
+        });
+    }
+}
+
+template <typename T, int NCH, int QB, int CAP>
+void launch_scan_t(const ScanArgs &a) {
+    hipLaunchKernelGGL((scan_topk_kernel<T, NCH, QB, CAP>), dim3(a.nblk), dim3(256), 0, a.stream, (const T *)a.rows, a.ld,
+                       a.n_rows, a.rows_per_block, a.qn, a.q0, a.nq_total, a.k, a.partial);
+    RC_LAUNCH_CHECK();
+}
+
+template <typename T, int NCH, int QB>
+void launch_scan_cap(const ScanArgs &a) {
+    const int cap = topk_cap(a.k);
+    if (cap <= 128) return launch_scan_t<T, NCH, QB, 128>(a);
+    if (cap <= 256) return launch_scan_t<T, NCH, QB, 256>(a);
+    if constexpr (QB == 1) return launch_scan_t<T, NCH, QB, 512>(a);
+    throw Error(RC_ERR_UNSUPPORTED, "multi-query pass needs k <= 128");
+}
+
+template <typename T, int NCH>
+void launch_scan_qb(const ScanArgs &a) {
+    if constexpr (NCH <= 2) {
+        if (a.qb == 4) return launch_scan_cap<T, NCH, 4>(a);
+    }
+    if constexpr (NCH <= 4) {
+        if (a.qb == 2) return launch_scan_cap<T, NCH, 2>(a);
+    }
+    if (a.qb == 1) return launch_scan_cap<T, NCH, 1>(a);
+    throw Error(RC_ERR_INVALID, "internal: no scan instantiation for this queries-per-pass");
+}
+
+template <typename T>
+void launch_scan_dtype(const ScanArgs &a) {
+    switch (a.nch) {
+        case 1: return launch_scan_qb<T, 1>(a);
+        case 2: return launch_scan_qb<T, 2>(a);
+        case 3: return launch_scan_qb<T, 3>(a);
+        case 4: return launch_scan_qb<T, 4>(a);
+        case 6: return launch_scan_qb<T, 6>(a);
+        case 8: return launch_scan_qb<T, 8>(a);
+        case 12: return launch_scan_qb<T, 12>(a);
+        case 16: return launch_scan_qb<T, 16>(a);
+        default: throw Error(RC_ERR_UNSUPPORTED, "unsupported row width");
+    }
+}
+#endif  // SCAN_INSTANTIATE
+
+}  // namespace rc

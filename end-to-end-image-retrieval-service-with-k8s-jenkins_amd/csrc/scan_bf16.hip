@@ -1,0 +1,7 @@
+// scan_bf16.hip — instantiates the streaming scan + top-k for bf16 index rows.
+#define SCAN_INSTANTIATE 1
+#include "index_common.h"
+
+namespace rc {
+void launch_scan_bf16(const ScanArgs &a) { launch_scan_dtype<bf16_t>(a); }
+}  // namespace rc

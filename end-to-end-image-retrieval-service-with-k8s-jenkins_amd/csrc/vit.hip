@@ -1,0 +1,553 @@
+// vit.hip — ViT-MSN embedding model: weights, workspace and the launch sequence
+// behind rc_embed (replaces embedding/main.py:97-114's ViTImageProcessor +
+// ViTMSNModel + CLS extraction).
+//
+// HBM layout per model (bf16 GEMM operands, f32 residual stream):
+//   weights   W_qkv [3H][H] (q,k,v rows concatenated), W_o [H][H], W_fc1 [MLP][H],
+//             W_fc2 [H][MLP], W_patch [H][3*P*P] — bf16, nn.Linear [out][in];
+//             biases / LayerNorm params / cls / pos — f32
+//   workspace (sized for max_batch images, rows padded to the GEMM tile):
+//             patches bf16 [Pp][3P²], hidden f32 [Mp][H], ln bf16 [Mp][H],
+//             qkv bf16 [Mp][3H], attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "vit_kernels.h"
+
+using namespace rc;
+
+namespace {
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// ---------------------------------------------- Pillow resample coefficients
+// Restates libImaging/Resample.c precompute_coeffs + normalize_coeffs_8bpc
+// (the same algorithm oracle/pil_resample.py pins against Pillow).
+struct ResampleCoeffs {
+    int ksize = 0;
+    std::vector<int> bounds;  // [out][2] = (xmin, xcount)
+    std::vector<int> coef;    // [out][ksize] fixed point, 22 fractional bits
+};
+
+double bicubic_filter(double x) {
+    const double a = -0.5;
+    if (x < 0.0) x = -x;
+    if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1.0;
+    if (x < 2.0) return (((x - 5.0) * x + 8.0) * x - 4.0) * a;
+    return 0.0;
+}
+double bilinear_filter(double x) {
+    if (x < 0.0) x = -x;
+    if (x < 1.0) return 1.0 - x;
+    return 0.0;
+}
+
+ResampleCoeffs precompute_coeffs(int in_size, int out_size, int resample) {
+    double (*filt)(double) = resample == RC_RESAMPLE_BICUBIC ? bicubic_filter : bilinear_filter;
+    const double fsupport = resample == RC_RESAMPLE_BICUBIC ? 2.0 : 1.0;
+    const double in0 = 0.0, in1 = (double)in_size;
+    const double scale = (in1 - in0) / out_size;
+    const double filterscale = scale < 1.0 ? 1.0 : scale;
+    const double support = fsupport * filterscale;
+    ResampleCoeffs r;
+    r.ksize = (int)std::ceil(support) * 2 + 1;
+    r.bounds.assign(2 * out_size, 0);
+    r.coef.assign((size_t)out_size * r.ksize, 0);
+    std::vector<double> k(r.ksize);
+    const double ss = 1.0 / filterscale;
+    for (int xx = 0; xx < out_size; ++xx) {
+        const double center = in0 + (xx + 0.5) * scale;
+        int xmin = (int)(center - support + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xmax = (int)(center + support + 0.5);
+        if (xmax > in_size) xmax = in_size;
+        xmax -= xmin;
+        double ww = 0.0;
+        for (int x = 0; x < xmax; ++x) {
+            const double w = filt((x + xmin - center + 0.5) * ss);
+            k[x] = w;
+            ww += w;
+        }
+        for (int x = 0; x < xmax; ++x) {
+            if (ww != 0.0) k[x] /= ww;
+        }
+        for (int x = 0; x < r.ksize; ++x) {
+            const double v = x < xmax ? k[x] : 0.0;
+            r.coef[(size_t)xx * r.ksize + x] = v < 0 ? (int)(-0.5 + v * (1 << 22)) : (int)(0.5 + v * (1 << 22));
+        }
+        r.bounds[2 * xx] = xmin;
+        r.bounds[2 * xx + 1] = xmax;
+    }
+    return r;
+}
+
+struct DeviceCoeffs {
+    int ksize = 0;
+    int *bounds = nullptr;
+    int *coef = nullptr;
+    int first = 0, last = 0;  // used source range [first, last)
+};
+
+struct Layer {
+    uint16_t *w_qkv = nullptr, *w_o = nullptr, *w_fc1 = nullptr, *w_fc2 = nullptr;
+    float *b_qkv = nullptr, *b_o = nullptr, *b_fc1 = nullptr, *b_fc2 = nullptr;
+    float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+};
+
+enum TimerId { T_GEMM = 0, T_FC1 = 1, T_ATTN = 2, T_LN = 3, T_PRE = 4, T_COUNT = 5 };
+
+}  // namespace
+
+struct rc_model {
+    std::mutex mu;
+    int device = 0;
+    rc_vit_config cfg{};
+    int tokens = 0, npatch = 0, kpatch = 0;
+    std::map<std::string, std::vector<int64_t>> shapes;  // expected tensors
+    std::map<std::string, std::vector<float>> host;      // staged until finalize
+    bool ready = false;
+    std::vector<void *> allocs;
+    // device weights
+    uint16_t *w_patch = nullptr;
+    float *b_patch = nullptr, *cls = nullptr, *pos = nullptr, *lnf_w = nullptr, *lnf_b = nullptr;
+    std::vector<Layer> layers;
+    // preprocessing
+    int resample = RC_RESAMPLE_BICUBIC;
+    double rescale = 1.0 / 255.0;
+    float mean[3] = {0.485f, 0.456f, 0.406f}, std_[3] = {0.229f, 0.224f, 0.225f};
+    float *lut = nullptr;
+    std::map<std::pair<int, int>, DeviceCoeffs> coeff_cache;  // (in, out) → coeffs
+    // workspace
+    int Mp = 0, Pp = 0;
+    uint16_t *patches = nullptr, *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
+    float *hidden = nullptr;
+    uint8_t *resized = nullptr, *resize_tmp = nullptr;
+    size_t resize_tmp_bytes = 0;
+    KernelTimer timers[T_COUNT];
+
+    void *alloc(size_t bytes) {
+        void *p = dmalloc(bytes);
+        allocs.push_back(p);
+        return p;
+    }
+    ~rc_model() {
+        for (auto &t : timers) t.destroy();
+        for (void *p : allocs) dfree(p);
+        dfree(resize_tmp);
+    }
+};
+
+namespace {
+
+std::string canonical_name(std::string n) {
+    if (n.rfind("vit.", 0) == 0) n = n.substr(4);
+    if (n.rfind("layers.", 0) == 0) n = "encoder.layer." + n.substr(7);
+    const std::pair<const char *, const char *> ren[] = {
+        {"attention.q_proj", "attention.attention.query"}, {"attention.k_proj", "attention.attention.key"},
+        {"attention.v_proj", "attention.attention.value"}, {"attention.o_proj", "attention.output.dense"},
+        {"mlp.fc1", "intermediate.dense"},                 {"mlp.fc2", "output.dense"},
+    };
+    for (auto &r : ren) {
+        const size_t p = n.find(r.first);
+        if (p != std::string::npos) {
+            n.replace(p, std::strlen(r.first), r.second);
+            break;
+        }
+    }
+    return n;
+}
+
+void build_shapes(rc_model *m) {
+    const auto &c = m->cfg;
+    const int64_t H = c.hidden, F = c.mlp;
+    auto &s = m->shapes;
+    s["embeddings.cls_token"] = {1, 1, H};
+    s["embeddings.position_embeddings"] = {1, m->tokens, H};
+    s["embeddings.patch_embeddings.projection.weight"] = {H, 3, c.patch, c.patch};
+    s["embeddings.patch_embeddings.projection.bias"] = {H};
+    for (int i = 0; i < c.layers; ++i) {
+        const std::string p = "encoder.layer." + std::to_string(i) + ".";
+        for (const char *nm : {"query", "key", "value"}) {
+            s[p + "attention.attention." + nm + ".weight"] = {H, H};
+            s[p + "attention.attention." + nm + ".bias"] = {H};
+        }
+        s[p + "attention.output.dense.weight"] = {H, H};
+        s[p + "attention.output.dense.bias"] = {H};
+        s[p + "intermediate.dense.weight"] = {F, H};
+        s[p + "intermediate.dense.bias"] = {F};
+        s[p + "output.dense.weight"] = {H, F};
+        s[p + "output.dense.bias"] = {H};
+        for (const char *nm : {"layernorm_before", "layernorm_after"}) {
+            s[p + nm + ".weight"] = {H};
+            s[p + nm + ".bias"] = {H};
+        }
+    }
+    s["layernorm.weight"] = {H};
+    s["layernorm.bias"] = {H};
+}
+
+int64_t numel_of(const std::vector<int64_t> &sh) {
+    int64_t n = 1;
+    for (auto d : sh) n *= d;
+    return n;
+}
+
+float *upload_f32(rc_model *m, const std::vector<float> &v) {
+    float *d = (float *)m->alloc(v.size() * sizeof(float));
+    RC_HIP(hipMemcpy(d, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+    return d;
+}
+
+uint16_t *upload_bf16(rc_model *m, const std::vector<const std::vector<float> *> &parts) {
+    size_t n = 0;
+    for (auto *p : parts) n += p->size();
+    std::vector<uint16_t> h(n);
+    size_t o = 0;
+    for (auto *p : parts)
+        for (float f : *p) h[o++] = host_f2bf(f);
+    uint16_t *d = (uint16_t *)m->alloc(n * sizeof(uint16_t));
+    RC_HIP(hipMemcpy(d, h.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice));
+    return d;
+}
+
+void build_lut(rc_model *m) {
+    float h[3 * 256];
+    for (int c = 0; c < 3; ++c)
+        for (int u = 0; u < 256; ++u) {
+            // transformers rescale: u8 -> f64 * factor -> f32; normalize in f32: (x - mean) / std
+            const float x = (float)((double)u * m->rescale);
+            h[c * 256 + u] = (x - m->mean[c]) / m->std_[c];
+        }
+    if (!m->lut) m->lut = (float *)m->alloc(sizeof(h));
+    RC_HIP(hipMemcpy(m->lut, h, sizeof(h), hipMemcpyHostToDevice));
+}
+
+const DeviceCoeffs &get_coeffs(rc_model *m, int in_size, int out_size) {
+    auto key = std::make_pair(in_size * 8 + m->resample, out_size);
+    auto it = m->coeff_cache.find(key);
+    if (it != m->coeff_cache.end()) return it->second;
+    ResampleCoeffs c = precompute_coeffs(in_size, out_size, m->resample);
+    DeviceCoeffs d;
+    d.ksize = c.ksize;
+    d.bounds = (int *)m->alloc(c.bounds.size() * sizeof(int));
+    d.coef = (int *)m->alloc(c.coef.size() * sizeof(int));
+    RC_HIP(hipMemcpy(d.bounds, c.bounds.data(), c.bounds.size() * sizeof(int), hipMemcpyHostToDevice));
+    RC_HIP(hipMemcpy(d.coef, c.coef.data(), c.coef.size() * sizeof(int), hipMemcpyHostToDevice));
+    d.first = c.bounds[0];
+    d.last = c.bounds[2 * (out_size - 1)] + c.bounds[2 * (out_size - 1) + 1];
+    return m->coeff_cache.emplace(key, d).first->second;
+}
+
+unsigned grid_for(int64_t work, int per_block = 256) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + per_block - 1) / per_block, 256 * 16));
+}
+
+// Pillow-exact resize of n images (h, w) → (S, S) into m->resized; returns the source to use.
+// As ImagingResampleInner: a pass runs only if its axis changes; the horizontal
+// pass covers just the source rows the vertical pass reads, whose bounds are then
+// taken relative to the first of them.
+const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, int w, hipStream_t s) {
+    const int S = m->cfg.image_size;
+    if (h == S && w == S) return images;
+    const bool need_h = w != S, need_v = h != S;
+    const DeviceCoeffs &cv = get_coeffs(m, h, S);
+    const DeviceCoeffs &ch = get_coeffs(m, w, S);
+    const uint8_t *cur = images;
+    int cur_h = h;
+    if (need_h) {
+        const int y0 = need_v ? cv.first : 0, Hs = need_v ? cv.last - cv.first : h;
+        const size_t bytes = (size_t)n * Hs * S * 3;
+        if (bytes > m->resize_tmp_bytes) {
+            RC_HIP(hipStreamSynchronize(s));
+            dfree(m->resize_tmp);
+            m->resize_tmp = nullptr;
+            m->resize_tmp = (uint8_t *)dmalloc(bytes);
+            m->resize_tmp_bytes = bytes;
+        }
+        hipLaunchKernelGGL(resize_h_kernel, dim3(grid_for((int64_t)n * Hs * S)), dim3(256), 0, s, images, h, w, y0, Hs,
+                           m->resize_tmp, S, ch.bounds, ch.coef, ch.ksize, n);
+        RC_LAUNCH_CHECK();
+        cur = m->resize_tmp;
+        cur_h = Hs;
+        if (!need_v) {
+            RC_HIP(hipMemcpyAsync(m->resized, cur, (size_t)n * S * S * 3, hipMemcpyDeviceToDevice, s));
+            return m->resized;
+        }
+    }
+    const int *vb = cv.bounds;
+    if (need_h && cv.first != 0) {
+        auto key = std::make_pair(-(h * 8 + m->resample), S);  // shifted copy of the vertical bounds
+        auto it = m->coeff_cache.find(key);
+        if (it == m->coeff_cache.end()) {
+            ResampleCoeffs c = precompute_coeffs(h, S, m->resample);
+            for (int i = 0; i < S; ++i) c.bounds[2 * i] -= cv.first;
+            DeviceCoeffs d = cv;
+            d.bounds = (int *)m->alloc(c.bounds.size() * sizeof(int));
+            RC_HIP(hipMemcpy(d.bounds, c.bounds.data(), c.bounds.size() * sizeof(int), hipMemcpyHostToDevice));
+            it = m->coeff_cache.emplace(key, d).first;
+        }
+        vb = it->second.bounds;
+    }
+    const int cur_w = need_h ? S : w;
+    hipLaunchKernelGGL(resize_v_kernel, dim3(grid_for((int64_t)n * S * cur_w)), dim3(256), 0, s, cur, cur_h, cur_w,
+                       m->resized, S, vb, cv.coef, cv.ksize, n);
+    RC_LAUNCH_CHECK();
+    return m->resized;
+}
+
+template <int EPI>
+void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, bool fc1 = false) {
+    RC_REQUIRE(a.N % GEMM_BN == 0 && a.K % GEMM_BK == 0, RC_ERR_UNSUPPORTED, "GEMM shape not tile aligned");
+    const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
+    const double flops = 2.0 * a.M * a.N * a.K;
+    const int t0 = m->timers[T_GEMM].begin(s);
+    const int t1 = fc1 ? m->timers[T_FC1].begin(s) : -1;
+    hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
+    RC_LAUNCH_CHECK();
+    if (fc1) m->timers[T_FC1].end(t1, s, flops);
+    m->timers[T_GEMM].end(t0, s, flops);
+}
+
+void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint16_t *y, int M, hipStream_t s) {
+    const int t = m->timers[T_LN].begin(s);
+    hipLaunchKernelGGL(layernorm_kernel<3>, dim3((M + 3) / 4), dim3(256), 0, s, x, g, b, y, M, m->cfg.ln_eps);
+    RC_LAUNCH_CHECK();
+    m->timers[T_LN].end(t, s, (double)M * m->cfg.hidden * 6.0);
+}
+
+void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw, float *normed, hipStream_t s) {
+    const auto &c = m->cfg;
+    const int H = c.hidden, T = m->tokens, M = n * T;
+    const int S = c.image_size;
+    // 1. preprocess: resize (if needed) + rescale/normalize/im2col → bf16 patches
+    const int tp = m->timers[T_PRE].begin(s);
+    const uint8_t *src = resize_batch(m, images, n, h, w, s);
+    hipLaunchKernelGGL(patchify_kernel<16>, dim3(grid_for((int64_t)n * m->npatch * (m->kpatch / 8))), dim3(256), 0, s, src,
+                       m->lut, m->patches, n, S);
+    RC_LAUNCH_CHECK();
+    m->timers[T_PRE].end(tp, s, (double)n * S * S * 3 + (double)n * m->npatch * m->kpatch * 2);
+    // 2. embeddings: CLS + pos, patch GEMM (+bias +pos) into the residual stream
+    hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, m->hidden, T, H, m->cls, m->pos);
+    RC_LAUNCH_CHECK();
+    {
+        GemmArgs a{m->patches, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, m->hidden, m->pos, T};
+        gemm<EPI_PATCH_F32>(m, a, s);
+    }
+    // 3. encoder layers
+    const float scale = 1.0f / std::sqrt((float)(H / c.heads));
+    for (int l = 0; l < c.layers; ++l) {
+        const Layer &L = m->layers[l];
+        layernorm(m, m->hidden, L.ln1_w, L.ln1_b, m->ln, M, s);
+        gemm<EPI_BF16>(m, GemmArgs{m->ln, L.w_qkv, L.b_qkv, M, 3 * H, H, m->qkv, nullptr, nullptr, T}, s);
+        const int ta = m->timers[T_ATTN].begin(s);
+        hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, m->qkv, m->attn, T, c.heads, scale);
+        RC_LAUNCH_CHECK();
+        m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
+        gemm<EPI_RESID_F32>(m, GemmArgs{m->attn, L.w_o, L.b_o, M, H, H, nullptr, m->hidden, nullptr, T}, s);
+        layernorm(m, m->hidden, L.ln2_w, L.ln2_b, m->ln, M, s);
+        gemm<EPI_GELU_BF16>(m, GemmArgs{m->ln, L.w_fc1, L.b_fc1, M, c.mlp, H, m->mlp, nullptr, nullptr, T}, s, true);
+        gemm<EPI_RESID_F32>(m, GemmArgs{m->mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, m->hidden, nullptr, T}, s);
+    }
+    // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
+    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, m->hidden, T, m->lnf_w, m->lnf_b, c.ln_eps, raw, normed);
+    RC_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
+    return guard([&] {
+        RC_REQUIRE(cfg && out, RC_ERR_INVALID, "null argument");
+        RC_REQUIRE(cfg->hidden == 768 && cfg->patch == 16 && cfg->heads * 64 == cfg->hidden, RC_ERR_UNSUPPORTED,
+                   "this build implements ViT-B/16 geometry (hidden 768, patch 16, head dim 64)");
+        RC_REQUIRE(cfg->image_size % cfg->patch == 0 && cfg->image_size <= 224, RC_ERR_UNSUPPORTED,
+                   "image_size must be a multiple of 16 and <= 224 (tokens <= 224)");
+        RC_REQUIRE(cfg->mlp % GEMM_BN == 0 && cfg->layers >= 1 && cfg->max_batch >= 1, RC_ERR_INVALID, "bad config");
+        DeviceScope ds(device);
+        auto *m = new rc_model();
+        try {
+            m->device = device;
+            m->cfg = *cfg;
+            m->npatch = (cfg->image_size / cfg->patch) * (cfg->image_size / cfg->patch);
+            m->tokens = m->npatch + 1;
+            m->kpatch = 3 * cfg->patch * cfg->patch;
+            build_shapes(m);
+            const int B = cfg->max_batch, H = cfg->hidden;
+            m->Mp = round_up(B * m->tokens, GEMM_BM);
+            m->Pp = round_up(B * m->npatch, GEMM_BM);
+            m->patches = (uint16_t *)m->alloc((size_t)m->Pp * m->kpatch * 2);
+            m->hidden = (float *)m->alloc((size_t)m->Mp * H * 4);
+            m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
+            m->qkv = (uint16_t *)m->alloc((size_t)m->Mp * 3 * H * 2);
+            m->attn = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
+            m->mlp = (uint16_t *)m->alloc((size_t)m->Mp * cfg->mlp * 2);
+            m->resized = (uint8_t *)m->alloc((size_t)B * cfg->image_size * cfg->image_size * 3);
+            // pad rows are read by the GEMM tiles: keep them finite (zero) forever
+            RC_HIP(hipMemset(m->patches, 0, (size_t)m->Pp * m->kpatch * 2));
+            RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
+            RC_HIP(hipMemset(m->ln, 0, (size_t)m->Mp * H * 2));
+            RC_HIP(hipMemset(m->qkv, 0, (size_t)m->Mp * 3 * H * 2));
+            RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
+            RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));
+            build_lut(m);
+        } catch (...) {
+            delete m;
+            throw;
+        }
+        *out = m;
+    });
+}
+
+int rc_model_destroy(rc_model *m) {
+    return guard([&] {
+        if (!m) return;
+        DeviceScope ds(m->device);
+        delete m;
+    });
+}
+
+int rc_model_set_weight(rc_model *m, const char *name, const float *host_data, int64_t numel) {
+    return guard([&] {
+        RC_REQUIRE(m && name && host_data, RC_ERR_INVALID, "null argument");
+        std::lock_guard<std::mutex> lk(m->mu);
+        const std::string key = canonical_name(name);
+        auto it = m->shapes.find(key);
+        RC_REQUIRE(it != m->shapes.end(), RC_ERR_INVALID, std::string("unknown weight name: ") + name);
+        RC_REQUIRE(numel == numel_of(it->second), RC_ERR_INVALID,
+                   std::string("size mismatch for ") + name + ": expected " + std::to_string(numel_of(it->second)));
+        m->host[key].assign(host_data, host_data + numel);
+        m->ready = false;
+    });
+}
+
+int rc_model_set_preprocess(rc_model *m, int resample, double rescale_factor, const float mean[3], const float std_[3]) {
+    return guard([&] {
+        RC_REQUIRE(m && mean && std_, RC_ERR_INVALID, "null argument");
+        RC_REQUIRE(resample == RC_RESAMPLE_BICUBIC || resample == RC_RESAMPLE_BILINEAR, RC_ERR_UNSUPPORTED,
+                   "resample must be BICUBIC (3) or BILINEAR (2)");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        m->resample = resample;
+        m->rescale = rescale_factor;
+        for (int c = 0; c < 3; ++c) {
+            m->mean[c] = mean[c];
+            m->std_[c] = std_[c];
+        }
+        build_lut(m);
+    });
+}
+
+int rc_model_finalize(rc_model *m) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        for (auto &kv : m->shapes)
+            RC_REQUIRE(m->host.count(kv.first), RC_ERR_STATE, "weight not set: " + kv.first);
+        auto &h = m->host;
+        m->w_patch = upload_bf16(m, {&h["embeddings.patch_embeddings.projection.weight"]});
+        m->b_patch = upload_f32(m, h["embeddings.patch_embeddings.projection.bias"]);
+        m->cls = upload_f32(m, h["embeddings.cls_token"]);
+        m->pos = upload_f32(m, h["embeddings.position_embeddings"]);
+        m->lnf_w = upload_f32(m, h["layernorm.weight"]);
+        m->lnf_b = upload_f32(m, h["layernorm.bias"]);
+        m->layers.assign(m->cfg.layers, Layer{});
+        for (int i = 0; i < m->cfg.layers; ++i) {
+            const std::string p = "encoder.layer." + std::to_string(i) + ".";
+            Layer &L = m->layers[i];
+            L.w_qkv = upload_bf16(m, {&h[p + "attention.attention.query.weight"], &h[p + "attention.attention.key.weight"],
+                                      &h[p + "attention.attention.value.weight"]});
+            std::vector<float> bqkv;
+            for (const char *nm : {"query", "key", "value"}) {
+                const auto &b = h[p + "attention.attention." + nm + ".bias"];
+                bqkv.insert(bqkv.end(), b.begin(), b.end());
+            }
+            L.b_qkv = upload_f32(m, bqkv);
+            L.w_o = upload_bf16(m, {&h[p + "attention.output.dense.weight"]});
+            L.b_o = upload_f32(m, h[p + "attention.output.dense.bias"]);
+            L.w_fc1 = upload_bf16(m, {&h[p + "intermediate.dense.weight"]});
+            L.b_fc1 = upload_f32(m, h[p + "intermediate.dense.bias"]);
+            L.w_fc2 = upload_bf16(m, {&h[p + "output.dense.weight"]});
+            L.b_fc2 = upload_f32(m, h[p + "output.dense.bias"]);
+            L.ln1_w = upload_f32(m, h[p + "layernorm_before.weight"]);
+            L.ln1_b = upload_f32(m, h[p + "layernorm_before.bias"]);
+            L.ln2_w = upload_f32(m, h[p + "layernorm_after.weight"]);
+            L.ln2_b = upload_f32(m, h[p + "layernorm_after.bias"]);
+        }
+        m->host.clear();
+        m->ready = true;
+    });
+}
+
+int rc_embed(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw_out, float *normed_out, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        RC_REQUIRE(n >= 0 && n <= m->cfg.max_batch, RC_ERR_INVALID, "batch size exceeds max_batch");
+        RC_REQUIRE(h > 0 && w > 0, RC_ERR_INVALID, "image height/width must be positive");
+        if (n == 0) return;
+        RC_REQUIRE(images && raw_out, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(m->mu);
+        RC_REQUIRE(m->ready, RC_ERR_STATE, "model weights not finalized");
+        DeviceScope ds(m->device);
+        forward(m, images, n, h, w, raw_out, normed_out, (hipStream_t)stream);
+    });
+}
+
+int rc_preprocess(rc_model *m, const uint8_t *images, int n, int h, int w, float *pixel_values, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        RC_REQUIRE(n >= 0 && n <= m->cfg.max_batch && h > 0 && w > 0, RC_ERR_INVALID, "bad batch/shape");
+        if (n == 0) return;
+        RC_REQUIRE(images && pixel_values, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        hipStream_t s = (hipStream_t)stream;
+        const int S = m->cfg.image_size;
+        const uint8_t *src = resize_batch(m, images, n, h, w, s);
+        hipLaunchKernelGGL(pixel_values_kernel, dim3(grid_for((int64_t)n * 3 * S * S)), dim3(256), 0, s, src, m->lut,
+                           pixel_values, n, S);
+        RC_LAUNCH_CHECK();
+    });
+}
+
+int rc_model_timing(rc_model *m, int enable) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        for (auto &t : m->timers) {
+            if (enable) t.create();
+            t.enabled = enable != 0;
+        }
+    });
+}
+
+int rc_model_timing_read(rc_model *m, int kernel_id, double *total_ms, int64_t *launches, double *flops) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        RC_REQUIRE(kernel_id >= 0 && kernel_id < T_COUNT, RC_ERR_INVALID, "bad kernel id");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        auto &t = m->timers[kernel_id];
+        t.flush();
+        if (total_ms) *total_ms = t.total_ms;
+        if (launches) *launches = t.launches;
+        if (flops) *flops = t.work;
+    });
+}
+
+int rc_model_timing_reset(rc_model *m) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        for (auto &t : m->timers) t.reset();
+    });
+}
+
+}  // extern "C"

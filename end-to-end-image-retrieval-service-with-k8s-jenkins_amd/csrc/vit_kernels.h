@@ -1,0 +1,462 @@
+// vit_kernels.h — device kernels of the ViT-MSN embedding path (gfx950).
+//
+// Reference arithmetic (transformers models/vit_msn/modeling_vit_msn.py, called
+// from embedding/main.py:111-113):
+//   patch embed Conv2d(3,768,16,16) (:57)  → gemm_bf16_kernel<EPI_PATCH_F32> on an
+//                                            im2col'd A built by patchify_kernel
+//   q/k/v/o, fc1, fc2 nn.Linear (:199-202,243-244) → gemm_bf16_kernel (bias / GELU /
+//                                            residual epilogues fused)
+//   LayerNorm eps 1e-6 (:258-259,327)      → layernorm_kernel (f32 in, bf16 out)
+//   eager attention, scale 1/8, fp32 softmax (:161-186) → attention_kernel
+//   last_hidden_state[:,0,:] (main.py:113) → cls_final_kernel (final LN on the
+//                                            CLS rows, raw + L2-normalised outputs)
+// Preprocessing (ViTImageProcessor, main.py:107): resize_{h,v}_kernel (Pillow
+// fixed-point resample), patchify_kernel (rescale+normalize via an exact f32 LUT,
+// HWC→im2col, bf16 cast).
+#pragma once
+
+#include "rc_common.h"
+
+namespace rc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+
+enum GemmEpi { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_PATCH_F32 = 3 };
+
+struct GemmArgs {
+    const uint16_t *A;  // [rows >= roundup(M, BM)][K] bf16, row-major
+    const uint16_t *W;  // [N][K] bf16 (nn.Linear weight layout)
+    const float *bias;  // [N]
+    int M, N, K;        // M = valid rows; N % 128 == 0; K % 64 == 0
+    uint16_t *out_bf16; // EPI_BF16 / EPI_GELU_BF16: [M][N]
+    float *out_f32;     // EPI_RESID_F32 (in place: out += A W^T + b) / EPI_PATCH_F32
+    const float *pos;   // EPI_PATCH_F32: position embeddings [tokens][N]
+    int tokens;         // EPI_PATCH_F32: tokens per image (patches + 1)
+};
+
+constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// C = A · Wᵀ (+ epilogue).  256 threads = 4 waves as 2 (M) × 2 (N), each wave a
+// 64×64 sub-tile of 4×4 mfma_f32_16x16x32_bf16 accumulators.  A/W tiles are
+// staged global→LDS with global_load_lds_dwordx4 (2-deep), rows of 128 B with
+// the 16-B chunk index XORed by (row>>1)&7 so the fragment ds_read_b128s are
+// bank-conflict-free; the XOR is applied to the per-lane SOURCE address because
+// the LDS-DMA destination is lane-linear.
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
+    constexpr int BM = GEMM_BM, BN = GEMM_BN, BK = GEMM_BK;
+    constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB (A) ; W tile same
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * TILE_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+
+    // XCD-aware, bijective block remap: blocks b and b+8 share an XCD, so give
+    // each XCD a contiguous run of tiles (tile = tm * ntn + tn: the N tiles of
+    // one A row-panel stay on one L2).
+    const int ntn = a.N / BN;
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int tm = tile / ntn, tn = tile % ntn;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    const int K = a.K;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+
+    // staging: wave w issues 4 A + 4 W LDS-DMA pieces of 1 KB (8 rows x 128 B)
+    auto stage = [&](int buf, int k0) {
+        uint8_t *As = smem + buf * 2 * TILE_BYTES;
+        uint8_t *Ws = As + TILE_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = wave * 4 + i;
+            const int r = piece * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            __builtin_amdgcn_global_load_lds((const void *)(Ag + (int64_t)r * K + k0 + c * 8),
+                                             (lds_void_t *)(As + piece * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(Wg + (int64_t)r * K + k0 + c * 8),
+                                             (lds_void_t *)(Ws + piece * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+        const uint8_t *As = smem + cur * 2 * TILE_BYTES;
+        const uint8_t *Ws = As + TILE_BYTES;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = s * 4 + (lane >> 4);
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = wm * 64 + mi * 16 + (lane & 15);
+                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int r = wn * 64 + ni * 16 + (lane & 15);
+                bfr[ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+        }
+        __syncthreads();  // next tile landed (vmcnt(0)) and everyone is done reading `cur`
+    }
+
+    // epilogue: lane holds C[row = 4*(lane>>4) + j][col = lane&15] of each 16x16 tile
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + wn * 64 + ni * 16 + (lane & 15);
+        const float bcol = a.bias[col];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = m0 + wm * 64 + mi * 16 + (lane >> 4) * 4 + j;
+                if (row >= a.M) continue;
+                float v = acc[mi][ni][j] + bcol;
+                if constexpr (EPI == EPI_BF16) {
+                    a.out_bf16[(int64_t)row * a.N + col] = f32_to_bf16(v);
+                } else if constexpr (EPI == EPI_GELU_BF16) {
+                    a.out_bf16[(int64_t)row * a.N + col] = f32_to_bf16(gelu_erf(v));
+                } else if constexpr (EPI == EPI_RESID_F32) {
+                    float *o = a.out_f32 + (int64_t)row * a.N + col;
+                    *o = *o + v;
+                } else {  // EPI_PATCH_F32: row = (image, patch) → hidden row image*tokens + 1 + patch
+                    const int np = a.tokens - 1;
+                    const int img = row / np, p = row - img * np;
+                    a.out_f32[((int64_t)img * a.tokens + 1 + p) * a.N + col] = v + a.pos[(int64_t)(1 + p) * a.N + col];
+                }
+            }
+        }
+    }
+}
+
+// One wave per row of H = 256*NV f32 values → bf16 LayerNorm output.
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ x, const float *__restrict__ g,
+                                                       const float *__restrict__ b, uint16_t *__restrict__ y, int M,
+                                                       float eps) {
+    constexpr int H = 256 * NV;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float4 *xr = reinterpret_cast<const float4 *>(x + (int64_t)row * H);
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        v[i] = xr[lane + 64 * i];
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) * (1.0f / H);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+        ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(ss) * (1.0f / H) + eps);
+    const float4 *g4 = reinterpret_cast<const float4 *>(g);
+    const float4 *b4 = reinterpret_cast<const float4 *>(b);
+    uint2 *yr = reinterpret_cast<uint2 *>(y + (int64_t)row * H);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float4 gg = g4[lane + 64 * i], bb = b4[lane + 64 * i];
+        const float o0 = (v[i].x - mean) * rstd * gg.x + bb.x;
+        const float o1 = (v[i].y - mean) * rstd * gg.y + bb.y;
+        const float o2 = (v[i].z - mean) * rstd * gg.z + bb.z;
+        const float o3 = (v[i].w - mean) * rstd * gg.w + bb.w;
+        yr[lane + 64 * i] = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
+    }
+}
+
+// Final LayerNorm of the CLS row of each image + the two /embed outputs.
+template <int NV>
+__global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__ hidden, int tokens,
+                                                      const float *__restrict__ g, const float *__restrict__ b,
+                                                      float eps, float *__restrict__ raw, float *__restrict__ normed) {
+    constexpr int H = 256 * NV;
+    const int lane = threadIdx.x;
+    const int img = blockIdx.x;
+    const float4 *xr = reinterpret_cast<const float4 *>(hidden + (int64_t)img * tokens * H);
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        v[i] = xr[lane + 64 * i];
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) * (1.0f / H);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+        ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(ss) * (1.0f / H) + eps);
+    const float4 *g4 = reinterpret_cast<const float4 *>(g);
+    const float4 *b4 = reinterpret_cast<const float4 *>(b);
+    float4 o[NV];
+    float n2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float4 gg = g4[lane + 64 * i], bb = b4[lane + 64 * i];
+        o[i].x = (v[i].x - mean) * rstd * gg.x + bb.x;
+        o[i].y = (v[i].y - mean) * rstd * gg.y + bb.y;
+        o[i].z = (v[i].z - mean) * rstd * gg.z + bb.z;
+        o[i].w = (v[i].w - mean) * rstd * gg.w + bb.w;
+        n2 += (o[i].x * o[i].x + o[i].y * o[i].y) + (o[i].z * o[i].z + o[i].w * o[i].w);
+        reinterpret_cast<float4 *>(raw + (int64_t)img * H)[lane + 64 * i] = o[i];
+    }
+    if (normed) {
+        const float nrm = sqrtf(wave_sum(n2));
+        const float inv = nrm > 0.f ? 1.0f / nrm : 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            reinterpret_cast<float4 *>(normed + (int64_t)img * H)[lane + 64 * i] =
+                make_float4(o[i].x * inv, o[i].y * inv, o[i].z * inv, o[i].w * inv);
+    }
+}
+
+// hidden[img*tokens + 0] = cls + pos[0]
+__global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidden, int tokens, int H,
+                                                      const float *__restrict__ cls, const float *__restrict__ pos) {
+    const int img = blockIdx.x;
+    for (int c = threadIdx.x; c < H; c += 256) hidden[(int64_t)img * tokens * H + c] = cls[c] + pos[c];
+}
+
+// Self-attention for one (image, head): S = 197 tokens, head dim 64.
+// K (XOR-swizzled 128-B rows) and V (160-B rows, conflict-free for the
+// transposed reads) of the head live in LDS; each wave takes 16-query tiles.
+// Sᵀ = K·Qᵀ puts the query on the MFMA column (lane&15), so softmax over keys
+// is a per-lane reduction plus two xor-shuffles, and Pᵀ sits in registers in
+// exactly the B-operand layout of Oᵀ = Vᵀ·Pᵀ (k order permuted per 32-key step:
+// element j of lane group g is key 16t+4g+j (j<4) or 16(t+1)+4g+j-4), whose A
+// operand comes from V by ds_read_b64_tr_b16.
+constexpr int ATT_TP = 224;  // keys padded to 14 tiles of 16
+constexpr int ATT_VROW = 160;
+
+__global__ __launch_bounds__(256) void attention_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+                                                       int tokens, int heads, float scale) {
+    constexpr int HD = 64;
+    __shared__ __attribute__((aligned(16))) uint8_t Ks[ATT_TP * 128];
+    __shared__ __attribute__((aligned(16))) uint8_t Vs[ATT_TP * ATT_VROW];
+    const int H = heads * HD, H3 = 3 * H;
+    const int img = blockIdx.x / heads, h = blockIdx.x % heads;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD;
+
+    for (int idx = tid; idx < ATT_TP * 8; idx += 256) {
+        const int r = idx >> 3, c = idx & 7;
+        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+        if (r < tokens) {
+            kv = *reinterpret_cast<const uint4 *>(base + (int64_t)r * H3 + H + c * 8);
+            vv = *reinterpret_cast<const uint4 *>(base + (int64_t)r * H3 + 2 * H + c * 8);
+        }
+        *reinterpret_cast<uint4 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = kv;
+        *reinterpret_cast<uint4 *>(Vs + r * ATT_VROW + c * 16) = vv;
+    }
+    __syncthreads();
+
+    const int g = lane >> 4, li = lane & 15;
+    const int nqt = (tokens + 15) / 16;
+    for (int qt = wave; qt < nqt; qt += 4) {
+        const int q = qt * 16 + li;
+        const int qc = q < tokens ? q : tokens - 1;
+        bf16x8 qf[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            qf[s] = *reinterpret_cast<const bf16x8 *>(base + (int64_t)qc * H3 + s * 32 + g * 8);
+
+        f32x4 st[14];
+#pragma unroll
+        for (int t = 0; t < 14; ++t) {
+            st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int r = t * 16 + li;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = s * 4 + g;
+                const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[t], 0, 0, 0);
+            }
+        }
+        // softmax over keys for query column li (keys spread over t, j and the 4 lane groups)
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 14; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = t * 16 + g * 4 + j;
+                const float v = key < tokens ? st[t][j] * scale : -INFINITY;
+                st[t][j] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 14; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float p = __expf(st[t][j] - mx);
+                st[t][j] = p;
+                sum += p;
+            }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+
+        f32x4 o[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+        for (int tp = 0; tp < 7; ++tp) {
+            const int t = tp * 2;
+            bf16x8 pf;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pf[j] = (__bf16)st[t][j];
+                pf[j + 4] = (__bf16)st[t + 1][j];
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int col = d * 16 + pp * 4;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4_t *)(Vs + (t * 16 + g * 4 + qq) * ATT_VROW + col * 2));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4_t *)(Vs + (t * 16 + 16 + g * 4 + qq) * ATT_VROW + col * 2));
+                const short __attribute__((ext_vector_type(8))) vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
+            }
+        }
+        if (q < tokens) {
+            const float inv = 1.0f / sum;
+            uint16_t *orow = out + ((int64_t)img * tokens + q) * H + h * HD;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                *reinterpret_cast<uint2 *>(orow + d * 16 + g * 4) =
+                    make_uint2(pack_bf16x2(o[d][0] * inv, o[d][1] * inv), pack_bf16x2(o[d][2] * inv, o[d][3] * inv));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- preprocess
+// Pillow 8bpc separable resample (horizontal then vertical), fixed point 22 bits.
+__device__ __forceinline__ uint8_t clip8_fixed(int acc) {
+    int v = acc >> 22;
+    return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+// src [n, H, W, 3] rows [y0, y0+Hs) → tmp [n, Hs, OW, 3]
+__global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t *__restrict__ src, int H, int W, int y0, int Hs,
+                                                      uint8_t *__restrict__ dst, int OW, const int *__restrict__ bounds,
+                                                      const int *__restrict__ coef, int ks, int n) {
+    const int64_t total = (int64_t)n * Hs * OW;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int x = (int)(i % OW);
+        const int64_t t = i / OW;
+        const int y = (int)(t % Hs), img = (int)(t / Hs);
+        const int xmin = bounds[2 * x], xn = bounds[2 * x + 1];
+        const uint8_t *row = src + (((int64_t)img * H + y0 + y) * W + xmin) * 3;
+        int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+        for (int k = 0; k < xn; ++k) {
+            const int c = coef[x * ks + k];
+            a0 += row[3 * k] * c;
+            a1 += row[3 * k + 1] * c;
+            a2 += row[3 * k + 2] * c;
+        }
+        uint8_t *o = dst + i * 3;
+        o[0] = clip8_fixed(a0);
+        o[1] = clip8_fixed(a1);
+        o[2] = clip8_fixed(a2);
+    }
+}
+
+// src [n, Hs, W, 3] → dst [n, OH, W, 3]
+__global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t *__restrict__ src, int Hs, int W,
+                                                      uint8_t *__restrict__ dst, int OH, const int *__restrict__ bounds,
+                                                      const int *__restrict__ coef, int ks, int n) {
+    const int64_t total = (int64_t)n * OH * W;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int x = (int)(i % W);
+        const int64_t t = i / W;
+        const int y = (int)(t % OH), img = (int)(t / OH);
+        const int ymin = bounds[2 * y], yn = bounds[2 * y + 1];
+        const uint8_t *col = src + (((int64_t)img * Hs + ymin) * W + x) * 3;
+        int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+        for (int k = 0; k < yn; ++k) {
+            const int c = coef[y * ks + k];
+            const uint8_t *p = col + (int64_t)k * W * 3;
+            a0 += p[0] * c;
+            a1 += p[1] * c;
+            a2 += p[2] * c;
+        }
+        uint8_t *o = dst + i * 3;
+        o[0] = clip8_fixed(a0);
+        o[1] = clip8_fixed(a1);
+        o[2] = clip8_fixed(a2);
+    }
+}
+
+// u8 [n, S, S, 3] → im2col'd bf16 A [n*(S/P)^2, 3*P*P], column c*P*P + kh*P + kw,
+// value = lut[c][u] (the exact f32 of rescale-then-normalize), 8 outputs per thread.
+template <int P>
+__global__ __launch_bounds__(256) void patchify_kernel(const uint8_t *__restrict__ img, const float *__restrict__ lut,
+                                                      uint16_t *__restrict__ A, int n, int S) {
+    constexpr int KC = 3 * P * P;
+    const int gp = S / P, np = gp * gp;
+    const int64_t total = (int64_t)n * np * (KC / 8);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int chunk = (int)(i % (KC / 8));
+        const int64_t m = i / (KC / 8);
+        const int b = (int)(m / np), p = (int)(m % np);
+        const int py = p / gp, px = p % gp;
+        const int col0 = chunk * 8;
+        const int c = col0 / (P * P), kh = (col0 % (P * P)) / P, kw0 = col0 % P;
+        const uint8_t *src = img + (((int64_t)b * S + py * P + kh) * S + px * P + kw0) * 3 + c;
+        const float *l = lut + c * 256;
+        uint32_t w[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w[t] = pack_bf16x2(l[src[6 * t]], l[src[6 * t + 3]]);
+        *reinterpret_cast<uint4 *>(A + m * KC + col0) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// u8 [n, S, S, 3] → f32 pixel_values [n, 3, S, S] (what ViTImageProcessor returns)
+__global__ __launch_bounds__(256) void pixel_values_kernel(const uint8_t *__restrict__ img, const float *__restrict__ lut,
+                                                          float *__restrict__ out, int n, int S) {
+    const int64_t total = (int64_t)n * 3 * S * S;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int x = (int)(i % S);
+        const int64_t t = i / S;
+        const int y = (int)(t % S);
+        const int64_t t2 = t / S;
+        const int c = (int)(t2 % 3), b = (int)(t2 / 3);
+        out[i] = lut[c * 256 + img[(((int64_t)b * S + y) * S + x) * 3 + c]];
+    }
+}
+
+}  // namespace rc

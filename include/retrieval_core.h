@@ -1,0 +1,170 @@
+/*
+ * retrieval_core.h — C ABI of the MI355X-native retrieval core.
+ *
+ * One hipcc-built shared library (libretrieval_core.so, gfx950) behind the
+ * reference's own API for the hot path "embed a batch of images → exact cosine
+ * top-k over an in-HBM index".  The reference has no FFI of its own: its hot
+ * path is remote Python (transformers in the embedding pod, Pinecone SaaS for
+ * the index).  Each entry point below names the reference call it replaces;
+ * INTEGRATION.md shows the ctypes binding a maintainer would add.
+ *
+ * Conventions
+ *   - every function returns int status (RC_OK = 0); on error the message is
+ *     in the thread-local rc_last_error(); no C++ exception crosses the ABI;
+ *   - device buffers are caller-owned (e.g. torch tensors' data_ptr) unless a
+ *     function says otherwise; `stream` is a hipStream_t (NULL = default);
+ *   - hot calls (rc_index_search, rc_index_upsert, rc_embed) allocate nothing
+ *     once the workspace is reserved (rc_index_reserve / rc_model_create);
+ *   - each handle is bound to the device it was created on and guarded by a
+ *     mutex, so a multi-threaded caller may share it.
+ */
+#ifndef RETRIEVAL_CORE_H
+#define RETRIEVAL_CORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RC_ABI_VERSION 1
+
+/* status codes */
+#define RC_OK 0
+#define RC_ERR_INVALID 1     /* bad argument (maps to ValueError)            */
+#define RC_ERR_HIP 2         /* HIP runtime failure                          */
+#define RC_ERR_OOM 3         /* device allocation failed                     */
+#define RC_ERR_UNSUPPORTED 4 /* valid request outside what the build handles */
+#define RC_ERR_STATE 5       /* handle not ready (e.g. weights missing)      */
+
+/* storage dtypes of index rows */
+#define RC_F32 0
+#define RC_F16 1
+#define RC_BF16 2
+
+/* Pillow resampling filters (PIL.Image.Resampling values) */
+#define RC_RESAMPLE_BILINEAR 2
+#define RC_RESAMPLE_BICUBIC 3
+
+#define RC_TOPK_MAX 256 /* largest k a single search call accepts */
+
+typedef struct rc_index rc_index;
+typedef struct rc_model rc_model;
+
+const char *rc_last_error(void);
+int rc_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * In-HBM exact cosine index.  Replaces the Pinecone index:
+ *   get_index(name)            ingesting/utils.py:23-38, retriever/utils.py:23-38
+ *   index.upsert([(id,v,md)])  ingesting/main.py:156-158
+ *   index.query(v, top_k)      retriever/utils.py:62-64
+ *   index.fetch(ids)           retriever/main.py:142
+ * Rows are stored L2-normalised in `dtype`, row-major with leading dimension
+ * ld = round_up(dim, 128) (zero padded).  String ids and metadata stay on the
+ * host; the device only knows row numbers.  `row_base` is added to every row
+ * a search returns (shard offset in a multi-GPU index).
+ * ---------------------------------------------------------------------- */
+
+/* replaces pc.create_index(metric="cosine", dimension=dim) — ingesting/utils.py:29-36 */
+int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t row_base, rc_index **out);
+int rc_index_destroy(rc_index *h);
+int rc_index_info(const rc_index *h, int *dim, int *dtype, int64_t *capacity, int64_t *ld);
+/* device pointer to row 0 of the stored (normalised, cast) rows */
+int rc_index_data(const rc_index *h, void **rows_dev, float **norms_dev);
+
+/* Size the search workspace for up to max_nq queries and k <= max_k.  Called
+ * once before the hot loop; search grows it on demand otherwise. */
+int rc_index_reserve(rc_index *h, int max_nq, int max_k);
+
+/* replaces index.upsert — ingesting/main.py:156-158.
+ * vecs: device f32 [n, dim]; rows: device i64 [n] local row slots (host-assigned:
+ * an existing id keeps its row, so upsert overwrites).  Each row is L2-normalised
+ * in f32, cast to the storage dtype and scattered; its norm is kept so fetch can
+ * return the original values.  An all-zero vector is rejected by the host layer. */
+int rc_index_upsert(rc_index *h, const float *vecs, int64_t n, const int64_t *rows, void *stream);
+
+/* replaces index.fetch(ids)["vectors"][id]["values"] — retriever/main.py:142.
+ * rows: device i64 [n]; out: device f32 [n, dim] = stored row × stored norm. */
+int rc_index_fetch(rc_index *h, const int64_t *rows, int64_t n, float *out, void *stream);
+/* The stored (normalised, dtype-rounded) rows as f32, without the norm —
+ * what the search actually scores against (parity tests run the oracle on these). */
+int rc_index_fetch_stored(rc_index *h, const int64_t *rows, int64_t n, float *out, void *stream);
+
+/* replaces index.query(vector, top_k) — retriever/utils.py:62-64.
+ * queries: device f32 [nq, dim] (normalised inside); rows [0, n_rows) are searched.
+ * scores: device f32 [nq, k] cosine, descending; out_rows: device i64 [nq, k]
+ * = row_base + local row.  Ties: score desc, then row asc.  Slots beyond n_rows
+ * get score -inf and row -1.  1 <= k <= RC_TOPK_MAX. */
+int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k,
+                    float *scores, int64_t *out_rows, void *stream);
+
+/* Synthetic rows for benchmarks (no reference counterpart): rows
+ * [row0, row0+n) get uniform[-1,1) values from a counter-based hash of
+ * (seed, row, col), normalised and cast like an upsert. */
+int rc_index_fill_random(rc_index *h, uint64_t seed, int64_t row0, int64_t n, void *stream);
+
+/* Merge nlists sorted top-k lists per query into one (cross-shard merge after
+ * the all-gather; no reference counterpart — Pinecone merges server-side).
+ * scores/rows: device [nlists, nq, k_in] (each list sorted score desc, row asc,
+ * lists ordered by ascending row range); out: device [nq, k]. */
+int rc_topk_merge(const float *scores, const int64_t *rows, int nlists, int nq, int k_in, int k,
+                  float *out_scores, int64_t *out_rows, void *stream);
+
+/* ------------------------------------------------------------------------
+ * ViT-MSN image embedding.  Replaces the /embed compute path —
+ * embedding/main.py:97-114: PIL decode (stays on host) → ViTImageProcessor
+ * (resize, rescale, normalize) → ViTMSNModel → last_hidden_state[:, 0, :].
+ * ---------------------------------------------------------------------- */
+typedef struct rc_vit_config {
+    int image_size;   /* 224 */
+    int patch;        /* 16 */
+    int hidden;       /* 768 */
+    int layers;       /* 12 */
+    int heads;        /* 12 */
+    int mlp;          /* 3072 */
+    float ln_eps;     /* 1e-6 */
+    int max_batch;    /* workspace is sized for this many images per rc_embed call */
+} rc_vit_config;
+
+/* replaces ViTMSNModel.from_pretrained(...).to(DEVICE) — embedding/main.py:37-39 */
+int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out);
+int rc_model_destroy(rc_model *m);
+/* One state-dict tensor by checkpoint key (legacy layout, e.g.
+ * "encoder.layer.3.attention.attention.query.weight"; an optional "vit."
+ * prefix and the transformers-5 names "layers.N.attention.q_proj.weight" are
+ * also accepted).  host_data: host f32, numel must match. */
+int rc_model_set_weight(rc_model *m, const char *name, const float *host_data, int64_t numel);
+/* Preprocessor parameters (ViTImageProcessor: resample, rescale_factor, image_mean, image_std). */
+int rc_model_set_preprocess(rc_model *m, int resample, double rescale_factor, const float mean[3], const float std_[3]);
+/* Verify every weight was set and build the fused device layouts. */
+int rc_model_finalize(rc_model *m);
+
+/* replaces embedding/main.py:107-114 for a batch.
+ * images: device u8 [n, h, w, 3] (HWC RGB, as decoded by PIL); n <= max_batch.
+ * (h, w) != (image_size, image_size) → Pillow-exact resize on the device first.
+ * raw_out: device f32 [n, hidden] = last_hidden_state[:, 0, :] (the /embed body);
+ * normed_out: device f32 [n, hidden] L2-normalised copy for the index (may be NULL). */
+int rc_embed(rc_model *m, const uint8_t *images, int n, int h, int w,
+             float *raw_out, float *normed_out, void *stream);
+
+/* Preprocess only: device u8 [n,h,w,3] → device f32 pixel_values [n,3,S,S]
+ * exactly as ViTImageProcessor produces them (for parity tests). */
+int rc_preprocess(rc_model *m, const uint8_t *images, int n, int h, int w, float *pixel_values, void *stream);
+
+/* Per-kernel timing with HIP events on the launch stream (bench/roofline).
+ * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM (dominant), 2 = attention,
+ * 3 = layernorm, 4 = preprocess. */
+int rc_model_timing(rc_model *m, int enable);
+int rc_model_timing_read(rc_model *m, int kernel_id, double *total_ms, int64_t *launches, double *flops);
+int rc_model_timing_reset(rc_model *m);
+
+/* Index-side timing of the dominant search kernel (scan), same conventions. */
+int rc_index_timing(rc_index *h, int enable);
+int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RETRIEVAL_CORE_H */
