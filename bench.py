@@ -1,0 +1,283 @@
+"""Benchmark of the MI355X retrieval core (driver contract: one JSON line on rank 0).
+
+Headline (``value``): BASELINE.json config 2 — batch-256 224x224 synthetic u8
+images through the full embedding path (preprocess → ViT-MSN-base 12 layers →
+CLS + L2) per GPU, images/s summed over ranks (data parallel, no collectives,
+weak scaling).  ``roofline`` prices the dominant kernel (the fc1 GEMM) from HIP
+events recorded around its launches inside the timed steps.
+
+Secondary (``search``): config 4's single-query variant, weak-scaled — each
+rank holds ``--rows-per-gpu`` x 512 fp16 rows (125M/GPU → 1B at 8 GPUs), a
+query is broadcast, every rank runs the HIP scan + top-k over its shard, the
+per-rank top-k lists are all-gathered over RCCL and merged on the device.  Also
+config 3 (1M x 512 f32, top-10, one GPU).  Its roofline is HBM: bytes = rows x
+512 x dtype bytes per query pass.
+
+``cpu_baseline`` (rank 0, N=1 only): the oracle (numpy fp32 ViT, numpy cosine
+top-k) timed on a bounded sample on this host's cores.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PKG = "end-to-end-image-retrieval-service-with-k8s-jenkins_amd"
+METRIC = "top-k queries/s over 1B×512 index + embed images/s; % HBM/MFMA roofline"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_profile_traffic(kernel_key: str):
+    """HBM traffic per launch from the committed PMC summary (profiles/pmc_*.json), if present."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_embed_baseline(budget_s: float = 12.0):
+    """Oracle ViT-MSN fp32 forward (numpy BLAS) on batches of 8 synthetic images, bounded by time."""
+    from threadpoolctl import threadpool_info
+
+    from oracle.preprocess import preprocess
+    from oracle.vit import embed_cls
+    from oracle.weights import seeded_vit_msn_weights
+
+    sd = seeded_vit_msn_weights(0)
+    rng = np.random.default_rng(3)
+    imgs = rng.integers(0, 256, (8, 224, 224, 3), dtype=np.uint8)
+    pv = np.stack([preprocess(x) for x in imgs])
+    embed_cls(pv[:1], sd, num_layers=1)  # warm BLAS
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or done == 0:
+        pv = np.stack([preprocess(x) for x in imgs])
+        embed_cls(pv, sd)
+        done += len(imgs)
+    el = time.perf_counter() - t0
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    return {"value": done / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{done} images (batches of 8, 224x224 u8) through oracle preprocess + numpy fp32 ViT-MSN-base, {el:.1f}s"}
+
+
+def cpu_search_baseline(n_rows=1_000_000, dim=512, budget_s=6.0):
+    from threadpoolctl import threadpool_info
+
+    from oracle.cosine_topk import cosine_topk_f32
+
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((n_rows, dim), dtype=np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    q = rng.standard_normal(dim).astype(np.float32)
+    cosine_topk_f32(X, q, 10)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or done == 0:
+        cosine_topk_f32(X, q, 10)
+        done += 1
+    el = time.perf_counter() - t0
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    return {"value": done / el, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{done} single queries, exact top-10 over {n_rows}x{dim} f32 (numpy X@q + argpartition), {el:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--rows-per-gpu", type=int, default=125_000_000)
+    ap.add_argument("--search-queries", type=int, default=20)
+    ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import importlib
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    vit = importlib.import_module(f"{PKG}.vit")
+    index = importlib.import_module(f"{PKG}.index")
+
+    # ------------------------------------------------------ embed (value) --
+    B = args.batch
+    model = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=local, max_batch=B)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    images = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
+    raw = torch.empty((B, 768), dtype=torch.float32, device=dev)
+    nrm = torch.empty((B, 768), dtype=torch.float32, device=dev)
+    for _ in range(args.warmup):
+        model.embed(images, out=(raw, nrm))
+    torch.cuda.synchronize()
+    model.timing(["fc1"])
+    model.timing_reset()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.embed(images, out=(raw, nrm))
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    fc1_ms, fc1_n, fc1_flops = model.timing_read("fc1")
+    model.timing(False)
+    assert torch.isfinite(raw).all()
+    imgs_per_s = world * B * args.steps / el
+    fc1_avg_ms = fc1_ms / max(fc1_n, 1)
+    fc1_flops_launch = fc1_flops / max(fc1_n, 1)
+    achieved = fc1_flops_launch / (fc1_avg_ms / 1e3) / 1e12
+    gflop = vit.gflop_per_image()
+    model_tflops = imgs_per_s / world * gflop / 1e3
+    model.close()
+    del images, raw, nrm
+    torch.cuda.empty_cache()
+
+    result = {
+        "metric": METRIC,
+        "value": imgs_per_s,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform u8 224x224x3 images, random-init ViT-MSN-base weights; no checkpoint offline)",
+        "config": {
+            "workload": "BASELINE config 2: batch-256 224x224 images per GPU through preprocess + ViT-MSN-base (12 layers) + CLS/L2-norm",
+            "global_batch": B * world,
+            "seq_len": 197,
+            "parallelism": f"dp{world}",
+        },
+        "roofline": {
+            "kernel": "gemm_bf16_kernel<EPI_GELU_BF16> (fc1: M=%d N=3072 K=768)" % (B * 197),
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_BF16_TFLOPS,
+            "traffic": load_profile_traffic("fc1"),
+            "avg_launch_ms": fc1_avg_ms,
+            "launches": fc1_n,
+            "flops_per_launch": fc1_flops_launch,
+        },
+        "model_tflops_per_gpu": model_tflops,
+        "model_mfma_frac": model_tflops / PEAK_BF16_TFLOPS,
+    }
+
+    # ------------------------------------------------- search (secondary) --
+    if not args.no_search:
+        dim = 512
+        rows = args.rows_per_gpu
+        sharded = importlib.import_module(f"{PKG}.sharded")
+        sidx = sharded.ShardedIndex(dim, dtype="float16", capacity_per_rank=rows, device=local)
+        sidx.fill_random(4 + rank, rows)
+        shard = sidx.local
+        shard.reserve(1, 10)
+        gq = torch.Generator(device=dev).manual_seed(5)
+        queries = torch.randn((args.search_queries, dim), device=dev, generator=gq)  # same on every rank
+        k = 10
+
+        def one_query(qi):
+            return sidx.search(queries[qi:qi + 1], k)
+
+        for qi in range(2):
+            one_query(qi)
+        torch.cuda.synchronize()
+        shard.timing(True)
+        barrier()
+        t0 = time.perf_counter()
+        for qi in range(args.search_queries):
+            one_query(qi)
+        torch.cuda.synchronize()
+        barrier()
+        sel = max_over_ranks(time.perf_counter() - t0)
+        scan_ms, scan_n, scan_bytes = shard.timing_read()
+        shard.timing(False)
+        scan_gbps = scan_bytes / (scan_ms / 1e3) / 1e9
+        result["search"] = {
+            "workload": f"BASELINE config 4 single-query variant: {rows * world:,} x 512 fp16 rows ({rows:,}/GPU), exact cosine top-{k}",
+            "value": args.search_queries / sel,
+            "unit": "queries/s",
+            "ms_per_query": sel / args.search_queries * 1e3,
+            "roofline": {"kernel": "scan_topk_kernel<f16,4,1,128>", "bound": "hbm", "achieved": scan_gbps,
+                         "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": scan_gbps / PEAK_HBM_GBPS,
+                         "traffic": load_profile_traffic("scan_f16"), "avg_launch_ms": scan_ms / max(scan_n, 1),
+                         "bytes_per_launch": scan_bytes / max(scan_n, 1)},
+        }
+        sidx.close()
+        del shard, sidx
+        torch.cuda.empty_cache()
+        # config 3: 1M x 512 f32, single query top-10 on one GPU (rank-local)
+        c3 = index.DeviceIndex(dim, dtype="float32", capacity=1_000_000, device=local)
+        c3.fill_random(2, 0, 1_000_000)
+        for qi in range(3):
+            c3.search(queries[qi:qi + 1], 10, 1_000_000)
+        torch.cuda.synchronize()
+        c3.timing(True)
+        t0 = time.perf_counter()
+        nq3 = 200
+        for qi in range(nq3):
+            c3.search(queries[qi % args.search_queries:qi % args.search_queries + 1], 10, 1_000_000)
+        torch.cuda.synchronize()
+        el3 = time.perf_counter() - t0
+        ms3, n3, b3 = c3.timing_read()
+        c3.close()
+        result["search"]["config3"] = {"workload": "BASELINE config 3: 1M x 512 f32, single query exact top-10, 1 GPU",
+                                       "value": nq3 / el3, "unit": "queries/s (per GPU)",
+                                       "scan_GBps": b3 / (ms3 / 1e3) / 1e9, "scan_frac": b3 / (ms3 / 1e3) / 1e9 / PEAK_HBM_GBPS}
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            result["cpu_baseline"] = cpu_embed_baseline()
+            if "search" in result:
+                result["search"]["cpu_baseline"] = cpu_search_baseline()
+        except Exception as e:  # the baseline must not kill the GPU bench line
+            result["cpu_baseline"] = {"error": repr(e)}
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

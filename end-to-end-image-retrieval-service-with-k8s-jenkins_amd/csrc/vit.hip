@@ -520,9 +520,11 @@ int rc_model_timing(rc_model *m, int enable) {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         std::lock_guard<std::mutex> lk(m->mu);
         DeviceScope ds(m->device);
-        for (auto &t : m->timers) {
-            if (enable) t.create();
-            t.enabled = enable != 0;
+        for (int i = 0; i < T_COUNT; ++i) {
+            auto &t = m->timers[i];
+            const bool on = (enable >> i) & 1;
+            if (on) t.create();
+            t.enabled = on;
         }
     });
 }

@@ -1,0 +1,100 @@
+"""``/embed`` service on the MI355X core (mirror of reference ``embedding/main.py``).
+
+Contract kept from the reference (``embedding/main.py:78-124``):
+  GET  /         → {"message": "Welcome to ViT-MSN Embedding API. Visit /docs to test."}
+  GET  /healthz  → {"status": "healthy"}
+  POST /embed    multipart field ``file`` → JSON list[float] (raw CLS vector, 768)
+                 400 {"detail": "Uploaded file is not a valid image."} on an unidentifiable image
+                 422 when ``file`` is missing; other decode errors propagate (500)
+
+Compute: PIL decode on the host (``:97``), then one ``rc_embed`` call on the GPU
+(resize → normalize → ViT-MSN → final LN of the CLS row) instead of
+``extractor`` + ``model`` (``:107-113``).  ``POST /embed_batch`` (field ``files``,
+repeated) returns one vector per image — the batched form of the same contract.
+OpenTelemetry/Prometheus instrumentation of the reference is out of scope.
+"""
+from __future__ import annotations
+
+import threading
+from io import BytesIO
+from typing import List
+
+from fastapi import FastAPI, HTTPException, Request
+from fastapi.exceptions import RequestValidationError
+from PIL import Image, UnidentifiedImageError
+
+from ..config import Config
+from ..multipart import parse_form
+
+app = FastAPI(title="ViT-MSN Embedding Service")
+
+_embedder = None
+_embedder_lock = threading.Lock()
+
+
+def get_embedder():
+    """Process-wide model singleton (reference loads it at import, ``:37-39``; here on first use)."""
+    global _embedder
+    with _embedder_lock:
+        if _embedder is None:
+            from ..vit import VitMsnEmbedder, random_state_dict
+
+            if Config.MODEL_PATH:
+                _embedder = VitMsnEmbedder.from_pretrained(Config.MODEL_PATH, max_batch=Config.EMBED_MAX_BATCH)
+            else:  # no checkpoint offline: deterministic seeded weights
+                _embedder = VitMsnEmbedder(random_state_dict(Config.WEIGHT_SEED), max_batch=Config.EMBED_MAX_BATCH)
+        return _embedder
+
+
+def _missing_file(field: str):
+    return RequestValidationError([{"type": "missing", "loc": ("body", field), "msg": "Field required", "input": None}])
+
+
+def decode_image(data: bytes) -> Image.Image:
+    try:
+        return Image.open(BytesIO(data)).convert("RGB")
+    except UnidentifiedImageError:
+        raise HTTPException(status_code=400, detail="Uploaded file is not a valid image.")
+
+
+def embed_bytes(data: bytes) -> list[float]:
+    """Core of /embed: image bytes → raw CLS vector (list of floats)."""
+    image = decode_image(data)  # validate before touching the model (400 needs no GPU)
+    return get_embedder().embed_pil([image])[0]
+
+
+@app.get("/")
+def read_root():
+    return {"message": "Welcome to ViT-MSN Embedding API. Visit /docs to test."}
+
+
+@app.get("/healthz")
+def health_check():
+    return {"status": "healthy"}
+
+
+@app.post("/embed", response_model=List[float])
+async def embed_image(request: Request):
+    form = parse_form(await request.body(), request.headers.get("content-type", ""))
+    f = form.get("file")
+    if f is None:
+        raise _missing_file("file")
+    return embed_bytes(f.data)
+
+
+@app.post("/embed_batch", response_model=List[List[float]])
+async def embed_images(request: Request):
+    body = await request.body()
+    ctype = request.headers.get("content-type", "")
+    from email.parser import BytesParser
+    from email.policy import HTTP
+
+    if not ctype.lower().startswith("multipart/form-data"):
+        raise _missing_file("files")
+    msg = BytesParser(policy=HTTP).parsebytes(b"Content-Type: " + ctype.encode("latin-1") + b"\r\n\r\n" + body)
+    blobs = [p.get_payload(decode=True) or b"" for p in msg.iter_parts()
+             if p.get_param("name", header="content-disposition") == "files"]
+    if not blobs:
+        raise _missing_file("files")
+    images = [decode_image(b) for b in blobs]
+    return get_embedder().embed_pil(images)

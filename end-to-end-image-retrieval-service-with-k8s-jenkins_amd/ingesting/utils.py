@@ -1,0 +1,61 @@
+"""Ingest helpers on the MI355X core (mirror of reference ``ingesting/utils.py``).
+
+* ``get_index(index_name)`` — reference ``:23-38`` opens or creates a Pinecone
+  cosine index of ``dimension=Config.INPUT_RESOLUTION``; here it opens or creates
+  the in-HBM exact index (one per name per process), same ``upsert``/``query``/
+  ``fetch`` shapes.
+* ``get_feature_vector(image_bytes)`` — reference ``:41-56``: POST the bytes to
+  ``Config.EMBEDDING_SERVICE_URL`` as field ``file``; any failure becomes
+  ``HTTPException(500, "Failed to get feature vector from embedding service")``.
+* ``embed_locally(image_bytes)`` — the same vector computed in-process on the GPU
+  (no HTTP hop) for deployments that co-locate ingest with the model.
+
+``get_storage_client`` (GCS) is out of scope: blob storage is not on the hot path.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+
+import requests
+from fastapi import HTTPException
+
+from ..config import Config
+
+logger = logging.getLogger(__name__)
+
+_indexes: dict = {}
+_lock = threading.Lock()
+
+
+def get_index(index_name: str, dimension: int | None = None, dtype: str | None = None, capacity: int | None = None):
+    from ..index import Index
+
+    with _lock:
+        idx = _indexes.get(index_name)
+        if idx is None:
+            idx = Index(index_name, dimension=dimension or Config.INPUT_RESOLUTION, metric="cosine",
+                        dtype=dtype or Config.INDEX_DTYPE, capacity=capacity or Config.INDEX_CAPACITY)
+            _indexes[index_name] = idx
+            logger.info("Created in-HBM index: %s", index_name)
+        return idx
+
+
+def get_feature_vector(image_bytes: bytes) -> list:
+    try:
+        logger.info("Calling embedding service at %s", Config.EMBEDDING_SERVICE_URL)
+        response = requests.post(
+            url=Config.EMBEDDING_SERVICE_URL,
+            files={"file": ("image.jpg", image_bytes, "image/jpeg")},
+        )
+        response.raise_for_status()
+        return response.json()
+    except Exception as e:
+        logger.error("Failed to get feature vector: %s", e)
+        raise HTTPException(status_code=500, detail="Failed to get feature vector from embedding service")
+
+
+def embed_locally(image_bytes: bytes) -> list:
+    from ..embedding.main import embed_bytes
+
+    return embed_bytes(image_bytes)

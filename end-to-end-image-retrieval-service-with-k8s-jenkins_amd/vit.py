@@ -1,0 +1,235 @@
+"""ViT-MSN image embedder on the HIP library (replaces ``extractor`` + ``model``).
+
+Reference: ``embedding/main.py:33-39`` builds ``ViTImageProcessor`` and
+``ViTMSNModel`` singletons; ``:97-114`` decodes with PIL, preprocesses, runs the
+model under ``no_grad`` and returns ``last_hidden_state[:, 0, :]``.  Here the
+decode stays on the host (PIL), the u8 HWC pixels go to HBM once, and
+``rc_embed`` does resize → rescale/normalize → patch embed → 12 layers → final
+LayerNorm of the CLS row on the GPU, returning the raw CLS vector (the /embed
+body) and its L2-normalised copy (what the index stores).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Iterable, Mapping, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+from .config import VIT_MSN_BASE, VIT_MSN_PREPROCESS
+
+TIMER_IDS = {"gemm": 0, "fc1": 1, "attention": 2, "layernorm": 3, "preprocess": 4}
+
+
+def _to_f32_numpy(t) -> np.ndarray:
+    if isinstance(t, torch.Tensor):
+        return t.detach().to("cpu", torch.float32).contiguous().numpy()
+    return np.ascontiguousarray(np.asarray(t, dtype=np.float32))
+
+
+def load_checkpoint_dir(path: str) -> tuple[dict, dict, dict]:
+    """(state_dict, model_config, preprocess) from a local HF-style checkpoint directory.
+
+    Loads only with loaders that execute nothing from the file: safetensors, or
+    ``torch.load(weights_only=True)``.
+    """
+    cfg = dict(VIT_MSN_BASE)
+    pre = dict(VIT_MSN_PREPROCESS)
+    cj = os.path.join(path, "config.json")
+    if os.path.exists(cj):
+        with open(cj) as f:
+            c = json.load(f)
+        for k in cfg:
+            if k in c:
+                cfg[k] = c[k]
+    pj = os.path.join(path, "preprocessor_config.json")
+    if os.path.exists(pj):
+        with open(pj) as f:
+            p = json.load(f)
+        if "resample" in p:
+            pre["resample"] = int(p["resample"])
+        if "rescale_factor" in p:
+            pre["rescale_factor"] = float(p["rescale_factor"])
+        if "image_mean" in p:
+            pre["image_mean"] = tuple(p["image_mean"])
+        if "image_std" in p:
+            pre["image_std"] = tuple(p["image_std"])
+        if isinstance(p.get("size"), dict) and "height" in p["size"]:
+            pre["size"] = (p["size"]["height"], p["size"]["width"])
+    st = os.path.join(path, "model.safetensors")
+    if os.path.exists(st):
+        from safetensors.numpy import load_file
+
+        sd = load_file(st)
+    else:
+        sd = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)
+    return dict(sd), cfg, pre
+
+
+class VitMsnEmbedder:
+    """One ``rc_model`` on one GPU: fixed weights, workspace for ``max_batch`` images."""
+
+    def __init__(self, state_dict: Mapping, device=None, max_batch: int = 32, model_config: dict | None = None,
+                 preprocess: dict | None = None):
+        self.lib = _lib.load()
+        cfg = dict(VIT_MSN_BASE)
+        cfg.update(model_config or {})
+        if model_config is None:
+            cfg["num_hidden_layers"] = sum(1 for k in state_dict if k.endswith("layernorm_before.weight"))
+        self.config = cfg
+        self.preprocess_params = dict(VIT_MSN_PREPROCESS)
+        self.preprocess_params.update(preprocess or {})
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index or 0)
+        self.max_batch = int(max_batch)
+        self.hidden = cfg["hidden_size"]
+        c = _lib.VitConfig(cfg["image_size"], cfg["patch_size"], cfg["hidden_size"], cfg["num_hidden_layers"],
+                           cfg["num_attention_heads"], cfg["intermediate_size"], float(cfg["layer_norm_eps"]),
+                           self.max_batch)
+        h = _lib.C.c_void_p()
+        check(self.lib.rc_model_create(self.device.index, _lib.C.byref(c), _lib.C.byref(h)))
+        self._h = h
+        try:
+            for name, t in state_dict.items():
+                if name.endswith("mask_token") or name.startswith("classifier"):
+                    continue
+                a = _to_f32_numpy(t)
+                check(self.lib.rc_model_set_weight(self._h, name.encode(), a.ctypes.data, a.size))
+            p = self.preprocess_params
+            mean = (_lib.C.c_float * 3)(*p["image_mean"])
+            std = (_lib.C.c_float * 3)(*p["image_std"])
+            check(self.lib.rc_model_set_preprocess(self._h, int(p["resample"]), float(p["rescale_factor"]), mean, std))
+            check(self.lib.rc_model_finalize(self._h))
+        except Exception:
+            self.close()
+            raise
+
+    @classmethod
+    def from_pretrained(cls, path: str, device=None, max_batch: int = 32) -> "VitMsnEmbedder":
+        sd, cfg, pre = load_checkpoint_dir(path)
+        return cls(sd, device=device, max_batch=max_batch, model_config=cfg, preprocess=pre)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            check(self.lib.rc_model_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ compute --
+    def _images(self, images_u8: torch.Tensor) -> torch.Tensor:
+        if images_u8.dtype != torch.uint8 or images_u8.dim() != 4 or images_u8.shape[-1] != 3:
+            raise ValueError("images must be uint8 [n, h, w, 3] (HWC RGB)")
+        if images_u8.shape[0] > self.max_batch:
+            raise ValueError(f"batch {images_u8.shape[0]} exceeds max_batch {self.max_batch}")
+        return images_u8.to(self.device).contiguous()
+
+    def embed(self, images_u8: torch.Tensor, normalized: bool = True, stream=None, out=None):
+        """u8 [n,h,w,3] (any equal h,w) → (raw [n,H], normed [n,H] or None) f32 on the device."""
+        x = self._images(images_u8)
+        n, h, w = x.shape[:3]
+        if out is None:
+            raw = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device)
+            nrm = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device) if normalized else None
+        else:
+            raw, nrm = out
+        check(self.lib.rc_embed(self._h, ptr(x), n, h, w, ptr(raw), ptr(nrm), stream_ptr(stream)))
+        return raw, nrm
+
+    def preprocess(self, images_u8: torch.Tensor, stream=None) -> torch.Tensor:
+        """u8 [n,h,w,3] → f32 pixel_values [n,3,S,S], exactly as ViTImageProcessor (parity hook)."""
+        x = self._images(images_u8)
+        n, h, w = x.shape[:3]
+        S = self.config["image_size"]
+        out = torch.empty((n, 3, S, S), dtype=torch.float32, device=self.device)
+        check(self.lib.rc_preprocess(self._h, ptr(x), n, h, w, ptr(out), stream_ptr(stream)))
+        return out
+
+    def embed_pil(self, images: Sequence) -> list[list[float]]:
+        """Host PIL RGB images (any sizes) → raw CLS vectors as Python lists (the /embed body)."""
+        out: list[list[float] | None] = [None] * len(images)
+        groups: dict[tuple[int, int], list[int]] = {}
+        for i, im in enumerate(images):
+            groups.setdefault((im.size[1], im.size[0]), []).append(i)
+        for (h, w), idx in groups.items():
+            for s in range(0, len(idx), self.max_batch):
+                chunk = idx[s:s + self.max_batch]
+                arr = np.stack([np.asarray(images[i].convert("RGB"), dtype=np.uint8) for i in chunk])
+                raw, _ = self.embed(torch.from_numpy(arr), normalized=False)
+                vals = raw.cpu().tolist()
+                for j, i in enumerate(chunk):
+                    out[i] = vals[j]
+        return out  # type: ignore[return-value]
+
+    # ------------------------------------------------------------- timing --
+    def timing(self, enable: bool | Iterable[str]) -> None:
+        """Enable event timing for all kernels (True), none (False) or the named ones."""
+        if isinstance(enable, bool):
+            mask = -1 if enable else 0
+        else:
+            mask = 0
+            for k in enable:
+                mask |= 1 << TIMER_IDS[k]
+        check(self.lib.rc_model_timing(self._h, mask))
+
+    def timing_reset(self) -> None:
+        check(self.lib.rc_model_timing_reset(self._h))
+
+    def timing_read(self, kernel: str):
+        ms = _lib.C.c_double()
+        n = _lib.C.c_int64()
+        w = _lib.C.c_double()
+        check(self.lib.rc_model_timing_read(self._h, TIMER_IDS[kernel], _lib.C.byref(ms), _lib.C.byref(n), _lib.C.byref(w)))
+        return ms.value, n.value, w.value
+
+
+def gflop_per_image(cfg: dict = VIT_MSN_BASE) -> float:
+    """Algorithmic FLOPs (2 x MACs) of one ViT forward incl. attention (35.126 GFLOP)."""
+    H, F, L = cfg["hidden_size"], cfg["intermediate_size"], cfg["num_hidden_layers"]
+    P = cfg["patch_size"]
+    np_ = (cfg["image_size"] // P) ** 2
+    T = np_ + 1
+    patch = np_ * H * 3 * P * P
+    per_layer = T * (3 * H * H + H * H + 2 * H * F) + 2 * T * T * H
+    return 2.0 * (patch + L * per_layer) / 1e9
+
+
+def random_state_dict(seed: int = 0, num_layers: int = 12, cfg: dict = VIT_MSN_BASE) -> dict[str, np.ndarray]:
+    """Random-init ViT-MSN weights in the checkpoint's key layout (benchmarks: no checkpoint offline)."""
+    g = torch.Generator().manual_seed(seed)
+    H, F, P, T = cfg["hidden_size"], cfg["intermediate_size"], cfg["patch_size"], (cfg["image_size"] // cfg["patch_size"]) ** 2 + 1
+
+    def rnd(*shape, std=0.02, mean=0.0):
+        return (torch.randn(*shape, generator=g) * std + mean).numpy()
+
+    sd = {
+        "embeddings.cls_token": rnd(1, 1, H),
+        "embeddings.position_embeddings": rnd(1, T, H),
+        "embeddings.patch_embeddings.projection.weight": rnd(H, 3, P, P),
+        "embeddings.patch_embeddings.projection.bias": rnd(H),
+        "layernorm.weight": rnd(H, std=0.1, mean=1.0),
+        "layernorm.bias": rnd(H),
+    }
+    for i in range(num_layers):
+        p = f"encoder.layer.{i}."
+        for nm in ("query", "key", "value"):
+            sd[p + f"attention.attention.{nm}.weight"] = rnd(H, H)
+            sd[p + f"attention.attention.{nm}.bias"] = rnd(H)
+        sd[p + "attention.output.dense.weight"] = rnd(H, H)
+        sd[p + "attention.output.dense.bias"] = rnd(H)
+        sd[p + "intermediate.dense.weight"] = rnd(F, H)
+        sd[p + "intermediate.dense.bias"] = rnd(F)
+        sd[p + "output.dense.weight"] = rnd(H, F)
+        sd[p + "output.dense.bias"] = rnd(H)
+        for nm in ("layernorm_before", "layernorm_after"):
+            sd[p + nm + ".weight"] = rnd(H, std=0.1, mean=1.0)
+            sd[p + nm + ".bias"] = rnd(H)
+    return sd

@@ -154,8 +154,8 @@ int rc_preprocess(rc_model *m, const uint8_t *images, int n, int h, int w, float
 
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM (dominant), 2 = attention,
- * 3 = layernorm, 4 = preprocess. */
-int rc_model_timing(rc_model *m, int enable);
+ * 3 = layernorm, 4 = preprocess; `mask` bit i enables id i (-1 = all, 0 = off). */
+int rc_model_timing(rc_model *m, int mask);
 int rc_model_timing_read(rc_model *m, int kernel_id, double *total_ms, int64_t *launches, double *flops);
 int rc_model_timing_reset(rc_model *m);
 

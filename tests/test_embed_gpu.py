@@ -1,0 +1,146 @@
+"""GPU parity of the ViT-MSN embedding path (rc_embed / rc_preprocess) against the oracle.
+
+Reference path replaced: ``embedding/main.py:97-114`` (PIL decode → ViTImageProcessor
+→ ViTMSNModel → ``last_hidden_state[:, 0, :]``).  Bars (north star):
+  * preprocessing is integer/byte work + an exact f32 LUT → bit-exact pixel_values;
+  * embeddings (bf16 MFMA GEMMs, f32 accumulate/residual) agree with the fp32
+    reference within 1e-2 cosine distance — tolerance written below as BF16_COS_TOL.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from conftest import GOLDEN, import_pkg
+from oracle.pil_resample import BICUBIC, BILINEAR
+from oracle.preprocess import VIT_MSN_PREPROCESS, preprocess
+from oracle.vit import cosine, embed_cls
+from oracle.weights import seeded_vit_msn_weights
+
+pytestmark = pytest.mark.gpu
+
+BF16_COS_TOL = 1e-2  # north-star bound for the bf16 path: 1 - cos(got, ref) <= 1e-2
+
+
+@pytest.fixture(scope="module")
+def vitmod(cuda):
+    return import_pkg("vit")
+
+
+@pytest.fixture(scope="module")
+def weights12():
+    return seeded_vit_msn_weights(1907)
+
+
+@pytest.fixture(scope="module")
+def model12(vitmod, weights12, cuda):
+    m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=16)
+    yield m
+    m.close()
+
+
+def _test_image():
+    return np.array(Image.open(os.path.join(GOLDEN, "test_image.jpeg")).convert("RGB"))
+
+
+def test_preprocess_test_image_bit_exact(model12):
+    import torch
+
+    g = json.load(open(os.path.join(GOLDEN, "golden.json")))
+    img = _test_image()
+    pv = model12.preprocess(torch.from_numpy(img[None])).cpu().numpy()[0]
+    assert hashlib.sha256(pv.tobytes()).hexdigest()[:16] == g["pixel_values_sha16"]
+
+
+@pytest.mark.parametrize("h,w", [(224, 224), (300, 168), (97, 480), (224, 100), (50, 224), (513, 511), (16, 16)])
+@pytest.mark.parametrize("resample", [BICUBIC, BILINEAR])
+def test_preprocess_random_sizes_bit_exact(vitmod, weights12, cuda, h, w, resample):
+    import torch
+
+    params = dict(VIT_MSN_PREPROCESS, resample=resample)
+    m = vitmod.VitMsnEmbedder({k: v for k, v in weights12.items() if "encoder.layer." not in k or ".layer.0." in k},
+                              device=0, max_batch=3, preprocess=params)
+    rng = np.random.default_rng(h * 1000 + w)
+    imgs = rng.integers(0, 256, (3, h, w, 3), dtype=np.uint8)
+    got = m.preprocess(torch.from_numpy(imgs)).cpu().numpy()
+    ref = np.stack([preprocess(x, params) for x in imgs])
+    assert np.array_equal(got, ref)
+    m.close()
+
+
+def test_embed_test_image_matches_reference(model12):
+    """Full 12-layer seeded model on the reference's own test image vs transformers' output."""
+    import torch
+
+    ref = np.load(os.path.join(GOLDEN, "test_image_embedding_seed1907.npy"))
+    img = _test_image()
+    raw, nrm = model12.embed(torch.from_numpy(img[None]))
+    raw = raw.cpu().numpy()[0]
+    assert np.isfinite(raw).all()
+    assert 1.0 - cosine(raw, ref) <= BF16_COS_TOL
+    assert 1.0 - cosine(raw, ref) <= 2e-3  # what this build actually achieves (regression guard)
+    nrm = nrm.cpu().numpy()[0]
+    assert np.allclose(nrm, raw / np.linalg.norm(raw), atol=1e-6)
+
+
+def test_embed_two_layer_synthetic(vitmod, cuda):
+    import torch
+
+    sd2 = seeded_vit_msn_weights(1907, num_layers=2)
+    m = vitmod.VitMsnEmbedder(sd2, device=0, max_batch=2)
+    imgs = np.load(os.path.join(GOLDEN, "synthetic_u8_2x224.npy"))
+    ref = np.load(os.path.join(GOLDEN, "synthetic_embedding_2layer_seed1907.npy"))
+    raw, _ = m.embed(torch.from_numpy(imgs))
+    raw = raw.cpu().numpy()
+    for i in range(2):
+        assert 1.0 - cosine(raw[i], ref[i]) <= BF16_COS_TOL
+    m.close()
+
+
+def test_embed_batch_equals_single_and_deterministic(model12):
+    """Rows of a batch are independent: batched == one-by-one, bitwise; repeat runs are bitwise equal."""
+    import torch
+
+    rng = np.random.default_rng(7)
+    imgs = torch.from_numpy(rng.integers(0, 256, (5, 224, 224, 3), dtype=np.uint8))
+    a, _ = model12.embed(imgs)
+    b, _ = model12.embed(imgs)
+    assert torch.equal(a, b)
+    for i in range(5):
+        s, _ = model12.embed(imgs[i:i + 1])
+        assert torch.equal(s[0], a[i])
+
+
+def test_embed_matches_numpy_oracle_random(model12, weights12):
+    import torch
+
+    rng = np.random.default_rng(9)
+    imgs = rng.integers(0, 256, (2, 224, 224, 3), dtype=np.uint8)
+    raw, _ = model12.embed(torch.from_numpy(imgs))
+    ref = embed_cls(np.stack([preprocess(x) for x in imgs]), weights12)
+    raw = raw.cpu().numpy()
+    for i in range(2):
+        assert 1.0 - cosine(raw[i], ref[i]) <= BF16_COS_TOL
+
+
+def test_embed_full_batch_256_properties(vitmod, weights12, cuda):
+    """Config 2's shape (batch 256, 224x224): finite, deterministic, spot rows vs the oracle."""
+    import torch
+
+    m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=256)
+    rng = np.random.default_rng(1)
+    imgs = rng.integers(0, 256, (256, 224, 224, 3), dtype=np.uint8)
+    raw, nrm = m.embed(torch.from_numpy(imgs))
+    raw2, _ = m.embed(torch.from_numpy(imgs))
+    assert torch.equal(raw, raw2)
+    assert torch.isfinite(raw).all()
+    assert torch.allclose(nrm.norm(dim=1), torch.ones(256, device=nrm.device), atol=1e-5)
+    pick = [0, 131, 255]
+    ref = embed_cls(np.stack([preprocess(imgs[i]) for i in pick]), weights12)
+    got = raw.cpu().numpy()[pick]
+    for j in range(len(pick)):
+        assert 1.0 - cosine(got[j], ref[j]) <= BF16_COS_TOL
+    m.close()
