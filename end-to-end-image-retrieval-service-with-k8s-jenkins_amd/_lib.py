@@ -87,6 +87,7 @@ SIGNATURES = {
     "rc_model_timing": (C.c_int, [_vp, _i32]),
     "rc_model_timing_read": (C.c_int, [_vp, _i32, _pd, _pi64, _pd]),
     "rc_model_timing_reset": (C.c_int, [_vp]),
+    "rc_gemm_bf16": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp]),
 }
 
 _lock = threading.Lock()

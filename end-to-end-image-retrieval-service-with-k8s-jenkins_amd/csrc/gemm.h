@@ -1,0 +1,191 @@
+// gemm.h — the projection GEMMs of ViT-MSN (QKV, O, fc1, fc2, patch embed) on
+// CDNA4 matrix cores: C[M][N] = A[M][K] · W[N][K]ᵀ + bias, bf16 in, f32 accumulate,
+// fused epilogues (bf16 store, exact-erf GELU, f32 residual add, patch→token scatter
+// + position embedding).
+//
+// Tile BM x 256 x 64 (BM = 256 or 128), 512 threads = 8 waves as 2 (M) x 4 (N);
+// each wave owns (BM/2) x 64 outputs = (BM/32) x 4 tiles of mfma_f32_16x16x32_bf16.
+// The MFMA operand roles are swapped — A-operand = weight rows, B-operand =
+// activation rows — so a lane's accumulator holds 4 CONSECUTIVE output columns
+// of one row: the epilogue reads bias/residual/pos as float4 and stores 8 B
+// (bf16) or 16 B (f32) per lane.
+// Staging: global_load_lds_dwordx4 into a 2-deep LDS ring, rows of 128 B with the
+// 16-B chunk XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 fragments;
+// swizzle applied to the per-lane SOURCE address, LDS destination lane-linear).
+// One raw s_barrier per K-step behind an explicit vmcnt(0): the next K-tile's
+// DMA is issued before this K-tile's MFMAs and lands under them.
+#pragma once
+
+#include "vit_kernels.h"
+
+namespace rc {
+
+constexpr int G2_BN = 256, G2_BK = 64;
+
+// erf via Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), one exp + one rcp.
+__device__ __forceinline__ float erf_as(float x) {
+    const float ax = fabsf(x);
+    const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    p *= t;
+    const float y = 1.0f - p * __expf(-ax * ax);
+    return copysignf(y, x);
+}
+__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
+
+template <int EPI, int BM>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
+    constexpr int BN = G2_BN, BK = G2_BK;
+    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+    constexpr int MI = BM / 32, NI = 4;
+    constexpr int A_PIECES = A_BYTES / 1024, B_PIECES = B_BYTES / 1024;  // 1-KB LDS-DMA pieces
+    constexpr int PIECES_PER_WAVE = (A_PIECES + B_PIECES) / 8;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int ntn = a.N / BN;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int tm = tile / ntn, tn = tile % ntn;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int K = a.K;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+
+    auto stage = [&](int buf, int k0) {
+        uint8_t *base = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < PIECES_PER_WAVE; ++i) {
+            const int piece = wave + 8 * i;  // wave-uniform
+            const int r = (piece < A_PIECES ? piece : piece - A_PIECES) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const uint16_t *src = piece < A_PIECES ? Ag + (int64_t)r * K : Wg + (int64_t)r * K;
+            __builtin_amdgcn_global_load_lds((const void *)(src + k0 + c * 8), (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+        const uint8_t *As = smem + cur * STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = s * 4 + g;
+            bf16x8 wf[NI], af[MI];
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+                const int r = wn * 64 + ni * 16 + li;
+                wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int mi = 0; mi < MI; ++mi) {
+                const int r = wm * (BM / 2) + mi * 16 + li;
+                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < NI; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+
+    // epilogue: acc[mi][ni][j] = C[m0 + wm*BM/2 + mi*16 + li][n0 + wn*64 + ni*16 + 4g + j]
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+        const int col = n0 + wn * 64 + ni * 16 + 4 * g;
+        const float4 bias = *reinterpret_cast<const float4 *>(a.bias + col);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+            const int row = m0 + wm * (BM / 2) + mi * 16 + li;
+            if (row >= a.M) continue;
+            float v0 = acc[mi][ni][0] + bias.x, v1 = acc[mi][ni][1] + bias.y;
+            float v2 = acc[mi][ni][2] + bias.z, v3 = acc[mi][ni][3] + bias.w;
+            if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+                if constexpr (EPI == EPI_GELU_BF16) {
+                    v0 = gelu_fast(v0);
+                    v1 = gelu_fast(v1);
+                    v2 = gelu_fast(v2);
+                    v3 = gelu_fast(v3);
+                }
+                *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * a.N + col) =
+                    make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+            } else if constexpr (EPI == EPI_RESID_F32) {
+                float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + col);
+                const float4 r = *o;
+                *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
+            } else {  // EPI_PATCH_F32
+                const int np = a.tokens - 1;
+                const int img = row / np, p = row - img * np;
+                const float4 ps = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + col);
+                *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + p) * a.N + col) =
+                    make_float4(v0 + ps.x, v1 + ps.y, v2 + ps.z, v3 + ps.w);
+            }
+        }
+    }
+}
+
+// Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
+// 3 = 128x256 8-wave, 0 = auto (256-row tiles when the N dimension gives >= 7
+// waves of tiles over 256 CUs, else 128-row tiles to shrink the last-wave tail).
+enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3 };
+
+inline int gemm_pick(const GemmArgs &a, int variant) {
+    if (variant != GEMM_AUTO) return variant;
+    if (a.N % G2_BN != 0) return GEMM_V1;
+    const int tiles256 = ((a.M + 255) / 256) * (a.N / G2_BN);
+    return tiles256 >= 7 * 256 ? GEMM_256x256 : GEMM_128x256;
+}
+
+// rows the A buffer must provide beyond M (the kernels read whole tiles)
+inline int gemm_row_pad() { return 256; }
+
+template <int EPI>
+void launch_gemm(const GemmArgs &a, int variant, hipStream_t s) {
+    RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
+    switch (gemm_pick(a, variant)) {
+        case GEMM_V1: {
+            RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
+            const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
+            hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
+            break;
+        }
+        case GEMM_256x256: {
+            RC_REQUIRE(a.N % G2_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            const int ntm = (a.M + 255) / 256, ntn = a.N / G2_BN;
+            hipLaunchKernelGGL((gemm256_kernel<EPI, 256>), dim3(ntm * ntn), dim3(512), 0, s, a);
+            break;
+        }
+        case GEMM_128x256: {
+            RC_REQUIRE(a.N % G2_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            const int ntm = (a.M + 127) / 128, ntn = a.N / G2_BN;
+            hipLaunchKernelGGL((gemm256_kernel<EPI, 128>), dim3(ntm * ntn), dim3(512), 0, s, a);
+            break;
+        }
+        default: throw Error(RC_ERR_INVALID, "unknown GEMM variant");
+    }
+    RC_LAUNCH_CHECK();
+}
+
+}  // namespace rc

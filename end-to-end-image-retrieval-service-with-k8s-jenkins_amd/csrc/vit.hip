@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "gemm.h"
 #include "vit_kernels.h"
 
 using namespace rc;
@@ -127,6 +128,7 @@ struct rc_model {
     uint8_t *resized = nullptr, *resize_tmp = nullptr;
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
+    int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
 
     void *alloc(size_t bytes) {
         void *p = dmalloc(bytes);
@@ -300,13 +302,10 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
 
 template <int EPI>
 void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, bool fc1 = false) {
-    RC_REQUIRE(a.N % GEMM_BN == 0 && a.K % GEMM_BK == 0, RC_ERR_UNSUPPORTED, "GEMM shape not tile aligned");
-    const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = fc1 ? m->timers[T_FC1].begin(s) : -1;
-    hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
-    RC_LAUNCH_CHECK();
+    launch_gemm<EPI>(a, m->gemm_variant, s);
     if (fc1) m->timers[T_FC1].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
@@ -378,8 +377,8 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->kpatch = 3 * cfg->patch * cfg->patch;
             build_shapes(m);
             const int B = cfg->max_batch, H = cfg->hidden;
-            m->Mp = round_up(B * m->tokens, GEMM_BM);
-            m->Pp = round_up(B * m->npatch, GEMM_BM);
+            m->Mp = round_up(B * m->tokens, gemm_row_pad());
+            m->Pp = round_up(B * m->npatch, gemm_row_pad());
             m->patches = (uint16_t *)m->alloc((size_t)m->Pp * m->kpatch * 2);
             m->hidden = (float *)m->alloc((size_t)m->Mp * H * 4);
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
@@ -395,6 +394,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));
             build_lut(m);
+            if (const char *gv = std::getenv("RC_GEMM_VARIANT")) m->gemm_variant = std::atoi(gv);
         } catch (...) {
             delete m;
             throw;
@@ -553,3 +553,22 @@ int rc_model_timing_reset(rc_model *m) {
 }
 
 }  // extern "C"
+
+extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N,
+                            int K, void *out, const float *pos, int tokens, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
+        GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
+        hipStream_t s = (hipStream_t)stream;
+        switch (epi) {
+            case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s); break;
+            case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s); break;
+            case EPI_RESID_F32: launch_gemm<EPI_RESID_F32>(a, variant, s); break;
+            case EPI_PATCH_F32:
+                RC_REQUIRE(pos && tokens > 1, RC_ERR_INVALID, "patch epilogue needs pos and tokens");
+                launch_gemm<EPI_PATCH_F32>(a, variant, s);
+                break;
+            default: throw Error(RC_ERR_INVALID, "unknown epilogue");
+        }
+    });
+}

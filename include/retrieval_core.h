@@ -159,6 +159,15 @@ int rc_model_timing(rc_model *m, int mask);
 int rc_model_timing_read(rc_model *m, int kernel_id, double *total_ms, int64_t *launches, double *flops);
 int rc_model_timing_reset(rc_model *m);
 
+/* Kernel-level entry to the projection GEMM (parity tests / microbenchmarks;
+ * inside rc_embed this is every nn.Linear of modeling_vit_msn.py:199-202,243-244).
+ * out = epilogue(A[M][K] · W[N][K]ᵀ + bias): epi 0 → bf16 out, 1 → bf16 GELU(out),
+ * 2 → f32 out += (residual, in place), 3 → f32 patch scatter (+pos, tokens/image).
+ * A must have round_up(M, 256) readable rows.  variant: 0 auto, 1 128x128,
+ * 2 256x256, 3 128x256 tiles. */
+int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N, int K,
+                 void *out, const float *pos, int tokens, void *stream);
+
 /* Index-side timing of the dominant search kernel (scan), same conventions. */
 int rc_index_timing(rc_index *h, int enable);
 int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *bytes);

@@ -1,0 +1,75 @@
+"""Numerics of the projection GEMM kernels (rc_gemm_bf16) against a plain PyTorch fp32 reference.
+
+Same bf16 inputs on both sides, f32 accumulation on both sides, so f32 outputs
+agree to summation-order rounding (atol/rtol 1e-4 here) and bf16 outputs to one
+bf16 rounding (rtol 1e-2).  Every tile variant and every fused epilogue.
+"""
+import pytest
+
+from conftest import import_pkg
+
+pytestmark = pytest.mark.gpu
+
+EPI_BF16, EPI_GELU, EPI_RESID, EPI_PATCH = 0, 1, 2, 3
+
+
+def run(epi, variant, A, W, bias, M, out, pos=None, tokens=0):
+    L = import_pkg("_lib")
+    lib = L.load()
+    import torch
+
+    N, K = W.shape
+    L.check(lib.rc_gemm_bf16(epi, variant, A.data_ptr(), W.data_ptr(), bias.data_ptr(), M, N, K, out.data_ptr(),
+                             None if pos is None else pos.data_ptr(), tokens, torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(300, 768, 768), (1000, 2304, 768), (513, 3072, 768), (257, 768, 3072), (64, 256, 64)])
+@pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
+def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
+    import torch
+
+    if variant in (2, 3) and N % 256:
+        pytest.skip("256-wide tiles need N % 256 == 0")
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    Mp = (M + 255) // 256 * 256
+    A = (torch.randn(Mp, K, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
+    A[M:] = 0
+    W = (torch.randn(N, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    ref = A[:M].float() @ W.float().T + bias
+    if epi == EPI_RESID:
+        resid = torch.randn(Mp, N, device=cuda, generator=g)
+        out = resid.clone()
+        run(epi, variant, A, W, bias, M, out)
+        assert torch.allclose(out[:M], resid[:M] + ref, atol=1e-4, rtol=1e-4)
+        assert torch.equal(out[M:], resid[M:])  # rows >= M untouched
+    else:
+        out = torch.full((Mp, N), 7.0, device=cuda).to(torch.bfloat16)
+        run(epi, variant, A, W, bias, M, out)
+        if epi == EPI_GELU:
+            ref = torch.nn.functional.gelu(ref)
+        assert torch.allclose(out[:M].float(), ref, atol=2e-3, rtol=1e-2)
+        assert bool((out[M:].float() == 7.0).all())
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_patch_epilogue_scatter(cuda, variant):
+    import torch
+
+    n_img, npatch, H, K = 3, 196, 768, 768
+    T = npatch + 1
+    M = n_img * npatch
+    g = torch.Generator(device=cuda).manual_seed(0)
+    A = torch.zeros((M + 255) // 256 * 256, K, device=cuda).to(torch.bfloat16)
+    A[:M] = (torch.randn(M, K, device=cuda, generator=g)).to(torch.bfloat16)
+    W = (torch.randn(H, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(H, device=cuda, generator=g)
+    pos = torch.randn(T, H, device=cuda, generator=g)
+    hidden = torch.full((n_img * T, H), -3.0, device=cuda)
+    run(EPI_PATCH, variant, A, W, bias, M, hidden, pos, T)
+    ref = (A[:M].float() @ W.float().T + bias).reshape(n_img, npatch, H) + pos[1:]
+    got = hidden.reshape(n_img, T, H)
+    assert torch.allclose(got[:, 1:], ref, atol=1e-4, rtol=1e-4)
+    assert bool((got[:, 0] == -3.0).all())  # CLS rows are not the GEMM's
