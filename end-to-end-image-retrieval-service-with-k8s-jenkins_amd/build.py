@@ -44,13 +44,18 @@ def _headers():
 
 def _compile(src: str, extra: list[str]) -> str:
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+    stamp = obj + ".flags"
+    flags = " ".join(CFLAGS + extra)
     newest_dep = max(os.path.getmtime(p) for p in [src, __file__] + _headers())
-    if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+    same_flags = os.path.exists(stamp) and open(stamp).read() == flags
+    if same_flags and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
     cmd = [HIPCC, *CFLAGS, *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(flags)
     return obj
 
 

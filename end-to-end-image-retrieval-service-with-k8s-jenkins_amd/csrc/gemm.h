@@ -146,16 +146,231 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
     }
 }
 
+// ----------------------------------------------------------- ping-pong GEMM --
+// 256x256x64 tile, 8 waves in two groups: G0 = waves 0-3 (output rows 0-127),
+// G1 = waves 4-7 (rows 128-255); wave w and w+4 share a SIMD.  Each wave owns
+// 128x64 outputs as 4 quadrants of 64x32 (16 MFMAs per quadrant per K-tile).
+// A K-tile is 4 phases; a phase is an M segment (ds_read this quadrant's
+// fragments, issue this wave's LDS-DMA share of K-tile t+1, lgkmcnt(0)) and a
+// C segment (16 MFMAs), each closed by a block barrier.  G1 runs one segment
+// behind G0 (one extra barrier up front), so on every SIMD one wave's MFMAs
+// overlap its partner's LDS reads / DMA issue / waits.
+// Hazards: DMA for t+1 goes to buffer (t+1)&1 only in phases 0-1 of K-tile t,
+// after the barrier that closes both groups' last reads of K-tile t-1 (every M
+// segment retires its ds_reads before its barrier); every wave waits vmcnt(0)
+// in its phase-3 M segment, and the barrier after G1's phase-3 M segment
+// precedes G0's first read of t+1.
+// ABL (diagnostic builds only): bit0 = no DMA in the K loop, bit1 = no MFMA,
+// bit2 = no epilogue (accumulators kept live).  ABL = 0 is the product kernel.
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+    constexpr int BM = 256, BN = 256, BK = 64;
+    constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;  // A tile then W tile, 32 KB each
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int ntn = a.N / BN;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int tm = tile / ntn, tn = tile % ntn;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int K = a.K;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+
+    // 64 pieces of 1 KB per K-tile (A: 0-31, W: 32-63); wave w owns pieces w + 8 i.
+    auto stage4 = [&](int buf, int k0, int i0) {
+        uint8_t *base = smem + buf * STAGE;
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = i < 4;
+            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
+            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+        }
+    };
+    auto bar = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+        for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+            for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage4(0, 0, 0);
+    stage4(0, 0, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: G1 one segment behind
+
+    bf16x8 af[4][2], wf[2][2];  // [mi][s], [ni][s]
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const uint8_t *As = smem + cur * STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+        const bool more = kt + 1 < nk;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mq = p >> 1;                 // quadrant rows
+            const int nq = (p == 1 || p == 2);     // snake: (0,0) (0,1) (1,1) (1,0)
+            // ---- M segment
+            if (p == 0 || p == 2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        const int c = s * 4 + g;
+                        af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                    const int c = s * 4 + g;
+                    wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                }
+            if (!(ABL & 1) && more && p < 2) stage4(cur ^ 1, (kt + 1) * BK, p * 4);
+            if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            // ---- C segment
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        if constexpr (!(ABL & 2))
+                            acc[mq][nq][mi][ni] =
+                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], acc[mq][nq][mi][ni], 0, 0, 0);
+                        else
+                            asm volatile("" ::"v"(wf[ni][s]), "v"(af[mi][s]));
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+    }
+    if (grp == 0) bar();  // balance the stagger barrier
+    if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+        for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+            for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+                for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                    for (int a3 = 0; a3 < 2; ++a3) asm volatile("" ::"v"(acc[a0][a1][a2][a3]));
+        return;
+    }
+
+    // epilogue: acc[mq][nq][mi][ni][j] = C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        // Stage the 256x256 bf16 tile in LDS (512-B rows, 16-B chunk XOR (row & 31)),
+        // then every wave stores whole 512-B row segments with 16-B stores.
+        // (The K loop's final barrier retired every ds_read and DMA: LDS is free.)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;  // tile-local column
+                const float4 bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+#pragma unroll
+                for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi) {
+                        const int rl = grp * 128 + mq * 64 + mi * 16 + li;
+                        const f32x4 v4 = acc[mq][nq][mi][ni];
+                        float v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
+                        if constexpr (EPI == EPI_GELU_BF16) {
+                            v0 = gelu_fast(v0);
+                            v1 = gelu_fast(v1);
+                            v2 = gelu_fast(v2);
+                            v3 = gelu_fast(v3);
+                        }
+                        const int off = rl * 512 + ((((cl >> 3) ^ (rl & 31))) << 4) + (cl & 7) * 2;
+                        *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+                    }
+            }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 512 + tid;
+            const int rl = id >> 5, ch = id & 31;
+            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
+            if (m0 + rl < a.M) *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+        }
+        return;
+    }
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+            const int col = n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g;
+            const float4 bias = *reinterpret_cast<const float4 *>(a.bias + col);
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                    if (row >= a.M) continue;
+                    const f32x4 v4 = acc[mq][nq][mi][ni];
+                    float v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
+                    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+                        if constexpr (EPI == EPI_GELU_BF16) {
+                            v0 = gelu_fast(v0);
+                            v1 = gelu_fast(v1);
+                            v2 = gelu_fast(v2);
+                            v3 = gelu_fast(v3);
+                        }
+                        *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * a.N + col) =
+                            make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+                    } else if constexpr (EPI == EPI_RESID_F32) {
+                        float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + col);
+                        const float4 r = *o;
+                        *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
+                    } else {
+                        const int np = a.tokens - 1;
+                        const int img = row / np, pp = row - img * np;
+                        const float4 ps = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + pp) * a.N + col);
+                        *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + pp) * a.N + col) =
+                            make_float4(v0 + ps.x, v1 + ps.y, v2 + ps.z, v3 + ps.w);
+                    }
+                }
+        }
+}
+
 // Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
-// 3 = 128x256 8-wave, 0 = auto (256-row tiles when the N dimension gives >= 7
-// waves of tiles over 256 CUs, else 128-row tiles to shrink the last-wave tail).
-enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3 };
+// 3 = 128x256 8-wave, 0 = auto.  Auto follows interleaved A/B timings on the
+// batch-256 shapes (tools/gemm_micro.py, profiles/): the 256x256 ping-pong kernel
+// everywhere except the short square O-projection (N = K = 768), where 128-row
+// tiles shrink the 2.3-wave tail enough to win.
+enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4 };
 
 inline int gemm_pick(const GemmArgs &a, int variant) {
-    if (variant != GEMM_AUTO) return variant;
+    if (variant != GEMM_AUTO) return variant;  // (100 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.N % G2_BN != 0) return GEMM_V1;
     const int tiles256 = ((a.M + 255) / 256) * (a.N / G2_BN);
-    return tiles256 >= 7 * 256 ? GEMM_256x256 : GEMM_128x256;
+    if (tiles256 < 4 * 256 && a.K <= 1024) return GEMM_128x256;
+    return GEMM_PINGPONG;
 }
 
 // rows the A buffer must provide beyond M (the kernels read whole tiles)
@@ -183,6 +398,27 @@ void launch_gemm(const GemmArgs &a, int variant, hipStream_t s) {
             hipLaunchKernelGGL((gemm256_kernel<EPI, 128>), dim3(ntm * ntn), dim3(512), 0, s, a);
             break;
         }
+        case GEMM_PINGPONG: {
+            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
+            hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(ntm * ntn), dim3(512), 0, s, a);
+            break;
+        }
+#if defined(RC_GEMM_ABLATION)
+        case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6: {
+            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
+            const dim3 gr(ntm * ntn), bl(512);
+            switch (variant - 100) {
+                case 1: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1>), gr, bl, 0, s, a); break;
+                case 2: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 2>), gr, bl, 0, s, a); break;
+                case 3: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 3>), gr, bl, 0, s, a); break;
+                case 4: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 4>), gr, bl, 0, s, a); break;
+                case 5: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 5>), gr, bl, 0, s, a); break;
+                case 6: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 6>), gr, bl, 0, s, a); break;
+            }
+            break;
+        }
+#endif
         default: throw Error(RC_ERR_INVALID, "unknown GEMM variant");
     }
     RC_LAUNCH_CHECK();

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidde
 constexpr int ATT_TP = 224;  // keys padded to 14 tiles of 16
 constexpr int ATT_VROW = 160;
 
-__global__ __launch_bounds__(256) void attention_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+__global__ __launch_bounds__(256, 2) void attention_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
                                                        int tokens, int heads, float scale) {
     constexpr int HD = 64;
     __shared__ __attribute__((aligned(16))) uint8_t Ks[ATT_TP * 128];

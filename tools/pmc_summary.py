@@ -1,0 +1,66 @@
+"""Summarise rocprofv3 PMC passes (tools/pmc_collect.sh output) per kernel.
+
+Per kernel (short name + grid size): mean counter values per dispatch, mean
+duration, and derived numbers:
+  hbm_read_bytes  = 2 * FETCH_SIZE * 1024   (gfx950: FETCH_SIZE reads half of a
+                    wide coalesced stream — MI355X_MICROARCH.md §HBM; calibrate on
+                    a known byte count before trusting absolutes)
+  hbm_write_bytes = WRITE_SIZE * 1024
+  l2_hit          = TCC_HIT / (TCC_HIT + TCC_MISS)
+  mfma_busy       = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * CUs * 4 SIMDs)  (approx)
+  clock_GHz       = GRBM_GUI_ACTIVE / 8 / duration
+usage: python tools/pmc_summary.py DIR [--json OUT]
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(.*", "", name)
+    name = name.replace("void ", "").replace("rc::", "")
+    return name[:60]
+
+
+def main():
+    d = sys.argv[1]
+    vals = defaultdict(lambda: defaultdict(list))
+    durs = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            key = (short(r["Kernel_Name"]), int(r["Grid_Size"]))
+            vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            durs[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    out = {}
+    for key, cs in sorted(vals.items(), key=lambda kv: -sum(durs[kv[0]])):
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        dur = sum(durs[key]) / len(durs[key])
+        rec = {"kernel": key[0], "grid": key[1], "dispatches": max(len(v) for v in cs.values()), "dur_us": dur * 1e6}
+        rec.update({c: m[c] for c in m})
+        if "FETCH_SIZE" in m:
+            rec["hbm_read_bytes"] = 2 * m["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in m:
+            rec["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+        if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
+            rec["l2_hit"] = m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
+        if "GRBM_GUI_ACTIVE" in m:
+            rec["clock_GHz"] = m["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                rec["mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 256 * 4)
+        out[f"{key[0]}@{key[1]}"] = rec
+    for k, r in out.items():
+        if r["dur_us"] < 20:
+            continue
+        keys = ["dur_us", "hbm_read_bytes", "hbm_write_bytes", "l2_hit", "clock_GHz", "mfma_busy", "SQ_WAIT_ANY",
+                "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"]
+        print(k, {x: (round(r[x], 3) if isinstance(r.get(x), float) else r.get(x)) for x in keys if x in r})
+    if "--json" in sys.argv:
+        json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
