@@ -36,6 +36,26 @@ __device__ __forceinline__ float erf_as(float x) {
 }
 __device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
 
+// The same GELU on two values with packed f32 math (v_pk_fma_f32 / v_pk_mul_f32)
+// for the polynomial and scaling steps; rcp/exp stay per element.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+    const f32x2 z = x * 0.70710678118654752f;
+    const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+    const f32x2 d = az * 0.3275911f + 1.0f;
+    const f32x2 t = {__frcp_rn(d.x), __frcp_rn(d.y)};
+    f32x2 p = t * 1.061405429f + -1.453152027f;
+    p = p * t + 1.421413741f;
+    p = p * t + -0.284496736f;
+    p = p * t + 0.254829592f;
+    p = p * t;
+    const f32x2 q = -az * az;
+    const f32x2 e = {__expf(q.x), __expf(q.y)};
+    const f32x2 y = 1.0f - p * e;  // erf(|z|)
+    const f32x2 ys = {copysignf(y.x, z.x), copysignf(y.y, z.y)};
+    return 0.5f * x * (1.0f + ys);
+}
+
 template <int EPI, int BM>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
     constexpr int BN = G2_BN, BK = G2_BK;
@@ -301,10 +321,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                         const f32x4 v4 = acc[mq][nq][mi][ni];
                         float v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
                         if constexpr (EPI == EPI_GELU_BF16) {
-                            v0 = gelu_fast(v0);
-                            v1 = gelu_fast(v1);
-                            v2 = gelu_fast(v2);
-                            v3 = gelu_fast(v3);
+                            const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
+                            v0 = lo.x;
+                            v1 = lo.y;
+                            v2 = hi.x;
+                            v3 = hi.y;
                         }
                         const int off = rl * 512 + ((((cl >> 3) ^ (rl & 31))) << 4) + (cl & 7) * 2;
                         *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
@@ -320,42 +341,66 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         }
         return;
     }
+    // f32 epilogues (residual add / patch scatter): the 256x256 f32 tile is 256 KB,
+    // so each group's 128 rows are staged in turn (1-KB rows, 16-B chunk XOR
+    // (row & 63)) and copied out by all 512 threads as whole 1-KB row segments:
+    // 16-B residual/pos loads issued back to back, then 16-B stores.
 #pragma unroll
-    for (int nq = 0; nq < 2; ++nq)
+    for (int h = 0; h < 2; ++h) {
+        if (grp == h) {
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-            const int col = n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g;
-            const float4 bias = *reinterpret_cast<const float4 *>(a.bias + col);
+            for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
-            for (int mq = 0; mq < 2; ++mq)
+                for (int ni = 0; ni < 2; ++ni) {
+                    const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                    const float4 bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
 #pragma unroll
-                for (int mi = 0; mi < 4; ++mi) {
-                    const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
-                    if (row >= a.M) continue;
-                    const f32x4 v4 = acc[mq][nq][mi][ni];
-                    float v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
-                    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-                        if constexpr (EPI == EPI_GELU_BF16) {
-                            v0 = gelu_fast(v0);
-                            v1 = gelu_fast(v1);
-                            v2 = gelu_fast(v2);
-                            v3 = gelu_fast(v3);
+                    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                        for (int mi = 0; mi < 4; ++mi) {
+                            const int rl = mq * 64 + mi * 16 + li;  // row within the half
+                            const f32x4 v4 = acc[mq][nq][mi][ni];
+                            const int off = rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4);
+                            *reinterpret_cast<float4 *>(smem + off) =
+                                make_float4(v4[0] + bias.x, v4[1] + bias.y, v4[2] + bias.z, v4[3] + bias.w);
                         }
-                        *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * a.N + col) =
-                            make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-                    } else if constexpr (EPI == EPI_RESID_F32) {
-                        float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + col);
-                        const float4 r = *o;
-                        *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
-                    } else {
-                        const int np = a.tokens - 1;
-                        const int img = row / np, pp = row - img * np;
-                        const float4 ps = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + pp) * a.N + col);
-                        *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + pp) * a.N + col) =
-                            make_float4(v0 + ps.x, v1 + ps.y, v2 + ps.z, v3 + ps.w);
-                    }
                 }
         }
+        __syncthreads();
+        float4 add[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 512 + tid;
+            const int rl = id >> 6, ch = id & 63;
+            const int row = m0 + h * 128 + rl;
+            const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
+            if constexpr (EPI == EPI_RESID_F32) {
+                add[it] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
+            } else {
+                const int np = a.tokens - 1;
+                const int p = rr % np;
+                add[it] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 512 + tid;
+            const int rl = id >> 6, ch = id & 63;
+            const int row = m0 + h * 128 + rl;
+            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
+            const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
+            if (row < a.M) {
+                if constexpr (EPI == EPI_RESID_F32) {
+                    *reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + n0 + ch * 4) = o;
+                } else {
+                    const int np = a.tokens - 1;
+                    const int img = row / np, p = row - img * np;
+                    *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + p) * a.N + n0 + ch * 4) = o;
+                }
+            }
+        }
+        if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
+    }
 }
 
 // Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
@@ -369,7 +414,7 @@ inline int gemm_pick(const GemmArgs &a, int variant) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.N % G2_BN != 0) return GEMM_V1;
     const int tiles256 = ((a.M + 255) / 256) * (a.N / G2_BN);
-    if (tiles256 < 4 * 256 && a.K <= 1024) return GEMM_128x256;
+    (void)tiles256;
     return GEMM_PINGPONG;
 }
 

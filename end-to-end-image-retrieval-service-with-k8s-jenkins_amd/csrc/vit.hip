@@ -129,6 +129,7 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
+    int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
 
     void *alloc(size_t bytes) {
         void *p = dmalloc(bytes);
@@ -342,7 +343,11 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
         layernorm(m, m->hidden, L.ln1_w, L.ln1_b, m->ln, M, s);
         gemm<EPI_BF16>(m, GemmArgs{m->ln, L.w_qkv, L.b_qkv, M, 3 * H, H, m->qkv, nullptr, nullptr, T}, s);
         const int ta = m->timers[T_ATTN].begin(s);
-        hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, m->qkv, m->attn, T, c.heads, scale);
+        if (m->attn_variant == 1 || T > ATT2_ROWS)
+            hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, m->qkv, m->attn, T, c.heads, scale);
+        else
+            hipLaunchKernelGGL(attention_v2_kernel, dim3(n * c.heads), dim3(256), 0, s, m->qkv, m->attn, T, c.heads,
+                               scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
         gemm<EPI_RESID_F32>(m, GemmArgs{m->attn, L.w_o, L.b_o, M, H, H, nullptr, m->hidden, nullptr, T}, s);
@@ -395,6 +400,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));
             build_lut(m);
             if (const char *gv = std::getenv("RC_GEMM_VARIANT")) m->gemm_variant = std::atoi(gv);
+            if (const char *av = std::getenv("RC_ATTN_VARIANT")) m->attn_variant = std::atoi(av);
         } catch (...) {
             delete m;
             throw;

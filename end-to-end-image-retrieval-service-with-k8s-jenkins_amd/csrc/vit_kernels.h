@@ -247,6 +247,150 @@ __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidde
     for (int c = threadIdx.x; c < H; c += 256) hidden[(int64_t)img * tokens * H + c] = cls[c] + pos[c];
 }
 
+// Self-attention v2 for one (image, head), tokens <= 208, head dim 64.
+// K and V of the head are staged by LDS-DMA (global_load_lds_dwordx4, 8 rows of
+// 128 B per wave-instruction) into XOR-swizzled rows: K chunk ^ ((row>>1)&7)
+// (conflict-free ds_read_b128 A-fragments), V chunk ^ (((row>>1)&3)<<1)
+// (conflict-free ds_read_b64_tr_b16); the swizzle is applied to the per-lane
+// source address.  Keys pad to 13 tiles of 16 (rows >= tokens re-read the last
+// token: finite, and masked to p = 0).  Sᵀ = K·Qᵀ (13 tiles), softmax in f32 with
+// scores pre-scaled by log2(e)/8 so p = exp2(s - max); Oᵀ = Vᵀ·Pᵀ in 6 steps of 32
+// keys (16x16x32) + one 16-key step (16x16x16).  3 blocks per CU (52 KB LDS).
+constexpr int ATT2_TILES = 13, ATT2_ROWS = ATT2_TILES * 16;  // 208 keys
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+                                                          int tokens, int heads, float scale_log2e) {
+    constexpr int HD = 64;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];
+    uint8_t *Ks = lds, *Vs = lds + ATT2_ROWS * 128;
+    const int H = heads * HD, H3 = 3 * H;
+    const int img = blockIdx.x / heads, h = blockIdx.x % heads;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD;
+
+    // 26 pieces of 1 KB for K and 26 for V; wave w issues pieces w, w+4, ...
+    for (int piece = wave; piece < 2 * ATT2_TILES * 2; piece += 4) {
+        const bool isv = piece >= ATT2_TILES * 2;
+        const int r = (isv ? piece - ATT2_TILES * 2 : piece) * 8 + (lane >> 3);
+        const int pc = lane & 7;
+        const int c = isv ? (pc ^ (((r >> 1) & 3) << 1)) : (pc ^ ((r >> 1) & 7));
+        const int rr = r < tokens ? r : tokens - 1;
+        const uint16_t *src = base + (int64_t)rr * H3 + (isv ? 2 * H : H) + c * 8;
+        __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(lds + piece * 1024), 16, 0, 0);
+    }
+
+    const int g = lane >> 4, li = lane & 15;
+    const int nqt = (tokens + 15) / 16;
+    auto load_q = [&](int qt, bf16x8 (&qf)[2]) {
+        const int q = qt * 16 + li;
+        const int qc = q < tokens ? q : tokens - 1;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) qf[s] = *reinterpret_cast<const bf16x8 *>(base + (int64_t)qc * H3 + s * 32 + g * 8);
+    };
+    bf16x8 qf[2];
+    load_q(wave < nqt ? wave : 0, qf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int qq = li >> 2, pp = li & 3;
+    for (int qt = wave; qt < nqt; qt += 4) {
+        bf16x8 qn[2];
+        const bool has_next = qt + 4 < nqt;
+        if (has_next) load_q(qt + 4, qn);  // prefetch the next tile's queries
+
+        f32x4 st[ATT2_TILES];
+#pragma unroll
+        for (int t = 0; t < ATT2_TILES; ++t) {
+            st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int r = t * 16 + li;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = s * 4 + g;
+                const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[t], 0, 0, 0);
+            }
+            if (t & 1) asm volatile("" ::: "memory");  // cap the K-fragment loads in flight (VGPRs)
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < ATT2_TILES; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = t * 16 + g * 4 + j;
+                const float v = key < tokens ? st[t][j] * scale_log2e : -INFINITY;
+                st[t][j] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < ATT2_TILES; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float p = exp2f(st[t][j] - mx);
+                st[t][j] = p;
+                sum += p;
+            }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+
+        f32x4 o[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto vrow_addr = [&](int row, int d) {
+            // bytes 32d + 8pp of the row, through the V swizzle (16-B chunk ^ ((row>>1)&3)*2)
+            const int chunk = (2 * d + (pp >> 1)) ^ (((row >> 1) & 3) << 1);
+            return (lds_s16x4_t *)(Vs + row * 128 + chunk * 16 + (pp & 1) * 8);
+        };
+#pragma unroll
+        for (int tp = 0; tp < ATT2_TILES / 2; ++tp) {
+            const int t = tp * 2;
+            bf16x8 pf;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pf[j] = (__bf16)st[t][j];
+                pf[j + 4] = (__bf16)st[t + 1][j];
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + g * 4 + qq, d));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + 16 + g * 4 + qq, d));
+                const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
+            }
+            asm volatile("" ::: "memory");  // cap the V transposed reads in flight (VGPRs)
+        }
+        {   // last 16-key tile: K = 16 MFMA, lane group g holds keys 192 + 4g + j
+            constexpr int t = ATT2_TILES - 1;
+            s16x4 pf4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pf4[j] = __builtin_bit_cast(short, (__bf16)st[t][j]);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const s16x4 v4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + g * 4 + qq, d));
+                o[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(v4, pf4, o[d], 0, 0, 0);
+            }
+        }
+        const int q = qt * 16 + li;
+        if (q < tokens) {
+            const float inv = 1.0f / sum;
+            uint16_t *orow = out + ((int64_t)img * tokens + q) * H + h * HD;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+                *reinterpret_cast<uint2 *>(orow + d * 16 + g * 4) =
+                    make_uint2(pack_bf16x2(o[d][0] * inv, o[d][1] * inv), pack_bf16x2(o[d][2] * inv, o[d][3] * inv));
+        }
+        if (has_next) {
+            qf[0] = qn[0];
+            qf[1] = qn[1];
+        }
+    }
+}
+
 // Self-attention for one (image, head): S = 197 tokens, head dim 64.
 // K (XOR-swizzled 128-B rows) and V (160-B rows, conflict-free for the
 // transposed reads) of the head live in LDS; each wave takes 16-query tiles.
