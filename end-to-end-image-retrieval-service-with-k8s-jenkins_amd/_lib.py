@@ -26,6 +26,8 @@ RC_ERR_STATE = 5
 
 RC_F32, RC_F16, RC_BF16 = 0, 1, 2
 RC_TOPK_MAX = 256
+RC_SEARCH_AUTO, RC_SEARCH_SCAN, RC_SEARCH_MFMA = 0, 1, 2
+SEARCH_MODES = {"auto": RC_SEARCH_AUTO, "scan": RC_SEARCH_SCAN, "mfma": RC_SEARCH_MFMA}
 DTYPES = {"float32": RC_F32, "f32": RC_F32, "float16": RC_F16, "f16": RC_F16, "bfloat16": RC_BF16, "bf16": RC_BF16}
 
 
@@ -73,6 +75,8 @@ SIGNATURES = {
     "rc_index_fetch": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "rc_index_fetch_stored": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "rc_index_search": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "rc_index_search_ex": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _i32, _vp]),
+    "rc_index_gemm_timing_read": (C.c_int, [_vp, _pd, _pi64, _pd, _pi64]),
     "rc_index_fill_random": (C.c_int, [_vp, C.c_uint64, _i64, _i64, _vp]),
     "rc_topk_merge": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "rc_index_timing": (C.c_int, [_vp, _i32]),

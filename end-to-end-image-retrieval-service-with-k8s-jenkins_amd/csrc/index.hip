@@ -215,13 +215,18 @@ struct rc_index {
     int ws_nq = 0, ws_k = 0, ws_nblk = 0;
     float *qn = nullptr;
     uint64_t *partial = nullptr;
-    KernelTimer timer;
+    BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
+    KernelTimer timer;   // scan_topk_kernel launches (bytes)
+    KernelTimer gtimer;  // filter_gemm_kernel launches (flops)
+    int64_t fallbacks = 0;  // batched searches that needed the exact-scan fallback
 };
 
 namespace {
 
 constexpr int kNchSet[] = {1, 2, 3, 4, 6, 8, 12, 16};
 constexpr int kMaxBlocks = 2048;
+constexpr int kBatchMinQueries = 8;      // below this the HBM-bound scan wins (1-4 queries per pass)
+constexpr int64_t kBatchMinRows = 65536;  // tiny shards: the staged path's fixed cost dominates
 
 int pick_nch(int dim) {
     const int need = (dim + 127) / 128;
@@ -299,6 +304,52 @@ void dispatch_dtype(int dtype, F &&f) {
     }
 }
 
+
+void scan_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores, int64_t *out_rows,
+                 hipStream_t s) {
+    // queries per scan pass: a power of two the kernel is instantiated for (1, 2, 4)
+    int qb = 1;
+    while (qb * 2 <= std::min(nq, scan_max_qb(h->nch, k))) qb *= 2;
+    const int nq_pad = (nq + qb - 1) / qb * qb;  // every scan pass runs qb real-or-zero query slots
+    ensure_workspace(h, nq_pad, k);
+    hipLaunchKernelGGL(normalize_queries_kernel, dim3(nq_pad), dim3(64), 0, s, queries, nq, h->dim, h->ld, h->qn);
+    RC_LAUNCH_CHECK();
+    int nblk = (int)std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (n_rows + 511) / 512));
+    int64_t rpb = (n_rows + nblk - 1) / nblk;
+    rpb = ((rpb + 31) / 32) * 32;
+    if (rpb == 0) rpb = 32;
+    nblk = (int)std::max<int64_t>(1, (n_rows + rpb - 1) / rpb);
+    const double bytes = (double)n_rows * h->ld * dtype_size(h->dtype);
+    if (h->timer.enabled) h->timer.create();
+    for (int q0 = 0; q0 < nq_pad; q0 += qb) {
+        const int slot = h->timer.begin(s);
+        ScanArgs a{h->rows, h->ld, h->nch, n_rows, rpb, nblk, h->qn, q0, qb, nq_pad, k, h->partial, s};
+        launch_scan(h, a);
+        h->timer.end(slot, s, bytes);
+    }
+    launch_merge_partials(h, nblk, nq, nq_pad, k, scores, out_rows, s);
+}
+
+// Batched MFMA search, then the exact scan for any query whose candidates
+// overflowed (one host sync per call: the flags decide what to re-run).
+void batched_search_exact(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
+                          int64_t *out_rows, hipStream_t s) {
+    h->bws.ensure(nq, k, h->ld, (int)dtype_size(h->dtype));
+    BatchPlan p{h->rows, h->dtype, h->dim, h->nch, h->ld, n_rows, h->row_base, queries, nq, k, scores, out_rows};
+    if (h->gtimer.enabled) h->gtimer.create();
+    batched_search(p, h->bws, s, h->gtimer.enabled ? &h->gtimer : nullptr);
+    RC_HIP(hipMemcpyAsync(h->bws.ovf_host, h->bws.ovf, sizeof(int), hipMemcpyDeviceToHost, s));
+    RC_HIP(hipStreamSynchronize(s));
+    if (*h->bws.ovf_host == 0) return;
+    std::vector<int> flags(nq);
+    RC_HIP(hipMemcpyAsync(flags.data(), h->bws.flags, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, s));
+    RC_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < nq; ++q)
+        if (flags[q]) scan_search(h, queries + (int64_t)q * h->dim, 1, n_rows, k, scores + (int64_t)q * k,
+                                  out_rows + (int64_t)q * k, s);
+    h->fallbacks += 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -324,9 +375,11 @@ int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t ro
         h->capacity = capacity;
         h->row_base = row_base;
         try {
-            h->rows = dmalloc((size_t)capacity * h->ld * dtype_size(dtype));
+            // whole 256-row tiles: the batched search reads row tiles without a bounds check
+            const int64_t cap_pad = (capacity + INDEX_ROW_PAD - 1) / INDEX_ROW_PAD * INDEX_ROW_PAD;
+            h->rows = dmalloc((size_t)cap_pad * h->ld * dtype_size(dtype));
             h->norms = (float *)dmalloc((size_t)capacity * sizeof(float));
-            RC_HIP(hipMemset(h->rows, 0, (size_t)capacity * h->ld * dtype_size(dtype)));
+            RC_HIP(hipMemset(h->rows, 0, (size_t)cap_pad * h->ld * dtype_size(dtype)));
             RC_HIP(hipMemset(h->norms, 0, (size_t)capacity * sizeof(float)));
             ensure_workspace(h, 4, 16);
         } catch (...) {
@@ -346,6 +399,8 @@ int rc_index_destroy(rc_index *h) {
         if (!h) return;
         DeviceScope ds(h->device);
         h->timer.destroy();
+        h->gtimer.destroy();
+        h->bws.release();
         dfree(h->rows);
         dfree(h->norms);
         dfree(h->qn);
@@ -430,37 +485,33 @@ int rc_index_fill_random(rc_index *h, uint64_t seed, int64_t row0, int64_t n, vo
 
 int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores, int64_t *out_rows,
                     void *stream) {
+    return rc_index_search_ex(h, queries, nq, n_rows, k, scores, out_rows, RC_SEARCH_AUTO, stream);
+}
+
+int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
+                       int64_t *out_rows, int mode, void *stream) {
     return guard([&] {
         RC_REQUIRE(h, RC_ERR_INVALID, "null index");
         RC_REQUIRE(nq >= 0, RC_ERR_INVALID, "negative query count");
         RC_REQUIRE(k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "top_k must be in [1, 256]");
         RC_REQUIRE(n_rows >= 0 && n_rows <= h->capacity, RC_ERR_INVALID, "n_rows out of range");
+        RC_REQUIRE(mode == RC_SEARCH_AUTO || mode == RC_SEARCH_SCAN || mode == RC_SEARCH_MFMA, RC_ERR_INVALID,
+                   "unknown search mode");
         if (nq == 0) return;
         RC_REQUIRE(queries && scores && out_rows, RC_ERR_INVALID, "null buffer");
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceScope ds(h->device);
         hipStream_t s = (hipStream_t)stream;
-        // queries per scan pass: a power of two the kernel is instantiated for (1, 2, 4)
-        int qb = 1;
-        while (qb * 2 <= std::min(nq, scan_max_qb(h->nch, k))) qb *= 2;
-        const int nq_pad = (nq + qb - 1) / qb * qb;  // every scan pass runs qb real-or-zero query slots
-        ensure_workspace(h, nq_pad, k);
-        hipLaunchKernelGGL(normalize_queries_kernel, dim3(nq_pad), dim3(64), 0, s, queries, nq, h->dim, h->ld, h->qn);
-        RC_LAUNCH_CHECK();
-        int nblk = (int)std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (n_rows + 511) / 512));
-        int64_t rpb = (n_rows + nblk - 1) / nblk;
-        rpb = ((rpb + 31) / 32) * 32;
-        if (rpb == 0) rpb = 32;
-        nblk = (int)std::max<int64_t>(1, (n_rows + rpb - 1) / rpb);
-        const double bytes = (double)n_rows * h->ld * dtype_size(h->dtype);
-        if (h->timer.enabled) h->timer.create();
-        for (int q0 = 0; q0 < nq_pad; q0 += qb) {
-            const int slot = h->timer.begin(s);
-            ScanArgs a{h->rows, h->ld, h->nch, n_rows, rpb, nblk, h->qn, q0, qb, nq_pad, k, h->partial, s};
-            launch_scan(h, a);
-            h->timer.end(slot, s, bytes);
+        const bool mfma_ok = h->dtype != RC_F32 && n_rows > 0;
+        RC_REQUIRE(mode != RC_SEARCH_MFMA || mfma_ok, RC_ERR_UNSUPPORTED,
+                   "batched MFMA search needs an f16/bf16 index with at least one row");
+        const bool use_mfma = mode == RC_SEARCH_MFMA ||
+                              (mode == RC_SEARCH_AUTO && mfma_ok && nq >= kBatchMinQueries && n_rows >= kBatchMinRows);
+        if (!use_mfma) {
+            scan_search(h, queries, nq, n_rows, k, scores, out_rows, s);
+            return;
         }
-        launch_merge_partials(h, nblk, nq, nq_pad, k, scores, out_rows, s);
+        batched_search_exact(h, queries, nq, n_rows, k, scores, out_rows, s);
     });
 }
 
@@ -487,8 +538,12 @@ int rc_index_timing(rc_index *h, int enable) {
         RC_REQUIRE(h, RC_ERR_INVALID, "null index");
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceScope ds(h->device);
-        if (enable) h->timer.create();
+        if (enable) {
+            h->timer.create();
+            h->gtimer.create();
+        }
         h->timer.enabled = enable != 0;
+        h->gtimer.enabled = enable != 0;
     });
 }
 
@@ -504,6 +559,22 @@ int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, doubl
         h->timer.total_ms = 0;
         h->timer.launches = 0;
         h->timer.work = 0;
+    });
+}
+
+int rc_index_gemm_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *flops, int64_t *fallbacks) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        h->gtimer.flush();
+        if (total_ms) *total_ms = h->gtimer.total_ms;
+        if (launches) *launches = h->gtimer.launches;
+        if (flops) *flops = h->gtimer.work;
+        if (fallbacks) *fallbacks = h->fallbacks;
+        h->gtimer.total_ms = 0;
+        h->gtimer.launches = 0;
+        h->gtimer.work = 0;
     });
 }
 

@@ -89,6 +89,47 @@ void launch_scan_f32(const ScanArgs &a);
 void launch_scan_f16(const ScanArgs &a);
 void launch_scan_bf16(const ScanArgs &a);
 
+// ------------------------------------------- batched MFMA search (search_mfma.hip)
+constexpr int BATCH_CAND_CAP = 4096;  // candidate slots per query per stage
+constexpr int INDEX_ROW_PAD = 256;    // row storage is allocated in whole 256-row tiles
+
+struct BatchWs {
+    int nq_cap = 0, k_cap = 0;
+    int64_t ld_cap = 0;
+    int cap = BATCH_CAND_CAP;
+    float *qn = nullptr;        // [nq_cap][ld] normalised queries (f32)
+    void *qh = nullptr;         // [nq_cap][ld] queries in the storage dtype (MFMA operand)
+    float *eps = nullptr;       // [nq_cap] bound on |s' - s|
+    float *thr = nullptr;       // [nq_cap] current filter threshold
+    uint32_t *cnt = nullptr;    // [nq_cap] candidates appended this stage
+    uint32_t *cand = nullptr;   // [nq_cap][cap] candidate rows
+    uint64_t *keys = nullptr;   // [nq_cap][k_cap] running top-k keys (sorted)
+    int *flags = nullptr;       // [nq_cap] 1 = candidate overflow, exact fallback needed
+    int *ovf = nullptr;         // number of overflowed queries (device)
+    int *ovf_host = nullptr;    // pinned copy
+    void ensure(int nq, int k, int64_t ld, int dtype_bytes);
+    void release();
+};
+
+struct BatchPlan {
+    const void *rows;
+    int dtype;
+    int dim;
+    int nch;
+    int64_t ld;
+    int64_t n_rows;
+    int64_t row_base;
+    const float *queries;  // device f32 [nq][dim]
+    int nq;
+    int k;
+    float *out_scores;
+    int64_t *out_rows;
+};
+
+// Enqueue the staged filter-GEMM / rescore search on `s` (no host sync).
+void batched_search(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer);
+int batch_stage_ratio(int k, int cap);
+
 #if defined(SCAN_INSTANTIATE)
 // qn holds nq_total (a multiple of QB) query rows, zero beyond the caller's
 // queries, so every slot is computed and stored unconditionally.

@@ -1,0 +1,489 @@
+// search_mfma.hip — batched exact cosine top-k on CDNA4 matrix cores
+// (BASELINE config 4: 1024 queries x top-100 over a 125M x 512 fp16 shard).
+//
+// Replaces index.query(vector, top_k) (retriever/utils.py:62-64) for a batch of
+// query vectors; the single-query path is the HBM-bound scan (index_common.h).
+//
+// A query batch is a GEMM: S = Q · Xᵀ (queries x rows, K = ld).  S is never
+// materialised.  The search runs in STAGES over growing row ranges
+// [0, b1), [b1, b2), ... with b(i+1) = g · b(i):
+//   filter_gemm_kernel  MFMA (f16/bf16 in, f32 acc) 256 queries x 256 rows x 64
+//                       tiles; the epilogue keeps (query, row) iff
+//                       s'(q,r) >= thr[q] and appends the row to the query's
+//                       candidate list (atomic counter, capacity CAND_CAP);
+//   rescore_kernel      per query: exact f32 score of every candidate (the same
+//                       arithmetic as the single-query scan, so both paths give
+//                       bit-identical scores), wavefront top-k merge with the
+//                       running top-k keys, thr[q] = kth_best - eps[q].
+// Why it is exact: s' uses the query rounded to the storage dtype q̂.  For a
+// stored row x̂ (||x̂|| <= 1.01) |s' - s| <= ||q - q̂||·||x̂|| + two f32
+// accumulation bounds (512·2^-24 each) =: eps[q] (computed per query).  The
+// running kth best T of the rows seen so far is a lower bound of the final kth
+// best, so any row of the final top-k has s >= T, hence s' >= T - eps: the
+// filter never drops a true member.  The stage ratio g keeps the expected
+// candidates per stage at ≈ k·(g-1) ≪ CAND_CAP.  A query whose candidates
+// overflow CAND_CAP in some stage (adversarial / duplicate-heavy data) is
+// flagged and re-run by the host through the exact scan (index.hip).
+//
+// HBM layout: rows [cap256][ld] T (capacity rounded up to 256 rows so whole
+// row tiles are readable), queries q̂ [nqb*256][ld] T (zero rows past nq).
+#include <algorithm>
+#include <vector>
+
+#include "index_common.h"
+
+namespace rc {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename T> struct MfmaOp;
+template <> struct MfmaOp<f16_t> {
+    typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+    static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct MfmaOp<bf16_t> {
+    typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+    static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+
+constexpr int SB_TILE = 256;  // queries per query block = rows per row tile
+
+// ------------------------------------------------------ query preparation --
+// One wave per query slot q < nq_pad: qn = q/||q|| (f32, the exact rescoring
+// operand, same arithmetic as normalize_queries_kernel), qh = cast(qn) (the
+// MFMA operand), eps = error bound of s' (see header), thr = -inf (real
+// query) or +inf (padding slot: never appends).
+template <typename T>
+__global__ __launch_bounds__(64) void prepare_queries_kernel(const float *__restrict__ q, int nq, int dim, int64_t ld,
+                                                            float *__restrict__ qn, T *__restrict__ qh,
+                                                            float *__restrict__ eps, float *__restrict__ thr) {
+    const int lane = threadIdx.x;
+    const int qi = blockIdx.x;
+    const bool valid = qi < nq;
+    const float *src = q + (int64_t)(valid ? qi : 0) * dim;
+    float ss = 0.f;
+    for (int c = lane; c < dim; c += 64) ss = valid ? fmaf(src[c], src[c], ss) : 0.f;
+    ss = wave_sum(ss);
+    const float inv = ss > 0.f ? 1.0f / sqrtf(ss) : 0.f;
+    float err = 0.f;
+    for (int c = lane; c < ld; c += 64) {
+        const float v = (valid && c < dim) ? src[c] * inv : 0.f;
+        const T h = Elem<T>::cast(v);
+        const float d = v - Elem<T>::load(&h, 0);
+        err = fmaf(d, d, err);
+        if (valid) qn[(int64_t)qi * ld + c] = v;
+        qh[(int64_t)qi * ld + c] = h;
+    }
+    err = wave_sum(err);
+    if (lane == 0) {
+        eps[qi] = 1.01f * sqrtf(err) + 6.5e-5f;
+        thr[qi] = valid ? -INFINITY : INFINITY;
+    }
+}
+
+// ------------------------------------------------------- filter GEMM -------
+struct FilterArgs {
+    const void *rows;  // [>= roundup(r_end, 256)][ld]
+    const void *qh;    // [nqb*256][ld]
+    int64_t ld;
+    int nkt;           // ld / 64
+    int64_t r_begin;   // multiple of 256
+    int64_t r_end;
+    int64_t tiles_per_chunk;
+    int nqb;
+    const float *thr;  // [nqb*256]
+    uint32_t *cnt;     // [nqb*256]
+    uint32_t *cand;    // [nqb*256][cap]
+    int cap;
+};
+
+// 256x256x64 tile, 512 threads = 8 waves in two groups (G0 = waves 0-3 own
+// query rows 0-127, G1 = waves 4-7 rows 128-255; wave w and w+4 share a SIMD).
+// Each wave owns 128 queries x 64 index rows as 4 quadrants of 64x32.  The
+// (row tile, K-tile) steps of the block's chunk are one flattened sequence, so
+// the next row tile's first K-tile streams in under the current tile's last
+// MFMAs.  A K-tile is 4 phases; each phase is an M segment (ds_read the
+// quadrant's fragments, issue this wave's LDS-DMA share of the next step,
+// lgkmcnt(0)) and a C segment (16 MFMAs), each closed by a block barrier; G1
+// runs one segment behind G0 so one wave per SIMD is in MFMAs while its partner
+// reads LDS.  MFMA roles: A operand = index rows, B operand = queries, so a
+// lane's accumulator holds 4 consecutive ROWS of one query: the epilogue tests
+// one per-lane threshold against 16 values at a time.
+// Block → (query block, chunk): blocks b and b+8 share an XCD; the nqb blocks
+// of one chunk are consecutive on one XCD, so each row tile is read from HBM
+// once and served to the other query blocks from that XCD's L2.
+template <typename T>
+__global__ __launch_bounds__(512, 1) void filter_gemm_kernel(FilterArgs a) {
+    using Op = MfmaOp<T>;
+    using v8 = typename Op::v8;
+    constexpr int BK = 64;
+    constexpr int A_BYTES = SB_TILE * BK * 2, STAGE = 2 * A_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int b = blockIdx.x, xcd = b & 7, jx = b >> 3;
+    const int qb = jx % a.nqb;
+    const int64_t chunk = (int64_t)(jx / a.nqb) * 8 + xcd;
+    const int64_t rt_total = (a.r_end - a.r_begin + SB_TILE - 1) / SB_TILE;
+    const int64_t rt0 = chunk * a.tiles_per_chunk;
+    const int64_t rt1 = min(rt_total, rt0 + a.tiles_per_chunk);
+    if (rt0 >= rt1) return;  // block-uniform
+    const int nkt = a.nkt;
+    const int64_t ld = a.ld;
+    const int64_t nsteps = (rt1 - rt0) * nkt;
+    const uint16_t *Ag = (const uint16_t *)a.qh + (int64_t)qb * SB_TILE * ld;
+    const uint16_t *Rg = (const uint16_t *)a.rows + (a.r_begin + rt0 * SB_TILE) * ld;
+
+    // 64 pieces of 1 KB per step (queries: 0-31, rows: 32-63); wave w owns pieces w + 8 i.
+    auto stage4 = [&](int buf, int64_t step, int i0) {
+        uint8_t *base = smem + buf * STAGE;
+        const int64_t rt = step / nkt;
+        const int k0 = (int)(step - rt * nkt) * BK;
+        const uint16_t *Wg = Rg + rt * SB_TILE * ld;
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_q = i < 4;
+            const int r = (is_q ? piece : piece - 32) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const uint16_t *src = (is_q ? Ag : Wg) + (int64_t)r * ld + k0 + c * 8;
+            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)(base + piece * 1024), 16, 0, 0);
+        }
+    };
+    auto bar = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    // thresholds of this lane's 8 query rows: q = qb*256 + grp*128 + mq*64 + mi*16 + li
+    float thr[2][4];
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) thr[mq][mi] = a.thr[qb * SB_TILE + grp * 128 + mq * 64 + mi * 16 + li];
+
+    f32x4_t acc[2][2][4][2];
+    auto zero_acc = [&] {
+#pragma unroll
+        for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+            for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+                for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                    for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    zero_acc();
+
+    stage4(0, 0, 0);
+    stage4(0, 0, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: G1 one segment behind
+
+    v8 af[4][2], wf[2][2];  // queries [mi][s], rows [ni][s]
+    for (int64_t step = 0; step < nsteps; ++step) {
+        const int cur = (int)(step & 1);
+        const uint8_t *As = smem + cur * STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+        const bool more = step + 1 < nsteps;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mq = p >> 1;
+            const int nq = (p == 1 || p == 2);
+            if (p == 0 || p == 2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        const int c = s * 4 + g;
+                        af[mi][s] = *reinterpret_cast<const v8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                    const int c = s * 4 + g;
+                    wf[ni][s] = *reinterpret_cast<const v8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                }
+            if (more && p < 2) stage4(cur ^ 1, step + 1, p * 4);
+            if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        acc[mq][nq][mi][ni] = Op::mma(wf[ni][s], af[mi][s], acc[mq][nq][mi][ni]);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+
+        if ((step + 1) % nkt == 0) {
+            // ---- epilogue of row tile rt: lane holds S[q][r .. r+3] for 8 q x 4 r-groups
+            const int64_t rt = rt0 + step / nkt;
+            const int64_t rbase = a.r_begin + rt * SB_TILE + wc * 64 + 4 * g;
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    const float t = thr[mq][mi];
+                    float m = -INFINITY;
+#pragma unroll
+                    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                        for (int ni = 0; ni < 2; ++ni) {
+                            const f32x4_t v = acc[mq][nq][mi][ni];
+                            m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+                        }
+                    if (__ballot(m >= t) == 0) continue;  // wave-uniform: the common case
+                    if (m >= t) {
+                        const int q = qb * SB_TILE + grp * 128 + mq * 64 + mi * 16 + li;
+#pragma unroll
+                        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    const int64_t row = rbase + nq * 32 + ni * 16 + j;
+                                    if (acc[mq][nq][mi][ni][j] >= t && row < a.r_end) {
+                                        const uint32_t pos = atomicAdd(&a.cnt[q], 1u);
+                                        if ((int)pos < a.cap) a.cand[(int64_t)q * a.cap + pos] = (uint32_t)row;
+                                    }
+                                }
+                    }
+                }
+            zero_acc();
+        }
+    }
+    if (grp == 0) bar();  // balance the stagger barrier
+}
+
+// ------------------------------------------------------- exact rescoring --
+// One block per query.  Candidates are scored exactly as scan_topk_kernel
+// scores a row (16 lanes per row, 16-B chunks, f32 FMA in chunk order, DPP
+// reduction), merged with the running top-k keys, and the threshold for the
+// next stage is set.  Overflow (more candidates than cap) is flagged for the
+// host's exact fallback; the counter is reset for the next stage.
+template <typename T, int NCH, int CAP>
+__global__ __launch_bounds__(256) void rescore_kernel(const T *__restrict__ rows, int64_t ld, const float *__restrict__ qn,
+                                                     int k, uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cand,
+                                                     int cap, uint64_t *__restrict__ keys, const float *__restrict__ eps,
+                                                     float *__restrict__ thr, int *__restrict__ flags,
+                                                     int *__restrict__ ovf_total, int final_pass, int64_t row_base,
+                                                     float *__restrict__ out_scores, int64_t *__restrict__ out_rows) {
+    constexpr int EPC = 16 / sizeof(T);
+    constexpr int CPL = NCH * 128 / (16 * EPC);
+    constexpr int U = 2;
+    __shared__ uint64_t lds[4][CAP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 15, rg = lane >> 4;
+    const int qi = blockIdx.x;
+
+    float q[CPL][EPC];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) q[i][e] = qn[(int64_t)qi * ld + (sub + 16 * i) * EPC + e];
+
+    const uint32_t n = cnt[qi];
+    const int nn = (int)min<uint32_t>(n, (uint32_t)cap);
+    const uint32_t *cl = cand + (int64_t)qi * cap;
+    const uint4 *base4 = reinterpret_cast<const uint4 *>(rows);
+    const int64_t ld4 = ld / EPC;
+
+    WaveTopK<CAP> tk;
+    tk.init(as_lds(&lds[wave][0]), k);
+    if (wave == 0) {  // the running top-k of the earlier stages
+        for (int j = 0; j < k; j += 64) {
+            const uint64_t key = (j + lane < k) ? keys[(int64_t)qi * k + j + lane] : KEY_EMPTY;
+            tk.reserve(64);
+            tk.push(key != KEY_EMPTY, key);
+        }
+    }
+    for (int j0 = wave * 4 * U; j0 < nn; j0 += 16 * U) {
+        uint4 x[U][CPL];
+        uint32_t rr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * 4 + rg;
+            rr[u] = cl[j < nn ? j : 0];
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) x[u][i] = base4[(int64_t)rr[u] * ld4 + sub + 16 * i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * 4 + rg;
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) {
+                float f[EPC];
+                unpack16<T>(x[u][i], f);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) acc = fmaf(f[e], q[i][e], acc);
+            }
+            const float s = sum16(acc);
+            tk.reserve(4);
+            tk.push(sub == 0 && j < nn, make_key(s, rr[u]));
+        }
+    }
+    tk.compact();
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < 4; ++w)
+            for (int j = 0; j < k; j += 64) {
+                const uint64_t key = (j + lane < k) ? as_lds(&lds[w][0])[j + lane] : KEY_EMPTY;
+                tk.reserve(64);
+                tk.push(key != KEY_EMPTY, key);
+            }
+        tk.compact();
+        for (int j = lane; j < k; j += 64) {
+            const uint64_t key = tk.buf[j];
+            keys[(int64_t)qi * k + j] = key;
+            if (final_pass) {
+                const bool ok = key != KEY_EMPTY;
+                out_scores[(int64_t)qi * k + j] = ok ? key_score(key) : -INFINITY;
+                out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) : -1;
+            }
+        }
+        if (lane == 0) {
+            thr[qi] = tk.count >= k ? key_score(tk.buf[k - 1]) - eps[qi] : -INFINITY;
+            if (n > (uint32_t)cap) {
+                flags[qi] = 1;
+                atomicAdd(ovf_total, 1);
+            }
+            cnt[qi] = 0;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host ---
+template <typename T, int NCH>
+void launch_rescore_cap(const BatchPlan &p, const BatchWs &ws, int final_pass, hipStream_t s) {
+    const int cap = topk_cap(p.k);
+#define RC_RESCORE(CAPV)                                                                                         \
+    hipLaunchKernelGGL((rescore_kernel<T, NCH, CAPV>), dim3(p.nq), dim3(256), 0, s, (const T *)p.rows, p.ld, ws.qn, \
+                       p.k, ws.cnt, ws.cand, ws.cap, ws.keys, ws.eps, ws.thr, ws.flags, ws.ovf, final_pass, p.row_base,  \
+                       p.out_scores, p.out_rows)
+    if (cap <= 128) RC_RESCORE(128);
+    else if (cap <= 256) RC_RESCORE(256);
+    else RC_RESCORE(512);
+#undef RC_RESCORE
+    RC_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipStream_t s) {
+    switch (p.nch) {
+        case 1: return launch_rescore_cap<T, 1>(p, ws, final_pass, s);
+        case 2: return launch_rescore_cap<T, 2>(p, ws, final_pass, s);
+        case 3: return launch_rescore_cap<T, 3>(p, ws, final_pass, s);
+        case 4: return launch_rescore_cap<T, 4>(p, ws, final_pass, s);
+        case 6: return launch_rescore_cap<T, 6>(p, ws, final_pass, s);
+        case 8: return launch_rescore_cap<T, 8>(p, ws, final_pass, s);
+        case 12: return launch_rescore_cap<T, 12>(p, ws, final_pass, s);
+        case 16: return launch_rescore_cap<T, 16>(p, ws, final_pass, s);
+        default: throw Error(RC_ERR_UNSUPPORTED, "unsupported row width");
+    }
+}
+
+int batch_stage_ratio(int k, int cap) {
+    const int g = cap / (5 * k / 2 + 1);
+    return std::max(2, std::min(64, g));
+}
+
+template <typename T>
+void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
+    const int nqb = (p.nq + SB_TILE - 1) / SB_TILE;
+    const int nq_pad = nqb * SB_TILE;
+    hipLaunchKernelGGL(prepare_queries_kernel<T>, dim3(nq_pad), dim3(64), 0, s, p.queries, p.nq, p.dim, p.ld, ws.qn,
+                       (T *)ws.qh, ws.eps, ws.thr);
+    RC_LAUNCH_CHECK();
+    RC_HIP(hipMemsetAsync(ws.keys, 0xFF, (size_t)p.nq * p.k * sizeof(uint64_t), s));
+    RC_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)nq_pad * sizeof(uint32_t), s));
+    RC_HIP(hipMemsetAsync(ws.flags, 0, (size_t)p.nq * sizeof(int), s));
+    RC_HIP(hipMemsetAsync(ws.ovf, 0, sizeof(int), s));
+
+    const int g = batch_stage_ratio(p.k, ws.cap);
+    int64_t b0 = 0, b1 = std::min<int64_t>(p.n_rows, ws.cap);  // stage 1: every row is a candidate
+    while (b0 < p.n_rows) {
+        const int64_t rt_total = (b1 - b0 + SB_TILE - 1) / SB_TILE;
+        int64_t nchunk = std::min<int64_t>(rt_total, std::max<int64_t>(1, (256 + nqb - 1) / nqb));
+        nchunk = (nchunk + 7) / 8 * 8;
+        const int64_t tpc = (rt_total + nchunk - 1) / nchunk;
+        FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), b0, b1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
+        const int slot = timer ? timer->begin(s) : -1;
+        hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
+        RC_LAUNCH_CHECK();
+        if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(b1 - b0) * (double)p.ld);
+        launch_rescore<T>(p, ws, b1 == p.n_rows ? 1 : 0, s);
+        b0 = b1;
+        b1 = std::min<int64_t>(p.n_rows, b1 * g);
+    }
+}
+
+void batched_search(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
+    RC_REQUIRE(p.ld % 64 == 0, RC_ERR_UNSUPPORTED, "batched search needs ld % 64 == 0");
+    RC_REQUIRE(p.n_rows > 0, RC_ERR_INVALID, "batched search over an empty range");
+    if (p.dtype == RC_F16) return run_batched<f16_t>(p, ws, s, timer);
+    if (p.dtype == RC_BF16) return run_batched<bf16_t>(p, ws, s, timer);
+    throw Error(RC_ERR_UNSUPPORTED, "batched MFMA search needs an f16 or bf16 index");
+}
+
+void BatchWs::ensure(int nq, int k, int64_t ld, int dtype_bytes) {
+    const int nq_pad = (nq + SB_TILE - 1) / SB_TILE * SB_TILE;
+    if (nq_pad <= nq_cap && k <= k_cap && ld <= ld_cap) return;
+    release();
+    nq_cap = std::max(nq_pad, 256);
+    k_cap = std::max(k, 16);
+    ld_cap = ld;
+    qn = (float *)dmalloc((size_t)nq_cap * ld * sizeof(float));
+    qh = dmalloc((size_t)nq_cap * ld * dtype_bytes);
+    eps = (float *)dmalloc((size_t)nq_cap * sizeof(float));
+    thr = (float *)dmalloc((size_t)nq_cap * sizeof(float));
+    cnt = (uint32_t *)dmalloc((size_t)nq_cap * sizeof(uint32_t));
+    cand = (uint32_t *)dmalloc((size_t)nq_cap * cap * sizeof(uint32_t));
+    keys = (uint64_t *)dmalloc((size_t)nq_cap * k_cap * sizeof(uint64_t));
+    flags = (int *)dmalloc((size_t)nq_cap * sizeof(int));
+    ovf = (int *)dmalloc(sizeof(int));
+    RC_HIP(hipHostMalloc((void **)&ovf_host, sizeof(int), hipHostMallocDefault));
+}
+
+void BatchWs::release() {
+    dfree(qn);
+    dfree(qh);
+    dfree(eps);
+    dfree(thr);
+    dfree(cnt);
+    dfree(cand);
+    dfree(keys);
+    dfree(flags);
+    dfree(ovf);
+    if (ovf_host) (void)hipHostFree(ovf_host);
+    qn = nullptr;
+    qh = nullptr;
+    eps = thr = nullptr;
+    cnt = cand = nullptr;
+    keys = nullptr;
+    flags = ovf = ovf_host = nullptr;
+    nq_cap = k_cap = 0;
+    ld_cap = 0;
+}
+
+}  // namespace rc

@@ -97,8 +97,13 @@ class DeviceIndex:
         check(self.lib.rc_index_fetch(self.handle, ptr(rows), rows.numel(), ptr(out), stream_ptr(stream)))
         return out
 
-    def search(self, queries: torch.Tensor, k: int, n_rows: int, stream=None, out=None):
-        """Exact cosine top-k over rows [0, n_rows): (scores f32 [nq,k], global rows i64 [nq,k])."""
+    def search(self, queries: torch.Tensor, k: int, n_rows: int, stream=None, out=None, mode: str = "auto"):
+        """Exact cosine top-k over rows [0, n_rows): (scores f32 [nq,k], global rows i64 [nq,k]).
+
+        ``mode``: "scan" (HBM-bound streaming scan), "mfma" (batched filter GEMM +
+        exact rescoring, f16/bf16 index) or "auto" (MFMA for >= 8 queries)."""
+        if mode not in _lib.SEARCH_MODES:
+            raise ValueError(f"unknown search mode {mode!r}")
         q = self._vecs(queries)
         nq = q.shape[0]
         if out is None:
@@ -106,7 +111,8 @@ class DeviceIndex:
             rows = torch.empty((nq, k), dtype=torch.int64, device=self.device)
         else:
             scores, rows = out
-        check(self.lib.rc_index_search(self.handle, ptr(q), nq, int(n_rows), int(k), ptr(scores), ptr(rows), stream_ptr(stream)))
+        check(self.lib.rc_index_search_ex(self.handle, ptr(q), nq, int(n_rows), int(k), ptr(scores), ptr(rows),
+                                          _lib.SEARCH_MODES[mode], stream_ptr(stream)))
         return scores, rows
 
     def fill_random(self, seed: int, row0: int, n: int, stream=None) -> None:
@@ -125,11 +131,22 @@ class DeviceIndex:
         check(self.lib.rc_index_timing(self.handle, 1 if enable else 0))
 
     def timing_read(self):
+        """Scan kernel: (total ms, launches, algorithmic bytes) since the last read."""
         ms = _lib.C.c_double()
         n = _lib.C.c_int64()
         b = _lib.C.c_double()
         check(self.lib.rc_index_timing_read(self.handle, _lib.C.byref(ms), _lib.C.byref(n), _lib.C.byref(b)))
         return ms.value, n.value, b.value
+
+    def gemm_timing_read(self):
+        """Batched filter GEMM: (total ms, launches, flops, fallback count) since the last read."""
+        ms = _lib.C.c_double()
+        n = _lib.C.c_int64()
+        f = _lib.C.c_double()
+        fb = _lib.C.c_int64()
+        check(self.lib.rc_index_gemm_timing_read(self.handle, _lib.C.byref(ms), _lib.C.byref(n), _lib.C.byref(f),
+                                                 _lib.C.byref(fb)))
+        return ms.value, n.value, f.value, fb.value
 
 
 def topk_merge(scores: torch.Tensor, rows: torch.Tensor, k: int, stream=None):

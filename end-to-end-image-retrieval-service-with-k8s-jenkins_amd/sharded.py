@@ -55,9 +55,11 @@ class ShardedIndex:
         self.local.fill_random(seed, 0, n_local)
         self.n_local = n_local
 
-    def search(self, queries: torch.Tensor, k: int):
-        """Exact global top-k for the (replicated) queries: (scores [nq,k], global rows [nq,k]) on every rank."""
-        s, r = self.local.search(queries, k, self.n_local)
+    def search(self, queries: torch.Tensor, k: int, **kw):
+        """Exact global top-k for the (replicated) queries: (scores [nq,k], global rows [nq,k]) on every rank.
+
+        ``kw`` goes to the shard's search (e.g. ``mode="mfma"`` for the batched MFMA path)."""
+        s, r = self.local.search(queries, k, self.n_local, **kw)
         if self.world == 1:
             return s, r
         nq = s.shape[0]

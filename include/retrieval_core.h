@@ -99,6 +99,21 @@ int rc_index_fetch_stored(rc_index *h, const int64_t *rows, int64_t n, float *ou
 int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k,
                     float *scores, int64_t *out_rows, void *stream);
 
+/* Search algorithm selection for rc_index_search_ex (same results either way):
+ *   RC_SEARCH_SCAN — HBM-bound streaming scan, 1-4 queries per pass over the rows;
+ *   RC_SEARCH_MFMA — batched: query-block x row-tile MFMA GEMM (f16/bf16 index only)
+ *                    whose epilogue keeps candidates within a proven error bound
+ *                    of the running kth score, exact f32 rescoring of candidates;
+ *                    blocks the calling thread once (overflow check);
+ *   RC_SEARCH_AUTO — MFMA for >= 8 queries on an f16/bf16 index of >= 64k rows.
+ * This is the batched form of index.query (retriever/utils.py:62-64) that
+ * BASELINE config 4 (1024 queries, top-100) exercises. */
+#define RC_SEARCH_AUTO 0
+#define RC_SEARCH_SCAN 1
+#define RC_SEARCH_MFMA 2
+int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows, int k,
+                       float *scores, int64_t *out_rows, int mode, void *stream);
+
 /* Synthetic rows for benchmarks (no reference counterpart): rows
  * [row0, row0+n) get uniform[-1,1) values from a counter-based hash of
  * (seed, row, col), normalised and cast like an upsert. */
@@ -171,6 +186,9 @@ int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, con
 /* Index-side timing of the dominant search kernel (scan), same conventions. */
 int rc_index_timing(rc_index *h, int enable);
 int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *bytes);
+/* Same for the batched search's filter GEMM (flops = 2 * query slots * rows * ld per launch);
+ * fallbacks = batched calls that re-ran an overflowed query through the exact scan. */
+int rc_index_gemm_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *flops, int64_t *fallbacks);
 
 #ifdef __cplusplus
 }

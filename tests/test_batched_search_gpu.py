@@ -1,0 +1,148 @@
+"""GPU parity of the batched MFMA search (filter GEMM + exact rescoring) — BASELINE config 4.
+
+Reference path replaced: Pinecone ``index.query`` (``retriever/utils.py:59-66``)
+for a batch of query vectors.  Bars (north star): top-k sets identical to the
+float64 oracle except ties within 1e-5, scores within 1e-5 of the oracle's
+score of the returned rows, recall@k = 1.0.  Stronger, size-independent
+property checked at every size: the MFMA path returns EXACTLY (bit for bit)
+what the single-query scan returns — both score candidates with the same f32
+arithmetic, so any row the filter wrongly dropped would show up as a diff.
+"""
+import numpy as np
+import pytest
+
+from conftest import import_pkg
+from oracle.cosine_topk import cosine_topk, topk_equal_modulo_ties
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def idxmod(cuda):
+    return import_pkg("index")
+
+
+def _oracle_check(X_stored, Q, k, s, r, tol=1e-5):
+    ref_r, ref_s = cosine_topk(X_stored, Q, k, rows_normalized=True)
+    s = s.cpu().numpy()
+    r = r.cpu().numpy()
+    kk = min(k, X_stored.shape[0])
+    for q in range(Q.shape[0]):
+        assert topk_equal_modulo_ties(r[q, :kk], s[q, :kk], ref_r[q], ref_s[q], tol), q
+        qn = Q[q].astype(np.float64) / np.linalg.norm(Q[q].astype(np.float64))
+        assert np.allclose(s[q, :kk], X_stored[r[q, :kk]].astype(np.float64) @ qn, atol=tol, rtol=0)
+        assert np.all(np.diff(s[q, :kk]) <= 0)
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+@pytest.mark.parametrize("dim", [512, 768, 100])
+@pytest.mark.parametrize("n,k,nq", [(200, 5, 3), (5000, 10, 1), (70_000, 100, 20), (70_000, 256, 9), (300_000, 10, 300)])
+def test_mfma_matches_oracle_and_scan(idxmod, cuda, dtype, dim, n, k, nq):
+    import torch
+
+    rng = np.random.default_rng(n + dim + k + nq)
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    Q = rng.standard_normal((nq, dim)).astype(np.float32)
+    Q[0] = X[n // 3]  # an exact hit
+    dev = idxmod.DeviceIndex(dim, dtype=dtype, capacity=n, device=cuda)
+    dev.upsert_rows(torch.from_numpy(X), torch.arange(n, dtype=torch.int64))
+    qt = torch.from_numpy(Q)
+    s_m, r_m = dev.search(qt, k, n, mode="mfma")
+    s_s, r_s = dev.search(qt, k, n, mode="scan")
+    torch.cuda.synchronize()
+    assert torch.equal(r_m, r_s), "MFMA path and scan disagree on rows"
+    assert torch.equal(s_m, s_s), "MFMA path and scan disagree on scores"
+    assert int(r_m[0, 0]) == n // 3
+    nchk = min(nq, 40)
+    _oracle_check(dev.stored_rows(n).cpu().numpy(), Q[:nchk], k, s_m[:nchk], r_m[:nchk])
+    dev.close()
+
+
+def test_mfma_k_larger_than_rows(idxmod, cuda):
+    import torch
+
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((37, 512)).astype(np.float32)
+    dev = idxmod.DeviceIndex(512, dtype="float16", capacity=40, device=cuda)
+    dev.upsert_rows(torch.from_numpy(X), torch.arange(37))
+    s, r = dev.search(torch.from_numpy(X[:10]), 64, 37, mode="mfma")
+    assert (r[:, 37:] == -1).all() and torch.isneginf(s[:, 37:]).all()
+    assert r[:, 0].cpu().tolist() == list(range(10))
+    s2, r2 = dev.search(torch.from_numpy(X[:10]), 64, 37, mode="scan")
+    assert torch.equal(r, r2) and torch.equal(s, s2)
+
+
+def test_mfma_duplicate_rows_fall_back_exactly(idxmod, cuda):
+    """Heavy exact ties overflow the candidate lists; the flagged queries are re-run
+    through the exact scan, so the tie rule (score desc, row asc) still holds exactly."""
+    import torch
+
+    rng = np.random.default_rng(3)
+    base = rng.standard_normal((3, 512)).astype(np.float32)
+    n = 100_000
+    X = base[rng.integers(0, 3, n)]
+    dev = idxmod.DeviceIndex(512, dtype="float16", capacity=n, device=cuda)
+    dev.upsert_rows(torch.from_numpy(X), torch.arange(n))
+    Q = np.concatenate([base[:2], rng.standard_normal((14, 512)).astype(np.float32)])
+    dev.timing(True)
+    s, r = dev.search(torch.from_numpy(Q), 50, n, mode="mfma")
+    fallbacks = dev.gemm_timing_read()[3]
+    dev.timing(False)
+    s2, r2 = dev.search(torch.from_numpy(Q), 50, n, mode="scan")
+    assert fallbacks >= 1
+    assert torch.equal(r, r2) and torch.equal(s, s2)
+    first = np.nonzero((X == base[0]).all(axis=1))[0][:50]
+    assert r[0].cpu().numpy().tolist() == first.tolist()
+
+
+def test_mfma_auto_mode_picks_batched_path(idxmod, cuda):
+    import torch
+
+    rng = np.random.default_rng(4)
+    n = 70_000
+    dev = idxmod.DeviceIndex(512, dtype="float16", capacity=n, device=cuda)
+    dev.fill_random(9, 0, n)
+    Q = torch.from_numpy(rng.standard_normal((16, 512)).astype(np.float32))
+    dev.timing(True)
+    s, r = dev.search(Q, 10, n)
+    ms, launches, flops, _ = dev.gemm_timing_read()
+    dev.timing(False)
+    assert launches >= 1 and flops > 0
+    s2, r2 = dev.search(Q, 10, n, mode="scan")
+    assert torch.equal(r, r2) and torch.equal(s, s2)
+
+
+def test_mfma_f32_index_rejected(idxmod, cuda):
+    import torch
+
+    dev = idxmod.DeviceIndex(512, dtype="float32", capacity=1000, device=cuda)
+    dev.fill_random(1, 0, 1000)
+    with pytest.raises(ValueError):
+        dev.search(torch.randn(4, 512), 5, 1000, mode="mfma")
+    s, r = dev.search(torch.randn(16, 512), 5, 1000)  # auto: scan on f32
+    assert (r >= 0).all()
+
+
+def test_config4_shard_full_size_properties(idxmod, cuda):
+    """Config 4 per-GPU shape at a reduced row count (20M x 512 fp16, 1024 queries, top-100):
+    planted exact hits come back first at score 1, results are sorted, and a sample
+    of queries matches the exact scan bit for bit."""
+    import torch
+
+    n, dim, nq, k = 20_000_000, 512, 1024, 100
+    dev = idxmod.DeviceIndex(dim, dtype="float16", capacity=n, device=cuda)
+    dev.fill_random(4, 0, n)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Q = torch.randn((nq, dim), device="cuda", generator=g)
+    planted = torch.tensor([0, 7, 19_999_999, 12_345_678], dtype=torch.int64)
+    Q[: len(planted)] = dev.stored_rows(planted)
+    s, r = dev.search(Q, k, n, mode="mfma")
+    assert r[: len(planted), 0].cpu().tolist() == planted.tolist()
+    # a query equal to a stored row x̂ scores x̂·x̂/||x̂|| = ||x̂|| (≈1 up to the f16 rounding of the row)
+    self_score = Q[: len(planted)].double().norm(dim=1).cpu()
+    assert torch.allclose(s[: len(planted), 0].cpu().double(), self_score, atol=1e-5)
+    assert (s[:, :-1] >= s[:, 1:]).all() and (r >= 0).all()
+    sel = torch.tensor([0, 5, 511, 512, 1023])
+    s2, r2 = dev.search(Q[sel], k, n, mode="scan")
+    assert torch.equal(r[sel.cuda()], r2) and torch.equal(s[sel.cuda()], s2)
+    dev.close()
