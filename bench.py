@@ -96,6 +96,35 @@ def cpu_search_baseline(n_rows=1_000_000, dim=512, budget_s=6.0):
             "sample": f"{done} single queries, exact top-10 over {n_rows}x{dim} f32 (numpy X@q + argpartition), {el:.1f}s"}
 
 
+def cpu_batch_search_baseline(n_rows=1_000_000, dim=512, nq=256, k=100, index_rows=1_000_000_000, budget_s=8.0):
+    """numpy fp32 batched exact top-k (X @ Q^T, argpartition per query) on a row sample, extrapolated to the index size."""
+    from threadpoolctl import threadpool_info
+
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((n_rows, dim), dtype=np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    Q = rng.standard_normal((nq, dim)).astype(np.float32)
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+
+    def once():
+        S = Q @ X.T
+        part = np.argpartition(-S, k - 1, axis=1)[:, :k]
+        sc = np.take_along_axis(S, part, axis=1)
+        order = np.lexsort((part, -sc), axis=1)
+        return np.take_along_axis(part, order, axis=1)
+
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or done == 0:
+        once()
+        done += 1
+    el = (time.perf_counter() - t0) / done
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    scale = index_rows / n_rows
+    return {"value": nq / (el * scale), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{done} x ({nq} queries x {n_rows}x{dim} f32 rows, top-{k}: numpy X@Q^T + argpartition) "
+                      f"= {el:.2f}s each, extrapolated linearly to {index_rows:,} rows"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +133,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rows-per-gpu", type=int, default=125_000_000)
     ap.add_argument("--search-queries", type=int, default=20)
+    ap.add_argument("--batch-queries", type=int, default=1024)
+    ap.add_argument("--batch-reps", type=int, default=3)
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -188,7 +219,7 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": {
-            "kernel": "gemm_bf16_kernel<EPI_GELU_BF16> (fc1: M=%d N=3072 K=768)" % (B * 197),
+            "kernel": "gemm_pp_kernel<EPI_GELU_BF16> (fc1: M=%d N=3072 K=768)" % (B * 197),
             "bound": "mfma",
             "achieved": achieved,
             "peak": PEAK_BF16_TFLOPS,
@@ -243,6 +274,38 @@ def main():
                          "traffic": load_profile_traffic("scan_f16"), "avg_launch_ms": scan_ms / max(scan_n, 1),
                          "bytes_per_launch": scan_bytes / max(scan_n, 1)},
         }
+        # config 4 as named: a batch of 1024 queries, top-100, batched MFMA path
+        # (staged filter GEMM + exact rescoring per shard, RCCL all-gather + merge)
+        nqb, kb = args.batch_queries, 100
+        gqb = torch.Generator(device=dev).manual_seed(6)
+        qbatch = torch.randn((nqb, dim), device=dev, generator=gqb)
+        sidx.search(qbatch, kb, mode="mfma")
+        torch.cuda.synchronize()
+        shard.timing(True)
+        shard.gemm_timing_read()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.batch_reps):
+            sidx.search(qbatch, kb, mode="mfma")
+        torch.cuda.synchronize()
+        barrier()
+        bel = max_over_ranks(time.perf_counter() - t0)
+        g_ms, g_n, g_flops, g_fb = shard.gemm_timing_read()
+        shard.timing(False)
+        g_tf = g_flops / (g_ms / 1e3) / 1e12 if g_ms > 0 else 0.0
+        result["search"]["batched"] = {
+            "workload": f"BASELINE config 4: {rows * world:,} x 512 fp16 rows ({rows:,}/GPU), batch of {nqb} queries, exact top-{kb}",
+            "value": nqb * args.batch_reps / bel,
+            "unit": "queries/s",
+            "ms_per_batch": bel / args.batch_reps * 1e3,
+            "roofline": {"kernel": "filter_gemm_kernel<f16> (256q x 256 rows x 64 MFMA tiles, candidate epilogue)",
+                         "bound": "mfma", "achieved": g_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": g_tf / PEAK_BF16_TFLOPS, "traffic": load_profile_traffic("filter_f16"),
+                         "avg_launch_ms": g_ms / max(g_n, 1), "launches": g_n,
+                         "flops_per_batch": g_flops / max(args.batch_reps, 1)},
+            "gemm_share_of_batch": (g_ms / args.batch_reps) / (bel / args.batch_reps * 1e3),
+            "exact_fallbacks": g_fb,
+        }
         sidx.close()
         del shard, sidx
         torch.cuda.empty_cache()
@@ -270,6 +333,9 @@ def main():
             result["cpu_baseline"] = cpu_embed_baseline()
             if "search" in result:
                 result["search"]["cpu_baseline"] = cpu_search_baseline()
+                if "batched" in result["search"]:
+                    result["search"]["batched"]["cpu_baseline"] = cpu_batch_search_baseline(
+                        index_rows=args.rows_per_gpu * world)
         except Exception as e:  # the baseline must not kill the GPU bench line
             result["cpu_baseline"] = {"error": repr(e)}
 

@@ -16,6 +16,9 @@
 // DMA is issued before this K-tile's MFMAs and lands under them.
 #pragma once
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "vit_kernels.h"
 
 namespace rc {
@@ -403,12 +406,340 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 }
 
+
+// ------------------------------------------------------ persistent GEMM ----
+// The ping-pong main loop of gemm_pp_kernel (256x256x64 tiles, G1 one segment
+// behind G0) run persistently: one 512-thread block per CU, with its (tile,
+// K-tile) steps flattened into one sequence so the next tile's first K-tile
+// streams in under the current tile's last MFMAs and no block pays a prologue
+// per tile.  Block slots come from the XCD-aware remap (consecutive slots share
+// an XCD and therefore its L2).
+//   SK = false: slot s owns whole tiles s, s + G, s + 2G, ...
+//   SK = true (Stream-K): the ntiles·nk steps are cut into G equal contiguous
+//     ranges, so every block does the same MFMA work and there is no partial
+//     last round (fc2/O-proj: 591 tiles on 256 CUs would otherwise run 3
+//     rounds for 2.31 rounds of work).  A tile cut by a range boundary is
+//     finished by its OWNER, the block holding its K-tile 0, at the END of the
+//     owner's range; every other block that holds part of it does that part
+//     FIRST in its range, stores the f32 partial accumulators (wave-linear,
+//     16-B write-through sc1 stores), drains and raises a per-wave flag
+//     (= launch epoch).  The owner's waves each poll their counterpart's flag
+//     (bounded spin), acquire at agent scope, and add the partials before the
+//     epilogue.  No block waits before publishing, and all G <= #CU blocks are
+//     resident (128 KB LDS = one block per CU), so the hand-off cannot deadlock.
+// The epilogue works from registers: bias / GELU / residual / position are
+// applied per lane; bf16 results are paired across 16-lane rows with
+// v_permlane16_swap so every lane stores 16 B (8 consecutive columns), one
+// store instruction per 64-B segment of 16 rows; f32 results are 16-B stores.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int EPI, bool SK>
+__global__ __launch_bounds__(512, 1) void gemm_persist_kernel(GemmArgs a) {
+    constexpr int BM = 256, BN = 256, BK = 64;
+    constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int ntn = a.N / BN;
+    const int ntiles = ((a.M + BM - 1) / BM) * ntn;
+    const int G = gridDim.x, orig = blockIdx.x;
+    const int q8 = G / 8, r8 = G % 8, xcd = orig % 8;
+    const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int K = a.K;
+    const int nk = K / BK;
+    const int64_t total = (int64_t)ntiles * nk;
+    int nsteps, ctile, ck;
+    if constexpr (SK) {
+        const int s0 = (int)((int64_t)slot * total / G), s1 = (int)((int64_t)(slot + 1) * total / G);
+        nsteps = s1 - s0;
+        ctile = s0 / nk;
+        ck = s0 - ctile * nk;
+    } else {
+        nsteps = slot < ntiles ? ((ntiles - slot + G - 1) / G) * nk : 0;
+        ctile = slot;
+        ck = 0;
+    }
+    if (nsteps <= 0) return;  // block-uniform, before any barrier
+    constexpr int TSTEP_SK = 1;
+    const int tstep = SK ? TSTEP_SK : G;
+
+    // 64 pieces of 1 KB per K-tile (A: 0-31, W: 32-63); wave w owns pieces w + 8 i.
+    auto stage4 = [&](int buf, int tile, int k0, int i0) {
+        uint8_t *base = smem + buf * STAGE;
+        const int tm = tile / ntn, tn = tile - tm * ntn;
+        const uint16_t *Ag = a.A + (int64_t)tm * BM * K;
+        const uint16_t *Wg = a.W + (int64_t)tn * BN * K;
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = i < 4;
+            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
+            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+        }
+    };
+    auto bar = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    f32x4 acc[2][2][4][2];
+    auto zero_acc = [&] {
+#pragma unroll
+        for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+            for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+                for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                    for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    zero_acc();
+
+    stage4(0, ctile, ck * BK, 0);
+    stage4(0, ctile, ck * BK, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: G1 one segment behind
+
+    int ltile = ctile, lk = ck + 1;  // load cursor: the step after (ctile, ck)
+    if (lk == nk) { lk = 0; ltile += tstep; }
+    int kb = ck;                     // K-tile at which the current segment started
+    bf16x8 af[4][2], wf[2][2];
+    for (int step = 0; step < nsteps; ++step) {
+        const int cur = step & 1;
+        const uint8_t *As = smem + cur * STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+        const bool more = step + 1 < nsteps;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mq = p >> 1;
+            const int nq = (p == 1 || p == 2);
+            if (p == 0 || p == 2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        const int c = s * 4 + g;
+                        af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                    const int c = s * 4 + g;
+                    wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                }
+            if (more && p < 2) stage4(cur ^ 1, ltile, lk * BK, p * 4);
+            if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        acc[mq][nq][mi][ni] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], acc[mq][nq][mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+        if (++lk == nk) { lk = 0; ltile += tstep; }
+        const bool tile_done = ck == nk - 1;
+        if (!tile_done && !(SK && step == nsteps - 1)) {
+            ++ck;
+            continue;
+        }
+
+        if constexpr (SK) {
+            f32x4 *part = reinterpret_cast<f32x4 *>(a.sk_ws);
+            if (kb > 0 && (a.sk_debug & 1)) {
+                zero_acc();
+                kb = 0;
+                ck = 0;
+                ctile += 1;
+                continue;
+            }
+            if (kb > 0) {
+                // ---- contributor: publish this range's share of tile ctile to its owner
+                // write-through (sc1) 16-B stores: visible at agent scope once drained,
+                // so no release fence (an agent release would write back this XCD's L2)
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(part + (int64_t)slot * 32 * 512, (short)0, 32 * 512 * 16, 0x00020000);
+#pragma unroll
+                for (int i = 0; i < 32; ++i) {
+                    const f32x4 v = acc[i >> 4][(i >> 3) & 1][(i >> 1) & 3][i & 1];
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (i * 512 + tid) * 16, 0, 16);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(a.sk_flags + slot * 8 + wave, a.sk_epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                zero_acc();
+                kb = 0;
+                ck = 0;
+                ctile += 1;
+                continue;
+            }
+            if (!tile_done && !(a.sk_debug & 2)) {
+                // ---- owner of a cut tile: add every later range's share
+                const int64_t tile_end = (int64_t)(ctile + 1) * nk;
+                for (int w2 = slot + 1; w2 < G && (int64_t)w2 * total / G < tile_end; ++w2) {
+                    const uint32_t *flag = a.sk_flags + w2 * 8 + wave;
+                    int spins = 0;
+                    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.sk_epoch) {
+                        if (++spins > (1 << 24)) {
+                            if (lane == 0) atomicOr(a.sk_err, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int i = 0; i < 32; ++i)
+                        acc[i >> 4][(i >> 3) & 1][(i >> 1) & 3][i & 1] += part[((int64_t)w2 * 32 + i) * 512 + tid];
+                }
+            }
+        }
+
+        // ---- epilogue of tile ctile: acc[mq][nq][mi][ni][j] =
+        //      C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
+        const int tm = ctile / ntn, tn = ctile - tm * ntn;
+        const int m0 = tm * BM, n0 = tn * BN;
+        float4 bias[2][2];
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                bias[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+#pragma unroll
+                    for (int nq = 0; nq < 2; ++nq) {
+                        uint32_t u[2][2];
+#pragma unroll
+                        for (int ni = 0; ni < 2; ++ni) {
+                            const f32x4 v4 = acc[mq][nq][mi][ni];
+                            const float4 b4 = bias[nq][ni];
+                            f32x2 lo = f32x2{v4[0] + b4.x, v4[1] + b4.y}, hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
+                            if constexpr (EPI == EPI_GELU_BF16) {
+                                lo = gelu_fast2(lo);
+                                hi = gelu_fast2(hi);
+                            }
+                            u[ni][0] = pack_bf16x2(lo.x, lo.y);
+                            u[ni][1] = pack_bf16x2(hi.x, hi.y);
+                        }
+                        // rows of 16 lanes (g): odd rows of u[0] <-> even rows of u[1]
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
+                            u[0][h] = r2[0];
+                            u[1][h] = r2[1];
+                        }
+                        const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
+                        if (row < a.M)
+                            *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * a.N + col) =
+                                make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
+                    }
+                } else if (row < a.M) {
+                    float4 add[2][2];
+                    int64_t dst;
+                    if constexpr (EPI == EPI_RESID_F32) {
+                        dst = (int64_t)row * a.N;
+#pragma unroll
+                        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                            for (int ni = 0; ni < 2; ++ni)
+                                add[nq][ni] = *reinterpret_cast<const float4 *>(a.out_f32 + dst + n0 + wc * 64 + nq * 32 +
+                                                                                ni * 16 + 4 * g);
+                    } else {  // EPI_PATCH_F32
+                        const int np = a.tokens - 1;
+                        const int img = row / np, pp = row - img * np;
+                        dst = ((int64_t)img * a.tokens + 1 + pp) * a.N;
+#pragma unroll
+                        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                            for (int ni = 0; ni < 2; ++ni)
+                                add[nq][ni] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + pp) * a.N + n0 +
+                                                                                wc * 64 + nq * 32 + ni * 16 + 4 * g);
+                    }
+#pragma unroll
+                    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                        for (int ni = 0; ni < 2; ++ni) {
+                            const f32x4 v4 = acc[mq][nq][mi][ni];
+                            const float4 b4 = bias[nq][ni], r4 = add[nq][ni];
+                            *reinterpret_cast<float4 *>(a.out_f32 + dst + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g) =
+                                make_float4(r4.x + (v4[0] + b4.x), r4.y + (v4[1] + b4.y), r4.z + (v4[2] + b4.z),
+                                            r4.w + (v4[3] + b4.w));
+                        }
+                }
+            }
+        zero_acc();
+        kb = 0;
+        ck = 0;
+        ctile += tstep;
+    }
+    if (grp == 0) bar();  // balance the stagger barrier
+}
+
+// Stream-K hand-off state: one partial-accumulator slab (256 KB) and 8 flags
+// per block slot, plus an error word; flags hold the epoch of the launch that
+// last published, so no per-launch reset is needed (epochs count up from 1 per
+// workspace; launches that share a workspace must be stream-ordered, which the
+// per-handle mutex of the callers guarantees).
+struct SkWorkspace {
+    float *ws = nullptr;
+    uint32_t *flags = nullptr;  // flags[0..slots*8) then the error word
+    int slots = 0;
+    uint32_t epoch = 0;
+    void ensure(int blocks) {
+        if (blocks <= slots) return;
+        release();
+        ws = (float *)dmalloc((size_t)blocks * 32 * 512 * 16);
+        flags = (uint32_t *)dmalloc(((size_t)blocks * 8 + 4) * sizeof(uint32_t));
+        RC_HIP(hipMemset(flags, 0, ((size_t)blocks * 8 + 4) * sizeof(uint32_t)));
+        slots = blocks;
+        epoch = 0;
+    }
+    void release() {
+        dfree(ws);
+        dfree(flags);
+        ws = nullptr;
+        flags = nullptr;
+        slots = 0;
+    }
+    uint32_t *err() const { return flags + (size_t)slots * 8; }
+    uint32_t next_epoch() {
+        if (++epoch == 0) epoch = 1;
+        return epoch;
+    }
+};
+
 // Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
 // 3 = 128x256 8-wave, 0 = auto.  Auto follows interleaved A/B timings on the
 // batch-256 shapes (tools/gemm_micro.py, profiles/): the 256x256 ping-pong kernel
 // everywhere except the short square O-projection (N = K = 768), where 128-row
 // tiles shrink the 2.3-wave tail enough to win.
-enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4 };
+enum GemmVariant {
+    GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4, GEMM_PERSIST = 5, GEMM_STREAMK = 6
+};
 
 inline int gemm_pick(const GemmArgs &a, int variant) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL: ablation builds, RC_GEMM_ABLATION)
@@ -418,11 +749,24 @@ inline int gemm_pick(const GemmArgs &a, int variant) {
     return GEMM_PINGPONG;
 }
 
+// compute units of the current device (one persistent block per CU)
+inline int gemm_num_cus() {
+    static thread_local int dev = -1, cus = 256;
+    int d = 0;
+    if (hipGetDevice(&d) == hipSuccess && d != dev) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0) cus = v;
+        dev = d;
+    }
+    return cus;
+}
+
 // rows the A buffer must provide beyond M (the kernels read whole tiles)
 inline int gemm_row_pad() { return 256; }
 
 template <int EPI>
-void launch_gemm(const GemmArgs &a, int variant, hipStream_t s) {
+void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *sk = nullptr) {
+    GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
     switch (gemm_pick(a, variant)) {
         case GEMM_V1: {
@@ -441,6 +785,26 @@ void launch_gemm(const GemmArgs &a, int variant, hipStream_t s) {
             RC_REQUIRE(a.N % G2_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             const int ntm = (a.M + 127) / 128, ntn = a.N / G2_BN;
             hipLaunchKernelGGL((gemm256_kernel<EPI, 128>), dim3(ntm * ntn), dim3(512), 0, s, a);
+            break;
+        }
+        case GEMM_PERSIST: {
+            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
+            hipLaunchKernelGGL((gemm_persist_kernel<EPI, false>), dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
+            break;
+        }
+        case GEMM_STREAMK: {
+            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            RC_REQUIRE(sk != nullptr, RC_ERR_INVALID, "internal: Stream-K GEMM without a workspace");
+            const int64_t steps = (int64_t)((a.M + 255) / 256) * (a.N / 256) * (a.K / 64);
+            const int G = (int)std::min<int64_t>(steps, gemm_num_cus());
+            sk->ensure(G);
+            a.sk_ws = sk->ws;
+            a.sk_flags = sk->flags;
+            a.sk_err = sk->err();
+            a.sk_epoch = sk->next_epoch();
+            if (const char *dbg = std::getenv("RC_SK_DEBUG")) a.sk_debug = std::atoi(dbg);
+            hipLaunchKernelGGL((gemm_persist_kernel<EPI, true>), dim3(G), dim3(512), 0, s, a);
             break;
         }
         case GEMM_PINGPONG: {

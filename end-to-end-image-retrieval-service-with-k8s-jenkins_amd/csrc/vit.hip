@@ -130,6 +130,7 @@ struct rc_model {
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
     int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
+    SkWorkspace sk;                // Stream-K partials/flags of this model's GEMMs
 
     void *alloc(size_t bytes) {
         void *p = dmalloc(bytes);
@@ -138,6 +139,7 @@ struct rc_model {
     }
     ~rc_model() {
         for (auto &t : timers) t.destroy();
+        sk.release();
         for (void *p : allocs) dfree(p);
         dfree(resize_tmp);
     }
@@ -306,7 +308,7 @@ void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, bool fc1 = false) {
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = fc1 ? m->timers[T_FC1].begin(s) : -1;
-    launch_gemm<EPI>(a, m->gemm_variant, s);
+    launch_gemm<EPI>(a, m->gemm_variant, s, &m->sk);
     if (fc1) m->timers[T_FC1].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
@@ -566,13 +568,20 @@ extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint1
         RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
         GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
         hipStream_t s = (hipStream_t)stream;
+        // one Stream-K workspace per device for this test/benchmark hook, calls serialised
+        static std::mutex mu;
+        static std::map<int, SkWorkspace> sk_by_dev;
+        std::lock_guard<std::mutex> lk(mu);
+        int dev = 0;
+        RC_HIP(hipGetDevice(&dev));
+        SkWorkspace *sk = &sk_by_dev[dev];
         switch (epi) {
-            case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s); break;
-            case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s); break;
-            case EPI_RESID_F32: launch_gemm<EPI_RESID_F32>(a, variant, s); break;
+            case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s, sk); break;
+            case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s, sk); break;
+            case EPI_RESID_F32: launch_gemm<EPI_RESID_F32>(a, variant, s, sk); break;
             case EPI_PATCH_F32:
                 RC_REQUIRE(pos && tokens > 1, RC_ERR_INVALID, "patch epilogue needs pos and tokens");
-                launch_gemm<EPI_PATCH_F32>(a, variant, s);
+                launch_gemm<EPI_PATCH_F32>(a, variant, s, sk);
                 break;
             default: throw Error(RC_ERR_INVALID, "unknown epilogue");
         }

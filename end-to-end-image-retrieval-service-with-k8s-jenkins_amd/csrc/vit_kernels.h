@@ -36,6 +36,12 @@ struct GemmArgs {
     float *out_f32;     // EPI_RESID_F32 (in place: out += A W^T + b) / EPI_PATCH_F32
     const float *pos;   // EPI_PATCH_F32: position embeddings [tokens][N]
     int tokens;         // EPI_PATCH_F32: tokens per image (patches + 1)
+    // Stream-K hand-off state (gemm_persist_kernel<EPI, true>); see SkWorkspace
+    float *sk_ws = nullptr;          // [blocks][32][512] f32x4 partial accumulators
+    uint32_t *sk_flags = nullptr;    // [blocks][8] per-wave publish flags (= epoch when ready)
+    uint32_t *sk_err = nullptr;      // bit 0: a bounded spin gave up
+    uint32_t sk_epoch = 0;           // this launch's flag value (never 0)
+    int sk_debug = 0;                // diagnostic builds only: bit0 skip publish, bit1 skip wait
 };
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;
