@@ -25,10 +25,11 @@ namespace rc {
 
 constexpr int G2_BN = 256, G2_BK = 64;
 
-// erf via Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), one exp + one rcp.
+// erf via Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), one exp + one v_rcp_f32
+// (a correctly rounded 1/x would cost a 9-instruction IEEE division sequence).
 __device__ __forceinline__ float erf_as(float x) {
     const float ax = fabsf(x);
-    const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));  // v_rcp_f32 (1 ulp)
     float p = fmaf(1.061405429f, t, -1.453152027f);
     p = fmaf(p, t, 1.421413741f);
     p = fmaf(p, t, -0.284496736f);
@@ -46,7 +47,7 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
     const f32x2 z = x * 0.70710678118654752f;
     const f32x2 az = {fabsf(z.x), fabsf(z.y)};
     const f32x2 d = az * 0.3275911f + 1.0f;
-    const f32x2 t = {__frcp_rn(d.x), __frcp_rn(d.y)};
+    const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
     f32x2 p = t * 1.061405429f + -1.453152027f;
     p = p * t + 1.421413741f;
     p = p * t + -0.284496736f;

@@ -160,8 +160,12 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     return (uint16_t)(u >> 16);
 }
 
+// Two f32 → packed bf16x2, round to nearest even: one v_cvt_pk_bf16_f32 (same
+// bits as f32_to_bf16 for finite inputs; keeps a NaN a NaN).
+typedef __bf16 rc_bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-    return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+    const rc_bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
