@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "vit_kernels.h"
 
@@ -700,6 +701,206 @@ __global__ __launch_bounds__(512, 1) void gemm_persist_kernel(GemmArgs a) {
     if (grp == 0) bar();  // balance the stagger barrier
 }
 
+// ------------------------------------------------- deferred-store GEMM ----
+// gemm_persist_kernel's loop for the bf16-output epilogues (QKV, fc1+GELU), with
+// the tile's stores taken off the critical path.  On gfx950 stores and LDS-DMA
+// loads share one in-order vmcnt, so a store burst at a tile boundary makes the
+// next K-tile's DMA wait behind it (every CU reaches its tile boundary at about
+// the same time: 256 x 128 KB).  Here the epilogue only computes (bias, GELU,
+// bf16 pack, permlane16 pairing) into 64 VGPRs; the 16 16-B stores are issued in
+// the NEXT tile's first K-step, 4 per phase, each group AFTER that phase's DMA
+// issue, and the phase-3 wait is vmcnt(12): it retires both DMA halves (older)
+// and the first 4 stores while the youngest 12 drain under the next phases'
+// MFMAs.  The first K-step's MFMAs take a zero C operand, so the accumulators
+// are dead between the epilogue and the next tile and share registers with the
+// pending stores.  Stores go through a buffer descriptor bounded at the tile's
+// valid rows: rows >= M are dropped by the hardware, so every wave always
+// issues exactly 16 stores and the counted wait stays exact.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_ds_kernel(GemmArgs a) {
+    static_assert(EPI == EPI_BF16 || EPI == EPI_GELU_BF16, "bf16-output epilogues only");
+    constexpr int BM = 256, BN = 256, BK = 64;
+    constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int N = a.N, K = a.K;
+    const int ntn = N / BN;
+    const int ntiles = ((a.M + BM - 1) / BM) * ntn;
+    const int G = gridDim.x, orig = blockIdx.x;
+    const int q8 = G / 8, r8 = G % 8, xcd = orig % 8;
+    const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    if (slot >= ntiles) return;
+    const int nmine = (ntiles - slot + G - 1) / G;
+    const int nk = K / BK;
+    const int nsteps = nmine * nk;
+
+    auto stage4 = [&](int buf, int tile, int k0, int i0) {
+        uint8_t *base = smem + buf * STAGE;
+        const int tm = tile / ntn, tn = tile - tm * ntn;
+        const uint16_t *Ag = a.A + (int64_t)tm * BM * K;
+        const uint16_t *Wg = a.W + (int64_t)tn * BN * K;
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = i < 4;
+            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
+            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+        }
+    };
+    auto bar = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    f32x4 acc[2][2][4][2];
+    uint4 pend[2][4][2];                  // packed bf16 results of the previous tile [mq][mi][nq]
+    const uint16_t *pbase = a.out_bf16;   // its output rows (row m0) ...
+    int prec = 0;                         // ... bounded at M (bytes)
+    int pn0 = 0;                          // its first column
+    bool has_pend = false;
+
+    auto store_group = [&](int j0) {      // pending stores j0 .. j0+3, j = (mq, mi, nq)
+        const __amdgpu_buffer_rsrc_t prs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)pbase, (short)0, (a.sk_debug & 16) ? 0 : prec, 0x00020000);
+#pragma unroll
+        for (int j = j0; j < j0 + 4; ++j) {
+            const int mq = j >> 3, mi = (j >> 1) & 3, nq = j & 1;
+            const int rl = grp * 128 + mq * 64 + mi * 16 + li;
+            const int col = pn0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
+            if (a.sk_debug & 32)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[mq][mi][nq]), prs,
+                                                       (rl * N + col) * 2, 0, 2);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[mq][mi][nq]), prs,
+                                                       (rl * N + col) * 2, 0, 0);
+        }
+    };
+
+    stage4(0, slot, 0, 0);
+    stage4(0, slot, 0, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: G1 one segment behind
+
+    int ltile = slot, lk = 1;  // load cursor: the step after the one being computed
+    if (lk == nk) { lk = 0; ltile += G; }
+    int buf = 0, gstep = 0;
+    bf16x8 af[4][2], wf[2][2];
+
+    auto step = [&](auto first_c) {
+        constexpr bool FIRST = decltype(first_c)::value;
+        const uint8_t *As = smem + buf * STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+        const bool more = gstep + 1 < nsteps;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mq = p >> 1;
+            const int nq = (p == 1 || p == 2);
+            if (p == 0 || p == 2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        const int c = s * 4 + g;
+                        af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                    const int c = s * 4 + g;
+                    wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                }
+            if (more && p < 2) stage4(buf ^ 1, ltile, lk * BK, p * 4);
+            if constexpr (FIRST) {
+                if (has_pend) store_group(4 * p);
+            }
+            if (p == 3) {
+                if (FIRST && has_pend) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const f32x4 cin = (FIRST && s == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mq][nq][mi][ni];
+                        acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], cin, 0, 0, 0);
+                    }
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+        if (++lk == nk) { lk = 0; ltile += G; }
+        buf ^= 1;
+        ++gstep;
+    };
+
+    int tile = slot;
+    for (int t = 0; t < nmine; ++t, tile += G) {
+        step(std::true_type{});
+        for (int k = 1; k < nk; ++k) step(std::false_type{});
+
+        // ---- epilogue math of this tile → pend (stores follow in the next tile's first step)
+        const int tm = tile / ntn, tn = tile - tm * ntn;
+        const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq) {
+            float4 bias[2];
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    uint32_t u[2][2];
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const f32x4 v4 = acc[mq][nq][mi][ni];
+                        const float4 b4 = bias[ni];
+                        f32x2 lo = f32x2{v4[0] + b4.x, v4[1] + b4.y}, hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
+                        if constexpr (EPI == EPI_GELU_BF16) {
+                            lo = gelu_fast2(lo);
+                            hi = gelu_fast2(hi);
+                        }
+                        u[ni][0] = pack_bf16x2(lo.x, lo.y);
+                        u[ni][1] = pack_bf16x2(hi.x, hi.y);
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
+                        u[0][h] = r2[0];
+                        u[1][h] = r2[1];
+                    }
+                    pend[mq][mi][nq] = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
+                }
+        }
+        const int rows_valid = min(BM, a.M - m0);
+        pbase = a.out_bf16 + (int64_t)m0 * N;
+        prec = rows_valid * N * 2;
+        pn0 = n0;
+        has_pend = true;
+    }
+#pragma unroll
+    for (int j0 = 0; j0 < 16; j0 += 4) store_group(j0);
+    if (grp == 0) bar();  // balance the stagger barrier
+}
+
 // Stream-K hand-off state: one partial-accumulator slab (256 KB) and 8 flags
 // per block slot, plus an error word; flags hold the epoch of the launch that
 // last published, so no per-launch reset is needed (epochs count up from 1 per
@@ -739,7 +940,8 @@ struct SkWorkspace {
 // everywhere except the short square O-projection (N = K = 768), where 128-row
 // tiles shrink the 2.3-wave tail enough to win.
 enum GemmVariant {
-    GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4, GEMM_PERSIST = 5, GEMM_STREAMK = 6
+    GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4, GEMM_PERSIST = 5, GEMM_STREAMK = 6,
+    GEMM_DEFERRED = 7
 };
 
 inline int gemm_pick(const GemmArgs &a, int variant) {
@@ -748,6 +950,17 @@ inline int gemm_pick(const GemmArgs &a, int variant) {
     const int tiles256 = ((a.M + 255) / 256) * (a.N / G2_BN);
     (void)tiles256;
     return GEMM_PINGPONG;
+}
+
+// Diagnostic bits for A/B experiments (RC_GEMM_DEBUG, read once; 0 in production):
+// 1 Stream-K skip publish, 2 skip wait, 16 deferred-store kernel drops its stores,
+// 32 deferred stores non-temporal.
+inline int gemm_debug_bits() {
+    static const int bits = [] {
+        const char *d = std::getenv("RC_GEMM_DEBUG");
+        return d ? std::atoi(d) : 0;
+    }();
+    return bits;
 }
 
 // compute units of the current device (one persistent block per CU)
@@ -794,6 +1007,16 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
             hipLaunchKernelGGL((gemm_persist_kernel<EPI, false>), dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
             break;
         }
+        case GEMM_DEFERRED: {
+            a.sk_debug = gemm_debug_bits();
+            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
+            if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16)
+                hipLaunchKernelGGL(gemm_ds_kernel<EPI>, dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
+            else  // f32 epilogues: the persistent kernel
+                hipLaunchKernelGGL((gemm_persist_kernel<EPI, false>), dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
+            break;
+        }
         case GEMM_STREAMK: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             RC_REQUIRE(sk != nullptr, RC_ERR_INVALID, "internal: Stream-K GEMM without a workspace");
@@ -804,7 +1027,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
             a.sk_flags = sk->flags;
             a.sk_err = sk->err();
             a.sk_epoch = sk->next_epoch();
-            if (const char *dbg = std::getenv("RC_SK_DEBUG")) a.sk_debug = std::atoi(dbg);
+            a.sk_debug = gemm_debug_bits();
             hipLaunchKernelGGL((gemm_persist_kernel<EPI, true>), dim3(G), dim3(512), 0, s, a);
             break;
         }

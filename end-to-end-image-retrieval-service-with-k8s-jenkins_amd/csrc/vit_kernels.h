@@ -41,7 +41,7 @@ struct GemmArgs {
     uint32_t *sk_flags = nullptr;    // [blocks][8] per-wave publish flags (= epoch when ready)
     uint32_t *sk_err = nullptr;      // bit 0: a bounded spin gave up
     uint32_t sk_epoch = 0;           // this launch's flag value (never 0)
-    int sk_debug = 0;                // diagnostic builds only: bit0 skip publish, bit1 skip wait
+    int sk_debug = 0;                // diagnostic bits (gemm_debug_bits), 0 in production
 };
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;

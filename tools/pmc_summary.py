@@ -9,7 +9,10 @@ duration, and derived numbers:
   l2_hit          = TCC_HIT / (TCC_HIT + TCC_MISS)
   mfma_busy       = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * CUs * 4 SIMDs)  (approx)
   clock_GHz       = GRBM_GUI_ACTIVE / 8 / duration
-usage: python tools/pmc_summary.py DIR [--json OUT]
+usage: python tools/pmc_summary.py DIR [--json OUT] [--latest profiles/pmc_latest.json]
+
+--latest writes the per-launch HBM traffic of the kernels bench.py prices
+(keys fc1, scan_f16, filter_f16), averaged over that kernel's launches.
 """
 import csv
 import glob
@@ -60,6 +63,21 @@ def main():
         print(k, {x: (round(r[x], 3) if isinstance(r.get(x), float) else r.get(x)) for x in keys if x in r})
     if "--json" in sys.argv:
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+    if "--latest" in sys.argv:
+        keys = {"fc1": "gemm_pp_kernel<1, 0>", "scan_f16": "scan_topk_kernel<f16_t, 4, 1, 128>",
+                "filter_f16": "filter_gemm_kernel<f16_t>"}
+        latest = {}
+        for key, kname in keys.items():
+            recs = [r for r in out.values() if r["kernel"] == kname]
+            if not recs or not all("hbm_read_bytes" in r and "hbm_write_bytes" in r for r in recs):
+                continue
+            n = sum(r["dispatches"] for r in recs)
+            tot = sum((r["hbm_read_bytes"] + r["hbm_write_bytes"]) * r["dispatches"] for r in recs)
+            latest[key] = {"kernel": kname, "dispatches": n, "hbm_bytes_per_launch": tot / n,
+                           "hbm_read_bytes_per_launch": sum(r["hbm_read_bytes"] * r["dispatches"] for r in recs) / n,
+                           "hbm_write_bytes_per_launch": sum(r["hbm_write_bytes"] * r["dispatches"] for r in recs) / n,
+                           "note": "FETCH_SIZE x 2 (gfx950 wide-stream correction) + WRITE_SIZE, KiB units -> bytes"}
+        json.dump(latest, open(sys.argv[sys.argv.index("--latest") + 1], "w"), indent=1)
 
 
 if __name__ == "__main__":
