@@ -114,15 +114,25 @@ __global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__r
     WaveTopK<CAP> tk;
     tk.init(as_lds(&lds[wave][0]), k);
     const int64_t total = (int64_t)nlist * k;
-    for (int64_t j0 = (int64_t)wave * 64; j0 < total; j0 += 256) {
-        const int64_t j = j0 + lane;
-        uint64_t key = KEY_EMPTY;
-        if (j < total) {
-            const int64_t l = j / k, t = j - l * k;
-            key = partial[(l * nq_total + qi) * k + t];
+    // MERGE_U independent loads in flight per lane before any is consumed: the
+    // loop is latency-bound otherwise (one dependent HBM/L2 round trip per 64 keys)
+    constexpr int MERGE_U = 8;
+    for (int64_t j0 = (int64_t)wave * 64 * MERGE_U; j0 < total; j0 += 256 * MERGE_U) {
+        uint64_t key[MERGE_U];
+#pragma unroll
+        for (int u = 0; u < MERGE_U; ++u) {
+            const int64_t j = j0 + u * 64 + lane;
+            key[u] = KEY_EMPTY;
+            if (j < total) {
+                const int64_t l = j / k, t = j - l * k;
+                key[u] = partial[(l * nq_total + qi) * k + t];
+            }
         }
-        tk.reserve(64);
-        tk.push(key != KEY_EMPTY, key);
+#pragma unroll
+        for (int u = 0; u < MERGE_U; ++u) {
+            tk.reserve(64);
+            tk.push(key[u] != KEY_EMPTY, key[u]);
+        }
     }
     tk.compact();
     __syncthreads();
