@@ -135,6 +135,8 @@ def main():
     ap.add_argument("--search-queries", type=int, default=20)
     ap.add_argument("--batch-queries", type=int, default=1024)
     ap.add_argument("--batch-reps", type=int, default=3)
+    ap.add_argument("--roofline-steps", type=int, default=5)
+    ap.add_argument("--parts", type=int, default=3, help="concurrent batch slices per GPU (rc_model_set_parts)")
     ap.add_argument("--ingest-images", type=int, default=16384, help="config 5 sample per GPU (0 = skip)")
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -170,6 +172,7 @@ def main():
     # ------------------------------------------------------ embed (value) --
     B = args.batch
     model = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=local, max_batch=B)
+    model.set_parts(args.parts)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     images = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
     raw = torch.empty((B, 768), dtype=torch.float32, device=dev)
@@ -187,10 +190,24 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = max_over_ranks(time.perf_counter() - t0)
-    fc1_ms, fc1_n, fc1_flops = model.timing_read("fc1")
+    fc1c_ms, fc1c_n, _ = model.timing_read("fc1")
     model.timing(False)
     assert torch.isfinite(raw).all()
     imgs_per_s = world * B * args.steps / el
+    # Roofline of the dominant kernel: the timed steps above run the batch as
+    # --parts concurrent slices, so an fc1 launch there shares the GPU; its own
+    # efficiency is timed on the unsplit batch (the GEMM alone on the chip).
+    model.set_parts(1)
+    model.embed(images, out=(raw, nrm))
+    torch.cuda.synchronize()
+    model.timing(["fc1"])
+    model.timing_reset()
+    for _ in range(args.roofline_steps):
+        model.embed(images, out=(raw, nrm))
+    torch.cuda.synchronize()
+    fc1_ms, fc1_n, fc1_flops = model.timing_read("fc1")
+    model.timing(False)
+    model.set_parts(args.parts)
     fc1_avg_ms = fc1_ms / max(fc1_n, 1)
     fc1_flops_launch = fc1_flops / max(fc1_n, 1)
     achieved = fc1_flops_launch / (fc1_avg_ms / 1e3) / 1e12
@@ -279,7 +296,10 @@ def main():
             "avg_launch_ms": fc1_avg_ms,
             "launches": fc1_n,
             "flops_per_launch": fc1_flops_launch,
+            "measured_on": "unsplit batch (parts=1), the GEMM alone on the GPU",
+            "concurrent_avg_launch_ms": fc1c_ms / max(fc1c_n, 1),
         },
+        "embed_parts": args.parts,
         "model_tflops_per_gpu": model_tflops,
         "model_mfma_frac": model_tflops / PEAK_BF16_TFLOPS,
     }

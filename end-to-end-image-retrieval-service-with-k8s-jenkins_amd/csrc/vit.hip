@@ -98,6 +98,8 @@ struct Layer {
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
 };
 
+constexpr int kMaxParts = 4;
+
 enum TimerId { T_GEMM = 0, T_FC1 = 1, T_ATTN = 2, T_LN = 3, T_PRE = 4, T_COUNT = 5 };
 
 }  // namespace
@@ -131,6 +133,10 @@ struct rc_model {
     int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
     int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
     SkWorkspace sk;                // Stream-K partials/flags of this model's GEMMs
+    int split = 3;                 // batch parts encoded concurrently (RC_EMBED_SPLIT / rc_model_set_parts)
+    int split_min = 32;            // fewest images per part
+    hipStream_t sp[4] = {};        // streams of parts 1..3 (part 0 runs on the caller's stream)
+    hipEvent_t ev_fork = nullptr, ev_join[4] = {};
 
     void *alloc(size_t bytes) {
         void *p = dmalloc(bytes);
@@ -140,6 +146,11 @@ struct rc_model {
     ~rc_model() {
         for (auto &t : timers) t.destroy();
         sk.release();
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        for (auto &e : ev_join)
+            if (e) (void)hipEventDestroy(e);
+        for (auto &q : sp)
+            if (q) (void)hipStreamDestroy(q);
         for (void *p : allocs) dfree(p);
         dfree(resize_tmp);
     }
@@ -320,9 +331,53 @@ void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint
     m->timers[T_LN].end(t, s, (double)M * m->cfg.hidden * 6.0);
 }
 
-void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw, float *normed, hipStream_t s) {
+// Encoder for images [i0, i0 + n) of the batch (their patches already built):
+// CLS + pos, patch GEMM, 12 layers, final LN on the CLS rows.  Every buffer is
+// addressed from the first image's rows, so two parts of a batch can run on two
+// streams at once (GEMM A tiles may read up to 255 rows past a part's last row;
+// those rows are allocated and their results are never stored).
+void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s) {
     const auto &c = m->cfg;
     const int H = c.hidden, T = m->tokens, M = n * T;
+    const int64_t r0 = (int64_t)i0 * T;  // first token row of this part
+    uint16_t *patches = m->patches + (int64_t)i0 * m->npatch * m->kpatch;
+    float *hidden = m->hidden + r0 * H;
+    uint16_t *ln = m->ln + r0 * H, *qkv = m->qkv + r0 * 3 * H, *attn = m->attn + r0 * H;
+    uint16_t *mlp = m->mlp + r0 * c.mlp;
+    // 2. embeddings: CLS + pos, patch GEMM (+bias +pos) into the residual stream
+    hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, hidden, T, H, m->cls, m->pos);
+    RC_LAUNCH_CHECK();
+    {
+        GemmArgs a{patches, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden, m->pos, T};
+        gemm<EPI_PATCH_F32>(m, a, s);
+    }
+    // 3. encoder layers
+    const float scale = 1.0f / std::sqrt((float)(H / c.heads));
+    for (int l = 0; l < c.layers; ++l) {
+        const Layer &L = m->layers[l];
+        layernorm(m, hidden, L.ln1_w, L.ln1_b, ln, M, s);
+        gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
+        const int ta = m->timers[T_ATTN].begin(s);
+        if (m->attn_variant == 1 || T > ATT2_ROWS)
+            hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads, scale);
+        else
+            hipLaunchKernelGGL(attention_v2_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f);
+        RC_LAUNCH_CHECK();
+        m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
+        gemm<EPI_RESID_F32>(m, GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, s);
+        layernorm(m, hidden, L.ln2_w, L.ln2_b, ln, M, s);
+        gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, true);
+        gemm<EPI_RESID_F32>(m, GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T}, s);
+    }
+    // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
+    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, hidden, T, m->lnf_w, m->lnf_b, c.ln_eps,
+                       raw + (int64_t)i0 * H, normed ? normed + (int64_t)i0 * H : nullptr);
+    RC_LAUNCH_CHECK();
+}
+
+void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw, float *normed, hipStream_t s) {
+    const auto &c = m->cfg;
     const int S = c.image_size;
     // 1. preprocess: resize (if needed) + rescale/normalize/im2col → bf16 patches
     const int tp = m->timers[T_PRE].begin(s);
@@ -331,35 +386,25 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
                        m->lut, m->patches, n, S);
     RC_LAUNCH_CHECK();
     m->timers[T_PRE].end(tp, s, (double)n * S * S * 3 + (double)n * m->npatch * m->kpatch * 2);
-    // 2. embeddings: CLS + pos, patch GEMM (+bias +pos) into the residual stream
-    hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, m->hidden, T, H, m->cls, m->pos);
-    RC_LAUNCH_CHECK();
-    {
-        GemmArgs a{m->patches, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, m->hidden, m->pos, T};
-        gemm<EPI_PATCH_F32>(m, a, s);
+    // 2-4. encoder: one stream, or P parts of the batch on P streams so that one
+    // part's memory-bound kernels (LayerNorm, attention) and GEMM epilogue store
+    // bursts overlap another part's MFMA main loops
+    int parts = std::max(1, std::min(m->split, kMaxParts));
+    while (parts > 1 && n < parts * m->split_min) --parts;
+    if (parts == 1) {
+        encode(m, 0, n, raw, normed, s);
+        return;
     }
-    // 3. encoder layers
-    const float scale = 1.0f / std::sqrt((float)(H / c.heads));
-    for (int l = 0; l < c.layers; ++l) {
-        const Layer &L = m->layers[l];
-        layernorm(m, m->hidden, L.ln1_w, L.ln1_b, m->ln, M, s);
-        gemm<EPI_BF16>(m, GemmArgs{m->ln, L.w_qkv, L.b_qkv, M, 3 * H, H, m->qkv, nullptr, nullptr, T}, s);
-        const int ta = m->timers[T_ATTN].begin(s);
-        if (m->attn_variant == 1 || T > ATT2_ROWS)
-            hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, m->qkv, m->attn, T, c.heads, scale);
-        else
-            hipLaunchKernelGGL(attention_v2_kernel, dim3(n * c.heads), dim3(256), 0, s, m->qkv, m->attn, T, c.heads,
-                               scale * 1.4426950408889634f);
-        RC_LAUNCH_CHECK();
-        m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
-        gemm<EPI_RESID_F32>(m, GemmArgs{m->attn, L.w_o, L.b_o, M, H, H, nullptr, m->hidden, nullptr, T}, s);
-        layernorm(m, m->hidden, L.ln2_w, L.ln2_b, m->ln, M, s);
-        gemm<EPI_GELU_BF16>(m, GemmArgs{m->ln, L.w_fc1, L.b_fc1, M, c.mlp, H, m->mlp, nullptr, nullptr, T}, s, true);
-        gemm<EPI_RESID_F32>(m, GemmArgs{m->mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, m->hidden, nullptr, T}, s);
+    RC_HIP(hipEventRecord(m->ev_fork, s));
+    for (int p = 1; p < parts; ++p) RC_HIP(hipStreamWaitEvent(m->sp[p], m->ev_fork, 0));
+    for (int p = 0; p < parts; ++p) {
+        const int i0 = (int)((int64_t)n * p / parts), i1 = (int)((int64_t)n * (p + 1) / parts);
+        encode(m, i0, i1 - i0, raw, normed, p == 0 ? s : m->sp[p]);
     }
-    // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
-    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, m->hidden, T, m->lnf_w, m->lnf_b, c.ln_eps, raw, normed);
-    RC_LAUNCH_CHECK();
+    for (int p = 1; p < parts; ++p) {
+        RC_HIP(hipEventRecord(m->ev_join[p], m->sp[p]));
+        RC_HIP(hipStreamWaitEvent(s, m->ev_join[p], 0));
+    }
 }
 
 }  // namespace
@@ -384,8 +429,9 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->kpatch = 3 * cfg->patch * cfg->patch;
             build_shapes(m);
             const int B = cfg->max_batch, H = cfg->hidden;
-            m->Mp = round_up(B * m->tokens, gemm_row_pad());
-            m->Pp = round_up(B * m->npatch, gemm_row_pad());
+            // + one tile: the second half of a split batch reads whole tiles past its last row
+            m->Mp = round_up(B * m->tokens, gemm_row_pad()) + gemm_row_pad();
+            m->Pp = round_up(B * m->npatch, gemm_row_pad()) + gemm_row_pad();
             m->patches = (uint16_t *)m->alloc((size_t)m->Pp * m->kpatch * 2);
             m->hidden = (float *)m->alloc((size_t)m->Mp * H * 4);
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
@@ -403,6 +449,12 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             build_lut(m);
             if (const char *gv = std::getenv("RC_GEMM_VARIANT")) m->gemm_variant = std::atoi(gv);
             if (const char *av = std::getenv("RC_ATTN_VARIANT")) m->attn_variant = std::atoi(av);
+            if (const char *sp = std::getenv("RC_EMBED_SPLIT")) m->split = std::atoi(sp);
+            RC_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+            for (int p = 1; p < kMaxParts; ++p) {
+                RC_HIP(hipStreamCreateWithFlags(&m->sp[p], hipStreamNonBlocking));
+                RC_HIP(hipEventCreateWithFlags(&m->ev_join[p], hipEventDisableTiming));
+            }
         } catch (...) {
             delete m;
             throw;
@@ -548,6 +600,15 @@ int rc_model_timing_read(rc_model *m, int kernel_id, double *total_ms, int64_t *
         if (total_ms) *total_ms = t.total_ms;
         if (launches) *launches = t.launches;
         if (flops) *flops = t.work;
+    });
+}
+
+int rc_model_set_parts(rc_model *m, int parts) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        RC_REQUIRE(parts >= 1 && parts <= kMaxParts, RC_ERR_INVALID, "parts must be in [1, 4]");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->split = parts;
     });
 }
 

@@ -180,6 +180,10 @@ class VitMsnEmbedder:
                 mask |= 1 << TIMER_IDS[k]
         check(self.lib.rc_model_timing(self._h, mask))
 
+    def set_parts(self, parts: int) -> None:
+        """Encode batches as ``parts`` concurrent slices on separate streams (1 = one stream)."""
+        check(self.lib.rc_model_set_parts(self._h, int(parts)))
+
     def timing_reset(self) -> None:
         check(self.lib.rc_model_timing_reset(self._h))
 

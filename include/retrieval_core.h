@@ -167,6 +167,13 @@ int rc_embed(rc_model *m, const uint8_t *images, int n, int h, int w,
  * exactly as ViTImageProcessor produces them (for parity tests). */
 int rc_preprocess(rc_model *m, const uint8_t *images, int n, int h, int w, float *pixel_values, void *stream);
 
+/* Encode a batch as `parts` (1..4) concurrent slices on their own HIP streams
+ * (default 3; slices below 32 images are merged).  Results are bit-identical
+ * for every setting: each image's arithmetic is the same.  One slice's memory-
+ * bound kernels (LayerNorm, attention) and GEMM store bursts then overlap the
+ * other slices' MFMA main loops.  rc_embed still returns ordered on `stream`. */
+int rc_model_set_parts(rc_model *m, int parts);
+
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM (dominant), 2 = attention,
  * 3 = layernorm, 4 = preprocess; `mask` bit i enables id i (-1 = all, 0 = off). */

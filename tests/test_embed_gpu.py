@@ -144,3 +144,25 @@ def test_embed_full_batch_256_properties(vitmod, weights12, cuda):
     for j in range(len(pick)):
         assert 1.0 - cosine(got[j], ref[j]) <= BF16_COS_TOL
     m.close()
+
+
+@pytest.mark.parametrize("parts", [2, 3, 4])
+def test_embed_split_streams_bitwise_equal(vitmod, cuda, parts, monkeypatch):
+    """A batch encoded as 2-4 concurrent parts on separate streams equals the one-stream result bit for bit."""
+    import torch
+
+    from oracle.weights import seeded_vit_msn_weights
+
+    sd = seeded_vit_msn_weights(1907, num_layers=2)
+    rng = np.random.default_rng(parts)
+    imgs = torch.from_numpy(rng.integers(0, 256, (250, 224, 224, 3), dtype=np.uint8))
+    monkeypatch.setenv("RC_EMBED_SPLIT", "1")
+    m1 = vitmod.VitMsnEmbedder(sd, device=0, max_batch=250)
+    a, an = m1.embed(imgs)
+    monkeypatch.setenv("RC_EMBED_SPLIT", str(parts))
+    mp = vitmod.VitMsnEmbedder(sd, device=0, max_batch=250)
+    b, bn = mp.embed(imgs)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(an, bn)
+    m1.close()
+    mp.close()
