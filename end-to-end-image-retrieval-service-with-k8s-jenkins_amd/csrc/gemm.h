@@ -237,6 +237,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
                 for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // bf16 epilogues: bias of this lane's 16 output columns, loaded before the K
+    // loop so its latency hides under the prologue wait instead of stalling the
+    // epilogue (the f32 epilogues keep their own load: 16 more live VGPRs there spill)
+    float4 biasr[2][2];
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                biasr[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
+    }
+
     const int nk = K / BK;
     stage4(0, 0, 0);
     stage4(0, 0, 4);
@@ -317,7 +329,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
                 const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;  // tile-local column
-                const float4 bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+                const float4 bias = biasr[nq][ni];
 #pragma unroll
                 for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
