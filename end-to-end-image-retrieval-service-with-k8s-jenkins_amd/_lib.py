@@ -75,6 +75,8 @@ SIGNATURES = {
     "rc_index_fetch": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "rc_index_fetch_stored": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "rc_index_search": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "rc_index_export": (C.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "rc_index_import": (C.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "rc_index_search_ex": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _i32, _vp]),
     "rc_index_gemm_timing_read": (C.c_int, [_vp, _pd, _pi64, _pd, _pi64]),
     "rc_index_fill_random": (C.c_int, [_vp, C.c_uint64, _i64, _i64, _vp]),

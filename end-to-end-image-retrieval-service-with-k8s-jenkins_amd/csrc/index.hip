@@ -493,6 +493,36 @@ int rc_index_fill_random(rc_index *h, uint64_t seed, int64_t row0, int64_t n, vo
     });
 }
 
+int rc_index_export(rc_index *h, int64_t row0, int64_t n, void *rows_out, float *norms_out, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(row0 >= 0 && n >= 0 && row0 + n <= h->capacity, RC_ERR_INVALID, "rows out of capacity");
+        if (n == 0) return;
+        RC_REQUIRE(rows_out && norms_out, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        const size_t rb = (size_t)h->ld * dtype_size(h->dtype);
+        hipStream_t s = (hipStream_t)stream;
+        RC_HIP(hipMemcpyAsync(rows_out, (const uint8_t *)h->rows + (size_t)row0 * rb, (size_t)n * rb, hipMemcpyDefault, s));
+        RC_HIP(hipMemcpyAsync(norms_out, h->norms + row0, (size_t)n * sizeof(float), hipMemcpyDefault, s));
+    });
+}
+
+int rc_index_import(rc_index *h, int64_t row0, int64_t n, const void *rows_in, const float *norms_in, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(row0 >= 0 && n >= 0 && row0 + n <= h->capacity, RC_ERR_INVALID, "rows out of capacity");
+        if (n == 0) return;
+        RC_REQUIRE(rows_in && norms_in, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        const size_t rb = (size_t)h->ld * dtype_size(h->dtype);
+        hipStream_t s = (hipStream_t)stream;
+        RC_HIP(hipMemcpyAsync((uint8_t *)h->rows + (size_t)row0 * rb, rows_in, (size_t)n * rb, hipMemcpyDefault, s));
+        RC_HIP(hipMemcpyAsync(h->norms + row0, norms_in, (size_t)n * sizeof(float), hipMemcpyDefault, s));
+    });
+}
+
 int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores, int64_t *out_rows,
                     void *stream) {
     return rc_index_search_ex(h, queries, nq, n_rows, k, scores, out_rows, RC_SEARCH_AUTO, stream);

@@ -14,6 +14,8 @@ the C ABI (``include/retrieval_core.h``).
 """
 from __future__ import annotations
 
+import json
+import os
 import threading
 from typing import Any, Iterable, Sequence
 
@@ -114,6 +116,24 @@ class DeviceIndex:
         check(self.lib.rc_index_search_ex(self.handle, ptr(q), nq, int(n_rows), int(k), ptr(scores), ptr(rows),
                                           _lib.SEARCH_MODES[mode], stream_ptr(stream)))
         return scores, rows
+
+    def export_rows(self, row0: int, n: int, stream=None):
+        """Raw stored rows [row0, row0+n) (storage dtype bits, ld-padded) and norms, on the device."""
+        el = 4 if self.dtype in ("float32", "f32") else 2
+        rows = torch.empty((n, self.ld * el), dtype=torch.uint8, device=self.device)
+        norms = torch.empty((n,), dtype=torch.float32, device=self.device)
+        check(self.lib.rc_index_export(self.handle, int(row0), int(n), ptr(rows), ptr(norms), stream_ptr(stream)))
+        return rows, norms
+
+    def import_rows(self, row0: int, rows: torch.Tensor, norms: torch.Tensor, stream=None) -> None:
+        """Inverse of export_rows: write raw stored rows + norms at [row0, row0+n)."""
+        el = 4 if self.dtype in ("float32", "f32") else 2
+        rows = rows.to(device=self.device, dtype=torch.uint8).contiguous()
+        norms = norms.to(device=self.device, dtype=torch.float32).contiguous()
+        n = norms.numel()
+        if rows.numel() != n * self.ld * el:
+            raise ValueError("row bytes do not match the index layout (dimension / dtype)")
+        check(self.lib.rc_index_import(self.handle, int(row0), n, ptr(rows), ptr(norms), stream_ptr(stream)))
 
     def fill_random(self, seed: int, row0: int, n: int, stream=None) -> None:
         check(self.lib.rc_index_fill_random(self.handle, int(seed), int(row0), int(n), stream_ptr(stream)))
@@ -284,6 +304,57 @@ class Index:
             for (vid, _), v in zip(found, vals):
                 vectors[vid] = {"id": vid, "values": v, "metadata": dict(self._meta.get(vid, {}))}
         return {"vectors": vectors, "namespace": namespace}
+
+    # ---------------------------------------------------------- persistence --
+    # Pinecone keeps an index durable server-side (the reference only opens it by
+    # name, ingesting/utils.py:23-38); the in-HBM index is saved to a directory:
+    # manifest.json (name, dimension, dtype, ids in row order, metadata) +
+    # rows.npy (raw stored bytes, exactly what search scores) + norms.npy.
+    SNAPSHOT_FORMAT = 1
+
+    def save(self, path: str) -> None:
+        with self._mu:
+            os.makedirs(path, exist_ok=True)
+            n = len(self._ids)
+            rows, norms = self._dev.export_rows(0, n)
+            torch.cuda.current_stream(self._dev.device).synchronize()
+            import numpy as np
+
+            np.save(os.path.join(path, "rows.npy"), rows.cpu().numpy())
+            np.save(os.path.join(path, "norms.npy"), norms.cpu().numpy())
+            manifest = {"format": self.SNAPSHOT_FORMAT, "name": self.name, "dimension": self.dimension,
+                        "metric": self.metric, "dtype": self._dev.dtype, "ld": self._dev.ld, "count": n,
+                        "capacity": self._dev.capacity,
+                        "ids": list(self._ids), "metadata": {i: self._meta.get(i, {}) for i in self._ids}}
+            tmp = os.path.join(path, "manifest.json.tmp")
+            with open(tmp, "w") as f:
+                json.dump(manifest, f)
+            os.replace(tmp, os.path.join(path, "manifest.json"))  # the manifest lands last
+
+    @classmethod
+    def load(cls, path: str, capacity: int | None = None, device=None) -> "Index":
+        import numpy as np
+
+        with open(os.path.join(path, "manifest.json")) as f:
+            man = json.load(f)
+        if man.get("format") != cls.SNAPSHOT_FORMAT:
+            raise ValueError(f"unsupported snapshot format {man.get('format')!r}")
+        n = int(man["count"])
+        idx = cls(man["name"], dimension=man["dimension"], metric=man["metric"], dtype=man["dtype"],
+                  capacity=max(int(capacity or man.get("capacity", 0)), n, 1), device=device)
+        if idx._dev.ld != man["ld"]:
+            raise ValueError("snapshot row layout does not match this build")
+        rows = np.load(os.path.join(path, "rows.npy"), allow_pickle=False)
+        norms = np.load(os.path.join(path, "norms.npy"), allow_pickle=False)
+        if rows.shape[0] != n or norms.shape[0] != n or len(man["ids"]) != n:
+            raise ValueError("snapshot files disagree on the vector count")
+        if n:
+            idx._dev.import_rows(0, torch.from_numpy(rows), torch.from_numpy(norms))
+            torch.cuda.current_stream(idx._dev.device).synchronize()
+        idx._ids = list(man["ids"])
+        idx._rows = {vid: r for r, vid in enumerate(idx._ids)}
+        idx._meta = {vid: dict(man["metadata"].get(vid, {})) for vid in idx._ids}
+        return idx
 
     def describe_index_stats(self) -> dict:
         return {"dimension": self.dimension, "index_fullness": len(self._ids) / self._dev.capacity,

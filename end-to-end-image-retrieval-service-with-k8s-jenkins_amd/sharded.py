@@ -13,6 +13,8 @@ Pinecone does the cross-partition merge server-side (the reference only sees
 """
 from __future__ import annotations
 
+import json
+import os
 from typing import Callable
 
 import torch
@@ -68,6 +70,37 @@ class ShardedIndex:
         dist.all_gather_into_tensor(gs, s.contiguous(), group=self.group)
         dist.all_gather_into_tensor(gr, r.contiguous(), group=self.group)
         return self.merge(gs.view(self.world, nq, k), gr.view(self.world, nq, k), k)
+
+    # ---------------------------------------------------------- persistence --
+    # Each rank snapshots its own shard (no collective): <path>/shard<rank>/
+    # {rows.npy, norms.npy, manifest.json}; restore needs the same world size and
+    # per-rank capacity, so global row numbers are unchanged.
+    def save(self, path: str) -> None:
+        import numpy as np
+
+        d = os.path.join(path, f"shard{self.rank}")
+        os.makedirs(d, exist_ok=True)
+        rows, norms = self.local.export_rows(0, self.n_local)
+        torch.cuda.synchronize()
+        np.save(os.path.join(d, "rows.npy"), rows.cpu().numpy())
+        np.save(os.path.join(d, "norms.npy"), norms.cpu().numpy())
+        with open(os.path.join(d, "manifest.json"), "w") as f:
+            json.dump({"format": 1, "rank": self.rank, "world": self.world, "dim": self.dim,
+                       "capacity_per_rank": self.capacity, "n_local": self.n_local}, f)
+
+    def load(self, path: str) -> None:
+        import numpy as np
+
+        d = os.path.join(path, f"shard{self.rank}")
+        with open(os.path.join(d, "manifest.json")) as f:
+            man = json.load(f)
+        if (man["world"], man["capacity_per_rank"], man["dim"]) != (self.world, self.capacity, self.dim):
+            raise ValueError("snapshot was taken with a different world size, capacity or dimension")
+        rows = np.load(os.path.join(d, "rows.npy"), allow_pickle=False)
+        norms = np.load(os.path.join(d, "norms.npy"), allow_pickle=False)
+        if man["n_local"]:
+            self.local.import_rows(0, torch.from_numpy(rows), torch.from_numpy(norms))
+        self.n_local = int(man["n_local"])
 
     def close(self) -> None:
         close = getattr(self.local, "close", None)

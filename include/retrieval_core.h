@@ -91,6 +91,14 @@ int rc_index_fetch(rc_index *h, const int64_t *rows, int64_t n, float *out, void
  * what the search actually scores against (parity tests run the oracle on these). */
 int rc_index_fetch_stored(rc_index *h, const int64_t *rows, int64_t n, float *out, void *stream);
 
+/* Snapshot / restore (Pinecone keeps an index durable server-side; the in-HBM
+ * index is saved by the host layer — Index.save / Index.load — through these).
+ * Raw copy of the stored rows [row0, row0+n) exactly as searched (storage dtype,
+ * ld-padded, normalised) and their norms.  Buffers may be device or host memory
+ * (hipMemcpyDefault); the copy is ordered on `stream`. */
+int rc_index_export(rc_index *h, int64_t row0, int64_t n, void *rows_out, float *norms_out, void *stream);
+int rc_index_import(rc_index *h, int64_t row0, int64_t n, const void *rows_in, const float *norms_in, void *stream);
+
 /* replaces index.query(vector, top_k) — retriever/utils.py:62-64.
  * queries: device f32 [nq, dim] (normalised inside); rows [0, n_rows) are searched.
  * scores: device f32 [nq, k] cosine, descending; out_rows: device i64 [nq, k]
