@@ -15,7 +15,8 @@ import threading
 import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libretrieval_core.so")
+# RC_LIB_PATH: diagnostic builds only (tools/build_diag.sh); the product loads the in-tree library
+LIB_PATH = os.environ.get("RC_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libretrieval_core.so")
 
 RC_OK = 0
 RC_ERR_INVALID = 1

@@ -26,39 +26,41 @@ namespace rc {
 
 constexpr int G2_BN = 256, G2_BK = 64;
 
-// erf via Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), one exp + one v_rcp_f32
-// (a correctly rounded 1/x would cost a 9-instruction IEEE division sequence).
-__device__ __forceinline__ float erf_as(float x) {
-    const float ax = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));  // v_rcp_f32 (1 ulp)
-    float p = fmaf(1.061405429f, t, -1.453152027f);
-    p = fmaf(p, t, 1.421413741f);
-    p = fmaf(p, t, -0.284496736f);
-    p = fmaf(p, t, 0.254829592f);
-    p *= t;
-    const float y = 1.0f - p * __expf(-ax * ax);
-    return copysignf(y, x);
-}
-__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
+// Exact-erf GELU, x·Φ(x), evaluated as x·σ(x·P(x²)): Φ(x) = σ(logit Φ(x)) and
+// logit Φ is odd, so x·P(x²) with P a degree-4 minimax fit on |x| <= 6.5
+// (max |Δ Φ| 1.4e-6; max |Δ GELU| 6.3e-6 over all f32 x, checked in
+// tests/test_gemm_gpu.py against torch's erf GELU).  x² is clamped at 42.25,
+// where Φ = 1 - 8e-11 and P > 0 keeps σ saturated; for x -> -inf the exp2
+// overflows to +inf and x·rcp(inf) = -0.  One exp2 + one rcp per element
+// (the A&S 7.1.26 erf this replaces needed an exp, an rcp and twice the FMAs:
+// fc1 GELU epilogue 60 us of a 288 us launch, tools/gemm_calib.py ablation 116).
+// Coefficients are pre-scaled by -log2(e): exp2(x·P'(u)) = exp(-x·P(u)).
+constexpr float GELU_P0 = -2.302165355e+00f, GELU_P1 = -1.050059413e-01f, GELU_P2 = 2.534135658e-04f,
+                GELU_P3 = 1.058749684e-04f, GELU_P4 = -4.111701558e-06f, GELU_UMAX = 42.25f;
 
-// The same GELU on two values with packed f32 math (v_pk_fma_f32 / v_pk_mul_f32)
-// for the polynomial and scaling steps; rcp/exp stay per element.
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float u = fminf(x * x, GELU_UMAX);
+    float p = fmaf(GELU_P4, u, GELU_P3);
+    p = fmaf(p, u, GELU_P2);
+    p = fmaf(p, u, GELU_P1);
+    p = fmaf(p, u, GELU_P0);
+    const float e = __builtin_amdgcn_exp2f(x * p);
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
+}
+
+// The same on two values with packed f32 math (v_pk_mul_f32 / v_pk_fma_f32 /
+// v_pk_add_f32); exp2 / rcp stay per element.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
-    const f32x2 z = x * 0.70710678118654752f;
-    const f32x2 az = {fabsf(z.x), fabsf(z.y)};
-    const f32x2 d = az * 0.3275911f + 1.0f;
-    const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    f32x2 p = t * 1.061405429f + -1.453152027f;
-    p = p * t + 1.421413741f;
-    p = p * t + -0.284496736f;
-    p = p * t + 0.254829592f;
-    p = p * t;
-    const f32x2 q = -az * az;
-    const f32x2 e = {__expf(q.x), __expf(q.y)};
-    const f32x2 y = 1.0f - p * e;  // erf(|z|)
-    const f32x2 ys = {copysignf(y.x, z.x), copysignf(y.y, z.y)};
-    return 0.5f * x * (1.0f + ys);
+    f32x2 u = x * x;
+    u = f32x2{fminf(u.x, GELU_UMAX), fminf(u.y, GELU_UMAX)};
+    f32x2 p = u * GELU_P4 + GELU_P3;
+    p = p * u + GELU_P2;
+    p = p * u + GELU_P1;
+    p = p * u + GELU_P0;
+    const f32x2 y = x * p;
+    const f32x2 d = f32x2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + 1.0f;
+    return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
 template <int EPI, int BM>
@@ -186,7 +188,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
 // in its phase-3 M segment, and the barrier after G1's phase-3 M segment
 // precedes G0's first read of t+1.
 // ABL (diagnostic builds only): bit0 = no DMA in the K loop, bit1 = no MFMA,
-// bit2 = no epilogue (accumulators kept live).  ABL = 0 is the product kernel.
+// bit2 = no epilogue (accumulators kept live), bit3 = no global stores in the
+// bf16 epilogue (LDS staging kept), bit4 = no GELU.  ABL = 0 is the product kernel.
 template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     constexpr int BM = 256, BN = 256, BK = 64;
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                         const int rl = grp * 128 + mq * 64 + mi * 16 + li;
                         const f32x4 v4 = acc[mq][nq][mi][ni];
                         float v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
-                        if constexpr (EPI == EPI_GELU_BF16) {
+                        if constexpr (EPI == EPI_GELU_BF16 && !(ABL & 16)) {
                             const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
                             v0 = lo.x;
                             v1 = lo.y;
@@ -354,7 +357,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
             const int id = it * 512 + tid;
             const int rl = id >> 5, ch = id & 31;
             const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
-            if (m0 + rl < a.M) *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+            if constexpr ((ABL & 8) != 0) {
+                asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+            } else if (m0 + rl < a.M) {
+                *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+            }
         }
         return;
     }
@@ -417,6 +424,210 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
             }
         }
         if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
+    }
+}
+
+
+// ------------------------------------------------- two-workgroup GEMM ----
+// 128 (rows) x 256 (cols) tile per 256-thread workgroup, TWO workgroups per CU.
+// A 256x256 f32 accumulator tile fills half the CU's register file, so with one
+// workgroup per CU the epilogue (bias / GELU / bf16 pack / stores, 35-40 % of an
+// fc1 launch when measured alone) cannot overlap any matrix work.  Two
+// independent 128x256 workgroups per CU desynchronise: one's epilogue (VALU,
+// LDS staging, stores) runs beside the other's MFMA main loop on every SIMD.
+// The price is 1.5x the L2->LDS bytes per flop, so the ring is 3 deep (two
+// K-steps in flight per workgroup, ~96 KB per CU).
+// Wave w owns all 128 rows x columns [64w, 64w+64): acc[mi][ni], 8 x 4 tiles of
+// mfma_f32_16x16x32_bf16 with swapped operands (A-operand = weight rows), so a
+// lane's accumulator holds 4 consecutive output columns of one row.
+// LDS ring: 3 slots x (A 128 rows + W 256 rows) x 64 B (BK = 32).  A 64-B row
+// holds 4 16-B chunks; chunk c of row r is stored at c ^ (((r >> 3) & 1) << 1),
+// which makes the fragment ds_read_b128 conflict-free for gfx950's lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same in the upper half).
+// Per K-step: wait for this slot's DMA (vmcnt(6): the next slot's 6 pieces may
+// still be in flight), barrier, issue the DMA two slots ahead (into the slot
+// every wave finished reading before the barrier), 12 fragment reads, 32 MFMAs.
+// ABL (diagnostic builds only, as gemm_pp_kernel): bit0 no DMA in the K loop,
+// bit1 no MFMA, bit2 no epilogue.
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
+    constexpr int BM = 128, BN = 256, BK = 32, NSLOT = 3;
+    constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 KB + 16 KB
+    constexpr int PIECES = SLOT / 1024, PPW = PIECES / 4;              // 24 pieces, 6 per wave
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * SLOT];  // 72 KB
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+
+    // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; each XCD gets a
+    // contiguous run of tile ids, walked in groups of GM row blocks (column-major
+    // inside a group) so co-resident tiles share A rows and W columns in its L2.
+    const int ntn = a.N / BN, ntm = (a.M + BM - 1) / BM;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    constexpr int GM = 8;
+    const int grp_tiles = GM * ntn, grp = t / grp_tiles, in = t - grp * grp_tiles;
+    const int gm = min(GM, ntm - grp * GM);
+    const int tm = grp * GM + in % gm, tn = in / gm;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int K = a.K;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+
+    // piece p (1 KB = 16 rows x 64 B): 0-7 A rows 16p.., 8-23 W rows 16(p-8)..
+    // lane l writes LDS bytes [16 l, 16 l + 16) of the piece: row l >> 2, stored
+    // chunk l & 3, which holds source chunk (l & 3) ^ (((l >> 5) & 1) << 1).
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    auto stage = [&](int slot, int k0) {
+        uint8_t *base = smem + slot * SLOT;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            const int piece = wave + 4 * i;  // wave-uniform
+            const uint16_t *src = piece < 8 ? Ag + (int64_t)(piece * 16 + prow) * K
+                                            : Wg + (int64_t)((piece - 8) * 16 + prow) * K;
+            __builtin_amdgcn_global_load_lds((const void *)(src + k0 + pchunk * 8), (lds_void_t *)(base + piece * 1024),
+                                             16, 0, 0);
+        }
+    };
+    // fragment of rows r0 + li (r0 % 16 == 0), k chunk g: 16 B at row*64 + (g ^ h(li))*16
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage(0, 0);
+    if (nk > 1) stage(1, BK);
+    for (int kt = 0; kt < nk; ++kt) {
+        // a raw s_barrier: __syncthreads() would add a full vmcnt(0) drain (its
+        // release fence), emptying the DMA pipeline every K-step
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (!(ABL & 1) && kt + 2 < nk) stage((kt + 2) % NSLOT, (kt + 2) * BK);
+        const uint8_t *As = smem + (kt % NSLOT) * SLOT;
+        const uint8_t *Ws = As + A_BYTES;
+        bf16x8 wf[4], af[8];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+            wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + (wave * 64 + ni * 16 + li) * 64 + fchunk);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+            af[mi] = *reinterpret_cast<const bf16x8 *>(As + (mi * 16 + li) * 64 + fchunk);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                if constexpr (!(ABL & 2))
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
+                else
+                    asm volatile("" ::"v"(wf[ni]), "v"(af[mi]));
+        // all 12 fragment reads first (in source order), then the 32 MFMAs: the
+        // compiler's counted lgkmcnt waits let MFMA (mi, *) start once af[mi] lands
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+    }
+
+    if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
+    // epilogue: acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + wave*64 + ni*16 + 4g + j]
+    float4 bias[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
+    __syncthreads();  // every wave's last fragment reads are done: the ring is free
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        // 128 x 256 bf16 tile staged in LDS (512-B rows, 16-B chunk XOR (row & 31)),
+        // stored as whole 512-B row segments, 16 B per lane.
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int cl = wave * 64 + ni * 16 + 4 * g;
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                const int rl = mi * 16 + li;
+                const f32x4 v4 = acc[mi][ni];
+                float v0 = v4[0] + bias[ni].x, v1 = v4[1] + bias[ni].y, v2 = v4[2] + bias[ni].z, v3 = v4[3] + bias[ni].w;
+                if constexpr (EPI == EPI_GELU_BF16) {
+                    const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
+                    v0 = lo.x;
+                    v1 = lo.y;
+                    v2 = hi.x;
+                    v3 = hi.y;
+                }
+                const int off = rl * 512 + (((cl >> 3) ^ (rl & 31)) << 4) + (cl & 7) * 2;
+                *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 256 + tid;
+            const int rl = id >> 5, ch = id & 31;
+            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
+            if (m0 + rl < a.M) *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+        }
+        return;
+    }
+    // f32 epilogues: two halves of 64 rows (64 KB each: 1-KB rows, 16-B chunk XOR
+    // (row & 63)), copied out as whole 1-KB row segments with the residual /
+    // position loads issued back to back before the adds and stores.
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int cl = wave * 64 + ni * 16 + 4 * g;
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq) {
+                const int rl = mq * 16 + li;
+                const f32x4 v4 = acc[h * 4 + mq][ni];
+                *reinterpret_cast<float4 *>(smem + rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4)) =
+                    make_float4(v4[0] + bias[ni].x, v4[1] + bias[ni].y, v4[2] + bias[ni].z, v4[3] + bias[ni].w);
+            }
+        }
+        __syncthreads();
+        float4 add[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 256 + tid;
+            const int rl = id >> 6, ch = id & 63;
+            const int row = m0 + h * 64 + rl;
+            const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
+            if constexpr (EPI == EPI_RESID_F32) {
+                add[it] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
+            } else {
+                const int p = rr % (a.tokens - 1);
+                add[it] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 256 + tid;
+            const int rl = id >> 6, ch = id & 63;
+            const int row = m0 + h * 64 + rl;
+            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
+            const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
+            if (row < a.M) {
+                if constexpr (EPI == EPI_RESID_F32) {
+                    *reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + n0 + ch * 4) = o;
+                } else {
+                    const int np = a.tokens - 1;
+                    const int img = row / np, p = row - img * np;
+                    *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + p) * a.N + n0 + ch * 4) = o;
+                }
+            }
+        }
+        if (h == 0) __syncthreads();  // the second half overwrites the staging rows
     }
 }
 
@@ -947,20 +1158,24 @@ struct SkWorkspace {
 };
 
 // Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
-// 3 = 128x256 8-wave, 0 = auto.  Auto follows interleaved A/B timings on the
-// batch-256 shapes (tools/gemm_micro.py, profiles/): the 256x256 ping-pong kernel
-// everywhere except the short square O-projection (N = K = 768), where 128-row
-// tiles shrink the 2.3-wave tail enough to win.
+// 3 = 128x256 8-wave, 4 = ping-pong, 5 = persistent, 6 = Stream-K, 7 = deferred
+// stores, 8 = two-workgroup 128x256, 0 = auto.  Auto follows interleaved A/B
+// timings on the batch-256 shapes (tools/gemm_calib.py): ping-pong everywhere
+// except the short square projections (gemm_pick).
 enum GemmVariant {
     GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4, GEMM_PERSIST = 5, GEMM_STREAMK = 6,
-    GEMM_DEFERRED = 7
+    GEMM_DEFERRED = 7, GEMM_W2 = 8
 };
 
 inline int gemm_pick(const GemmArgs &a, int variant) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.N % G2_BN != 0) return GEMM_V1;
-    const int tiles256 = ((a.M + 255) / 256) * (a.N / G2_BN);
-    (void)tiles256;
+    // Short square projections (O-proj, patch embed: N = K = 768) finish in
+    // ~2.3 rounds of 256x256 tiles and carry a heavy f32 epilogue (residual /
+    // position read + write): the two-workgroup kernel overlaps that epilogue
+    // with the co-resident workgroup's MFMAs (O-proj 96 -> 89 us at batch 256,
+    // tools/gemm_calib.py).  Everything else streams K at 128 flop/B: ping-pong.
+    if (a.N <= 768 && a.K <= 768) return GEMM_W2;
     return GEMM_PINGPONG;
 }
 
@@ -1043,6 +1258,13 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
             hipLaunchKernelGGL((gemm_persist_kernel<EPI, true>), dim3(G), dim3(512), 0, s, a);
             break;
         }
+        case GEMM_W2: {
+            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            RC_REQUIRE(a.K % 32 == 0, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 32");
+            const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
+            hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3(ntm * ntn), dim3(256), 0, s, a);
+            break;
+        }
         case GEMM_PINGPONG: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
@@ -1050,7 +1272,19 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
             break;
         }
 #if defined(RC_GEMM_ABLATION)
-        case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6: {
+        case 200 + 1: case 200 + 2: case 200 + 4: case 200 + 6: {
+            const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
+            const dim3 gr(ntm * ntn), bl(256);
+            switch (variant - 200) {
+                case 1: hipLaunchKernelGGL((gemm_w2_kernel<EPI, 1>), gr, bl, 0, s, a); break;
+                case 2: hipLaunchKernelGGL((gemm_w2_kernel<EPI, 2>), gr, bl, 0, s, a); break;
+                case 4: hipLaunchKernelGGL((gemm_w2_kernel<EPI, 4>), gr, bl, 0, s, a); break;
+                case 6: hipLaunchKernelGGL((gemm_w2_kernel<EPI, 6>), gr, bl, 0, s, a); break;
+            }
+            break;
+        }
+        case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
+        case 100 + 8: case 100 + 16: case 100 + 24: {
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
             switch (variant - 100) {
@@ -1060,6 +1294,9 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
                 case 4: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 4>), gr, bl, 0, s, a); break;
                 case 5: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 5>), gr, bl, 0, s, a); break;
                 case 6: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 6>), gr, bl, 0, s, a); break;
+                case 8: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 8>), gr, bl, 0, s, a); break;
+                case 16: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 16>), gr, bl, 0, s, a); break;
+                case 24: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 24>), gr, bl, 0, s, a); break;
             }
             break;
         }

@@ -360,8 +360,11 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
         const int ta = m->timers[T_ATTN].begin(s);
         if (m->attn_variant == 1 || T > ATT2_ROWS)
             hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads, scale);
+        else if (T == 197)  // ViT-B/16 at 224x224: the token count as a constant
+            hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f);
         else
-            hipLaunchKernelGGL(attention_v2_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+            hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));

@@ -266,9 +266,13 @@ constexpr int ATT2_TILES = 13, ATT2_ROWS = ATT2_TILES * 16;  // 208 keys
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
+// TOK > 0: the token count as a compile-time constant (197 for ViT-B/16 at 224),
+// so only the last key tile carries the padding mask; TOK = 0 reads `tokens`.
+template <int TOK>
 __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                          int tokens, int heads, float scale_log2e) {
+                                                          int tokens_rt, int heads, float scale_log2e) {
     constexpr int HD = 64;
+    const int tokens = TOK > 0 ? TOK : tokens_rt;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];
     uint8_t *Ks = lds, *Vs = lds + ATT2_ROWS * 128;
     const int H = heads * HD, H3 = 3 * H;
@@ -320,24 +324,29 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
             }
             if (t & 1) asm volatile("" ::: "memory");  // cap the K-fragment loads in flight (VGPRs)
         }
+        // padded keys (only in tiles that reach past `tokens`: a uniform branch)
+        // are masked to -inf; the max runs on the raw scores and the scale is
+        // folded into one fma per score: p = exp2(s·c − max·c), c = log2(e)/8 > 0
+#pragma unroll
+        for (int t = 0; t < ATT2_TILES; ++t)
+            if ((t + 1) * 16 > tokens) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (t * 16 + g * 4 + j >= tokens) st[t][j] = -INFINITY;
+            }
         float mx = -INFINITY;
 #pragma unroll
         for (int t = 0; t < ATT2_TILES; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = t * 16 + g * 4 + j;
-                const float v = key < tokens ? st[t][j] * scale_log2e : -INFINITY;
-                st[t][j] = v;
-                mx = fmaxf(mx, v);
-            }
+            mx = fmaxf(mx, fmaxf(fmaxf(st[t][0], st[t][1]), fmaxf(st[t][2], st[t][3])));
         mx = fmaxf(mx, __shfl_xor(mx, 16));
         mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float nmc = -mx * scale_log2e;
         float sum = 0.f;
 #pragma unroll
         for (int t = 0; t < ATT2_TILES; ++t)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float p = exp2f(st[t][j] - mx);
+                const float p = __builtin_amdgcn_exp2f(fmaf(st[t][j], scale_log2e, nmc));
                 st[t][j] = p;
                 sum += p;
             }
