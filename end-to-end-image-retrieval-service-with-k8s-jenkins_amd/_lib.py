@@ -55,6 +55,25 @@ class VitConfig(C.Structure):
     ]
 
 
+class JpegInfo(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("ncomp", C.c_int32),
+        ("supported", C.c_int32),
+        ("hmax", C.c_int32),
+        ("vmax", C.c_int32),
+        ("restart_interval", C.c_int32),
+        ("mcux", C.c_int32),
+        ("mcuy", C.c_int32),
+        ("h", C.c_int32 * 3),
+        ("v", C.c_int32 * 3),
+        ("bw", C.c_int32 * 3),
+        ("bh", C.c_int32 * 3),
+        ("blocks", C.c_int64),
+    ]
+
+
 _vp = C.c_void_p
 _i64 = C.c_int64
 _i32 = C.c_int
@@ -96,6 +115,11 @@ SIGNATURES = {
     "rc_model_timing_read": (C.c_int, [_vp, _i32, _pd, _pi64, _pd]),
     "rc_model_timing_reset": (C.c_int, [_vp]),
     "rc_gemm_bf16": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp]),
+    "rc_jpeg_probe": (C.c_int, [C.c_char_p, _i64, C.POINTER(JpegInfo)]),
+    "rc_jpeg_decode_coefficients": (C.c_int, [C.c_char_p, _i64, _vp, _vp]),
+    "rc_jpeg_decoder_create": (C.c_int, [_i32, _i32, _i64, C.POINTER(_vp)]),
+    "rc_jpeg_decoder_destroy": (C.c_int, [_vp]),
+    "rc_jpeg_decode": (C.c_int, [_vp, _i32, C.POINTER(C.c_char_p), _pi64, _vp, _pi64, _vp]),
 }
 
 _lock = threading.Lock()

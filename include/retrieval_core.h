@@ -205,6 +205,44 @@ int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, doubl
  * fallbacks = batched calls that re-ran an overflowed query through the exact scan. */
 int rc_index_gemm_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *flops, int64_t *fallbacks);
 
+
+/* ------------------------------------------------------------------------
+ * JPEG decode.  Replaces Image.open(BytesIO(bytes)).convert("RGB") —
+ * embedding/main.py:97 — for baseline JPEGs: Huffman decode on the host
+ * (one thread per image), dequantisation + islow IDCT + fancy upsampling +
+ * YCbCr->RGB on the GPU, bit-exact with Pillow/libjpeg-turbo defaults.
+ * Other streams (progressive, arithmetic, 12-bit, CMYK/RGB colour spaces,
+ * multi-scan) report supported = 0 and stay on the host decode path.
+ * ---------------------------------------------------------------------- */
+typedef struct rc_jpeg_info {
+    int32_t width, height, ncomp, supported;
+    int32_t hmax, vmax, restart_interval, mcux, mcuy;
+    int32_t h[3], v[3];   /* sampling factors per component */
+    int32_t bw[3], bh[3]; /* 8x8 blocks per component plane (MCU padded) */
+    int64_t blocks;       /* coefficient blocks of the image, all planes */
+} rc_jpeg_info;
+typedef struct rc_jpeg_decoder rc_jpeg_decoder;
+
+/* Header walk: size, components, sampling, whether rc_jpeg_decode handles it.
+ * RC_ERR_INVALID if the bytes are not a JPEG stream (the caller's
+ * UnidentifiedImageError path, embedding/main.py:115-119). */
+int rc_jpeg_probe(const uint8_t *jpg, int64_t len, rc_jpeg_info *info);
+/* Host-only entropy decode (test hook): quantised coefficients of every block,
+ * natural order, planes in component order ([blocks][64] int16), and each
+ * component's quantisation table in natural order ([ncomp][64] u16). */
+int rc_jpeg_decode_coefficients(const uint8_t *jpg, int64_t len, int16_t *coef, uint16_t *qtab);
+/* Pinned host staging + device workspace for up to max_images images and
+ * max_blocks coefficient blocks per call (no allocation in rc_jpeg_decode). */
+int rc_jpeg_decoder_create(int device, int max_images, int64_t max_blocks, rc_jpeg_decoder **out);
+int rc_jpeg_decoder_destroy(rc_jpeg_decoder *h);
+/* Decode n JPEGs (host buffers) into device HWC RGB u8: image i is written at
+ * rgb + rgb_offsets[i] (host array, bytes), height x width x 3.  The host
+ * buffers may be reused once the call returns; the reconstruction is ordered
+ * on `stream`.  RC_ERR_UNSUPPORTED if any image is outside what the decoder
+ * handles (probe first), RC_ERR_INVALID for damaged or truncated data. */
+int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens, uint8_t *rgb,
+                   const int64_t *rgb_offsets, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,73 @@
+"""GPU JPEG decode (rc_jpeg_decode) against Pillow's decode of the same bytes —
+the reference's own decode path, embedding/main.py:97.  Integer work: bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import import_pkg
+from jpeg_cases import cases, pil_rgb, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def J(cuda):
+    return import_pkg("jpeg")
+
+
+@pytest.fixture(scope="module")
+def dec(J, cuda):
+    d = J.JpegDecoder(device=0, max_images=128, max_pixels=1 << 21)
+    yield d
+    d.close()
+
+
+def test_batch_of_mixed_streams_bit_exact(dec):
+    cs = cases()
+    outs = dec.decode([d for _, d in cs])
+    for (name, data), got in zip(cs, outs):
+        assert np.array_equal(got.cpu().numpy(), pil_rgb(data)), name
+
+
+@pytest.mark.parametrize("name,data", cases()[::7], ids=[c[0] for c in cases()[::7]])
+def test_single_image_calls_bit_exact(dec, name, data):
+    (got,) = dec.decode([data])
+    assert np.array_equal(got.cpu().numpy(), pil_rgb(data))
+
+
+def test_repeated_calls_reuse_the_staging(dec):
+    datas = [synthetic(224, 224, 100 + i, quality=85, subsampling=2) for i in range(24)]
+    refs = [pil_rgb(d) for d in datas]
+    for _ in range(3):
+        outs = dec.decode(datas)  # no sync between calls: staging reuse must wait for the upload
+        outs2 = dec.decode(datas[::-1])
+        for o, r in zip(outs, refs):
+            assert np.array_equal(o.cpu().numpy(), r)
+        for o, r in zip(outs2, refs[::-1]):
+            assert np.array_equal(o.cpu().numpy(), r)
+
+
+def test_unsupported_stream_raises(J, dec):
+    prog = synthetic(64, 64, 7, quality=80, progressive=True)
+    with pytest.raises(J.JpegUnsupported):
+        dec.decode([synthetic(32, 32, 1), prog])
+
+
+def test_damaged_stream_raises_value_error(dec):
+    data = synthetic(96, 96, 9, quality=90)
+    with pytest.raises(ValueError):
+        dec.decode([data[: len(data) // 2] + b"\xff\xd9"])
+
+
+def test_gpu_decoded_embedding_equals_pil_decoded(dec, cuda):
+    import torch
+
+    vit = import_pkg("vit")
+    from oracle.weights import seeded_vit_msn_weights
+
+    m = vit.VitMsnEmbedder(seeded_vit_msn_weights(1907, num_layers=2), device=0, max_batch=4)
+    data = dict(cases())["test_image"]
+    (img,) = dec.decode([data])
+    raw_gpu, _ = m.embed(img[None])
+    raw_pil, _ = m.embed(torch.from_numpy(pil_rgb(data).copy())[None])
+    assert torch.equal(raw_gpu, raw_pil)
+    m.close()
