@@ -76,6 +76,39 @@ def cpu_embed_baseline(budget_s: float = 12.0):
             "sample": f"{done} images (batches of 8, 224x224 u8) through oracle preprocess + numpy fp32 ViT-MSN-base, {el:.1f}s"}
 
 
+def synthetic_jpegs(n: int, seed: int, size: int = 224) -> list[bytes]:
+    """Baseline 4:2:0 q90 JPEGs of smooth random content plus noise (PIL encoder)."""
+    import io
+
+    from PIL import Image
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        base = rng.integers(0, 256, (size // 8 + 1, size // 8 + 1, 3), dtype=np.uint8)
+        arr = np.asarray(Image.fromarray(base).resize((size, size), Image.BILINEAR)).astype(np.int16)
+        arr = np.clip(arr + rng.integers(-12, 13, arr.shape), 0, 255).astype(np.uint8)
+        b = io.BytesIO()
+        Image.fromarray(arr).save(b, format="JPEG", quality=90, subsampling=2)
+        out.append(b.getvalue())
+    return out
+
+
+def cpu_jpeg_baseline(datas: list[bytes], budget_s: float = 4.0):
+    """The reference decode (embedding/main.py:97: PIL open + convert RGB), one host thread."""
+    import io
+
+    from PIL import Image
+
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or done == 0:
+        Image.open(io.BytesIO(datas[done % len(datas)])).convert("RGB").load()
+        done += 1
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "images/s", "cores": 1, "kind": "reference",
+            "sample": f"{done} decodes of the same 224x224 JPEGs with Pillow (the reference's own decode), {el:.1f}s"}
+
+
 def cpu_search_baseline(n_rows=1_000_000, dim=512, budget_s=6.0):
     from threadpoolctl import threadpool_info
 
@@ -138,6 +171,7 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=5)
     ap.add_argument("--parts", type=int, default=3, help="concurrent batch slices per GPU (rc_model_set_parts)")
     ap.add_argument("--ingest-images", type=int, default=16384, help="config 5 sample per GPU (0 = skip)")
+    ap.add_argument("--jpeg-images", type=int, default=256, help="JPEG decode sample per GPU (0 = skip)")
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -262,6 +296,38 @@ def main():
         sidx5.close()
         del sidx5
 
+    # --------------------------- JPEG decode + decode→embed --
+    jpeg = None
+    if args.jpeg_images > 0:
+        J = importlib.import_module(f"{PKG}.jpeg")
+        datas = synthetic_jpegs(args.jpeg_images, 7000 + rank)
+        dec = J.JpegDecoder(local, max_images=len(datas), max_pixels=len(datas) * 224 * 224)
+        dec.decode(datas)
+        torch.cuda.synchronize()
+        reps = 5
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dec.decode(datas)
+        torch.cuda.synchronize()
+        barrier()
+        eld = max_over_ranks(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            batch = torch.stack(dec.decode(datas)[:B])
+            model.embed(batch, out=(raw, nrm))
+        torch.cuda.synchronize()
+        barrier()
+        ele = max_over_ranks(time.perf_counter() - t0)
+        dec.close()
+        jpeg = {"workload": f"{len(datas)} synthetic 224x224 q90 4:2:0 baseline JPEGs per GPU (~{sum(map(len, datas)) // len(datas) // 1024} KB "
+                            f"each): host Huffman decode (threaded) + HIP islow IDCT / fancy upsampling / YCbCr->RGB, "
+                            f"bit-exact with PIL; host buffers in, device HWC RGB out",
+                "value": world * len(datas) * reps / eld, "unit": "images/s (decode)",
+                "decode_embed": {"value": world * min(B, len(datas)) * reps / ele, "unit": "images/s (JPEG bytes -> embedding)"}}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            jpeg["cpu_baseline"] = cpu_jpeg_baseline(datas)
+
     model.close()
     del images, raw, nrm
     torch.cuda.empty_cache()
@@ -305,6 +371,8 @@ def main():
     }
     if ingest is not None:
         result["ingest"] = ingest
+    if jpeg is not None:
+        result["jpeg"] = jpeg
 
     # ------------------------------------------------- search (secondary) --
     if not args.no_search:

@@ -28,6 +28,7 @@ class Config:
     EMBED_MAX_BATCH = int(os.getenv("RC_EMBED_MAX_BATCH", "32"))
     MODEL_PATH = os.getenv("RC_MODEL_PATH", "")  # local checkpoint dir (config.json + weights)
     WEIGHT_SEED = int(os.getenv("RC_WEIGHT_SEED", "1907"))
+    GPU_JPEG = os.getenv("RC_GPU_JPEG", "1") != "0"  # decode baseline JPEGs on the GPU (bit-exact with PIL)
 
 
 # facebook/vit-msn-base preprocessing (ViTImageProcessor). The checkpoint's

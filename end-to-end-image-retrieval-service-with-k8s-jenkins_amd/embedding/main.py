@@ -7,9 +7,11 @@ Contract kept from the reference (``embedding/main.py:78-124``):
                  400 {"detail": "Uploaded file is not a valid image."} on an unidentifiable image
                  422 when ``file`` is missing; other decode errors propagate (500)
 
-Compute: PIL decode on the host (``:97``), then one ``rc_embed`` call on the GPU
-(resize → normalize → ViT-MSN → final LN of the CLS row) instead of
-``extractor`` + ``model`` (``:107-113``).  ``POST /embed_batch`` (field ``files``,
+Compute: baseline JPEGs are decoded on the GPU (host Huffman + HIP IDCT /
+upsampling / colour, bit-exact with the reference's PIL decode at ``:97``); any
+other image goes through PIL on the host as in the reference.  Then one
+``rc_embed`` call on the GPU (resize → normalize → ViT-MSN → final LN of the CLS
+row) instead of ``extractor`` + ``model`` (``:107-113``).  ``POST /embed_batch`` (field ``files``,
 repeated) returns one vector per image — the batched form of the same contract.
 OpenTelemetry/Prometheus instrumentation of the reference is out of scope.
 """
@@ -57,10 +59,38 @@ def decode_image(data: bytes) -> Image.Image:
         raise HTTPException(status_code=400, detail="Uploaded file is not a valid image.")
 
 
+def _gpu_jpeg(data: bytes) -> bool:
+    if not Config.GPU_JPEG:
+        return False
+    from ..jpeg import is_gpu_decodable
+
+    return is_gpu_decodable(data)
+
+
+def embed_many(blobs: List[bytes]) -> list[list[float]]:
+    """Image bytes → raw CLS vectors: GPU JPEG decode where it applies, PIL otherwise."""
+    out: list = [None] * len(blobs)
+    gpu = [i for i, b in enumerate(blobs) if _gpu_jpeg(b)]
+    host = [i for i in range(len(blobs)) if i not in set(gpu)]
+    images = {i: decode_image(blobs[i]) for i in host}  # validate before touching the model (400 needs no GPU)
+    emb = get_embedder()
+    if gpu:
+        try:
+            for i, v in zip(gpu, emb.embed_jpeg([blobs[i] for i in gpu])):
+                out[i] = v
+        except ValueError:  # a damaged stream: the reference's host decode decides (image or 400)
+            for i in gpu:
+                images[i] = decode_image(blobs[i])
+            host = sorted(images)
+    if host:
+        for i, v in zip(host, emb.embed_pil([images[i] for i in host])):
+            out[i] = v
+    return out
+
+
 def embed_bytes(data: bytes) -> list[float]:
     """Core of /embed: image bytes → raw CLS vector (list of floats)."""
-    image = decode_image(data)  # validate before touching the model (400 needs no GPU)
-    return get_embedder().embed_pil([image])[0]
+    return embed_many([data])[0]
 
 
 @app.get("/")
@@ -96,5 +126,4 @@ async def embed_images(request: Request):
              if p.get_param("name", header="content-disposition") == "files"]
     if not blobs:
         raise _missing_file("files")
-    images = [decode_image(b) for b in blobs]
-    return get_embedder().embed_pil(images)
+    return embed_many(blobs)

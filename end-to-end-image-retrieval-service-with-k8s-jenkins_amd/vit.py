@@ -87,6 +87,7 @@ class VitMsnEmbedder:
         self.device = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index or 0)
         self.max_batch = int(max_batch)
         self.hidden = cfg["hidden_size"]
+        self._jpeg = None  # GPU JPEG decoder, created on first embed_jpeg
         c = _lib.VitConfig(cfg["image_size"], cfg["patch_size"], cfg["hidden_size"], cfg["num_hidden_layers"],
                            cfg["num_attention_heads"], cfg["intermediate_size"], float(cfg["layer_norm_eps"]),
                            self.max_batch)
@@ -114,6 +115,9 @@ class VitMsnEmbedder:
         return cls(sd, device=device, max_batch=max_batch, model_config=cfg, preprocess=pre)
 
     def close(self) -> None:
+        if getattr(self, "_jpeg", None) is not None:
+            self._jpeg.close()
+            self._jpeg = None
         if getattr(self, "_h", None) is not None:
             check(self.lib.rc_model_destroy(self._h))
             self._h = None
@@ -164,6 +168,28 @@ class VitMsnEmbedder:
                 chunk = idx[s:s + self.max_batch]
                 arr = np.stack([np.asarray(images[i].convert("RGB"), dtype=np.uint8) for i in chunk])
                 raw, _ = self.embed(torch.from_numpy(arr), normalized=False)
+                vals = raw.cpu().tolist()
+                for j, i in enumerate(chunk):
+                    out[i] = vals[j]
+        return out  # type: ignore[return-value]
+
+    def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
+        """Baseline-JPEG byte strings → raw CLS vectors, decoded on the GPU (rc_jpeg_decode,
+        bit-exact with the reference's PIL decode) and embedded without a host RGB copy.
+        Raises jpeg.JpegUnsupported for streams the GPU decoder does not handle."""
+        from .jpeg import JpegDecoder
+
+        if self._jpeg is None:
+            self._jpeg = JpegDecoder(self.device, max_images=max(self.max_batch, 32), max_pixels=1 << 24)
+        imgs = self._jpeg.decode(datas)
+        out: list[list[float] | None] = [None] * len(imgs)
+        groups: dict[tuple[int, int], list[int]] = {}
+        for i, im in enumerate(imgs):
+            groups.setdefault(tuple(im.shape[:2]), []).append(i)
+        for idx in groups.values():
+            for s in range(0, len(idx), self.max_batch):
+                chunk = idx[s:s + self.max_batch]
+                raw, _ = self.embed(torch.stack([imgs[i] for i in chunk]), normalized=False)
                 vals = raw.cpu().tolist()
                 for j, i in enumerate(chunk):
                     out[i] = vals[j]

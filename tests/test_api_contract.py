@@ -163,3 +163,28 @@ def test_ingest_then_retrieve_end_to_end(test_image_bytes, cuda):
         idx.upsert([("bad", [0.0] * 768, {})])
     with pytest.raises(ValueError):
         idx.query(vector=[1.0] * 10, top_k=3)
+
+
+@pytest.mark.gpu
+def test_embed_gpu_jpeg_path_equals_pil_path(client, test_image_bytes, cuda, monkeypatch):
+    """/embed on a baseline JPEG decodes on the GPU; the vector equals the host-PIL-decode path's."""
+    import io
+
+    import numpy as np
+    from PIL import Image
+
+    main = import_pkg("embedding.main")
+    J = import_pkg("jpeg")
+    assert J.is_gpu_decodable(test_image_bytes)
+    gpu_vec = client.post("/embed", files={"file": ("t.jpeg", test_image_bytes, "image/jpeg")}).json()
+    monkeypatch.setattr(main.Config, "GPU_JPEG", False)
+    pil_vec = client.post("/embed", files={"file": ("t.jpeg", test_image_bytes, "image/jpeg")}).json()
+    assert gpu_vec == pil_vec
+    monkeypatch.setattr(main.Config, "GPU_JPEG", True)
+    b = io.BytesIO()
+    Image.fromarray(np.full((40, 30, 3), 90, np.uint8)).save(b, format="PNG")
+    r = client.post("/embed_batch", files=[("files", ("a.png", b.getvalue(), "image/png")),
+                                          ("files", ("b.jpeg", test_image_bytes, "image/jpeg"))])
+    assert r.status_code == 200
+    vs = r.json()
+    assert len(vs) == 2 and vs[1] == gpu_vec and len(vs[0]) == 768
