@@ -205,7 +205,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    const int tm = tile / ntn, tn = tile % ntn;
+    int tm = tile / ntn, tn = tile % ntn;
+    if (a.group_m > 0) {  // groups of group_m row tiles, column-major inside a group
+        const int ntm = (a.M + BM - 1) / BM;
+        const int gt = a.group_m * ntn, gi = tile / gt, in = tile - gi * gt;
+        const int gm = min(a.group_m, ntm - gi * a.group_m);
+        tm = gi * a.group_m + in % gm;
+        tn = in / gm;
+    }
     const int m0 = tm * BM, n0 = tn * BN;
     const int K = a.K;
     const uint16_t *Ag = a.A + (int64_t)m0 * K;
@@ -1190,6 +1197,19 @@ inline int gemm_debug_bits() {
     return bits;
 }
 
+// Ping-pong tile order: groups of 8 row tiles (column-major inside a group) when
+// a row has >= 6 column tiles (QKV: 176 -> 170 us, fc1: 285 -> 274 us at batch
+// 256, interleaved A/B in tools/gemm_calib.py), row-major otherwise (fc2 prefers
+// it by 2 %).  RC_GEMM_GM (read once) overrides for A/B runs.
+inline int gemm_group_m(const GemmArgs &a) {
+    static const int env = [] {
+        const char *d = std::getenv("RC_GEMM_GM");
+        return d ? std::atoi(d) : -1;
+    }();
+    if (env >= 0) return env;
+    return a.N / 256 >= 6 ? 8 : 0;
+}
+
 // compute units of the current device (one persistent block per CU)
 inline int gemm_num_cus() {
     static thread_local int dev = -1, cus = 256;
@@ -1209,6 +1229,11 @@ template <int EPI>
 void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *sk = nullptr) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
+    int gm_override = -1;  // A/B hook (rc_gemm_bf16 only): variant + 1000 * G = ping-pong with group_m G
+    if (variant >= 1000) {
+        gm_override = variant / 1000;
+        variant %= 1000;
+    }
     switch (gemm_pick(a, variant)) {
         case GEMM_V1: {
             RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
@@ -1267,6 +1292,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
         }
         case GEMM_PINGPONG: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            a.group_m = gm_override >= 0 ? gm_override : gemm_group_m(a);
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(ntm * ntn), dim3(512), 0, s, a);
             break;

@@ -195,6 +195,41 @@ class VitMsnEmbedder:
                     out[i] = vals[j]
         return out  # type: ignore[return-value]
 
+    def embed_jpeg_stream(self, batches: Iterable[Sequence[bytes]], normalized: bool = True):
+        """Pipelined JPEG bytes → embeddings for a stream of equal-size-image batches
+        (bulk ingest): batch i+1 is Huffman-decoded on a host worker thread and
+        reconstructed on a side stream while the GPU embeds batch i.  Yields
+        (raw, normed) device tensors per batch (valid until the next iteration)."""
+        import concurrent.futures as cf
+
+        from .jpeg import JpegDecoder
+
+        if self._jpeg is None:
+            self._jpeg = JpegDecoder(self.device, max_images=max(self.max_batch, 32), max_pixels=1 << 24)
+        dec = self._jpeg
+        side = torch.cuda.Stream(device=self.device)
+        main = torch.cuda.current_stream(self.device)
+
+        def decode(datas):
+            with torch.cuda.device(self.device), torch.cuda.stream(side):
+                imgs = dec.decode(datas, stream=side)
+                x = torch.stack(imgs)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return x, ev
+
+        it = iter(batches)
+        with cf.ThreadPoolExecutor(1) as ex:
+            first = next(it, None)
+            fut = ex.submit(decode, first) if first is not None else None
+            while fut is not None:
+                x, ev = fut.result()
+                nxt = next(it, None)
+                fut = ex.submit(decode, nxt) if nxt is not None else None
+                main.wait_event(ev)
+                x.record_stream(main)
+                yield self.embed(x, normalized=normalized)
+
     # ------------------------------------------------------------- timing --
     def timing(self, enable: bool | Iterable[str]) -> None:
         """Enable event timing for all kernels (True), none (False) or the named ones."""

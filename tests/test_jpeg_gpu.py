@@ -71,3 +71,19 @@ def test_gpu_decoded_embedding_equals_pil_decoded(dec, cuda):
     raw_pil, _ = m.embed(torch.from_numpy(pil_rgb(data).copy())[None])
     assert torch.equal(raw_gpu, raw_pil)
     m.close()
+
+
+def test_embed_jpeg_stream_matches_unpipelined(cuda):
+    """Pipelined decode (worker thread + side stream) -> embed equals embedding PIL-decoded pixels."""
+    import torch
+
+    vit = import_pkg("vit")
+    from oracle.weights import seeded_vit_msn_weights
+
+    m = vit.VitMsnEmbedder(seeded_vit_msn_weights(1907, num_layers=2), device=0, max_batch=8)
+    batches = [[synthetic(224, 224, 300 + 8 * b + i, quality=90, subsampling=2) for i in range(8)] for b in range(4)]
+    got = [raw.clone() for raw, _ in m.embed_jpeg_stream(batches)]
+    for b, datas in enumerate(batches):
+        ref, _ = m.embed(torch.from_numpy(np.stack([pil_rgb(d) for d in datas])))
+        assert torch.equal(got[b], ref)
+    m.close()
