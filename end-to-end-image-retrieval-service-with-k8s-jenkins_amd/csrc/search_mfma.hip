@@ -275,6 +275,175 @@ __global__ __launch_bounds__(512, 1) void filter_gemm_kernel(FilterArgs a) {
     if (grp == 0) bar();  // balance the stagger barrier
 }
 
+// Query-stationary filter GEMM (ld = 64·NKT <= 512).  The filter GEMM above
+// streams BOTH operands through LDS (256 queries x 256 rows per 64 KB K-step:
+// 128 flop/B), which the L2->LDS fill rate caps near 45 % of MFMA peak.  Here a
+// block's 256 queries live in REGISTERS for the whole launch and only index rows
+// stream: one wave per SIMD (4 waves, up to 512 VGPRs each), wave w holds
+// queries [64w, 64w+64) of the block's query group as 4 x 2·NKT B-fragments
+// (256 VGPRs at ld 512) plus a 64 x 128 f32 accumulator (128 VGPRs).  Rows come
+// in 128-row tiles, one 16 KB K-step (128 rows x 64) per stage of an 8-deep LDS
+// ring (7 steps ≈ 112 KB in flight: enough to hide the HBM latency of a row
+// tile's first touch): 2·256·128·64 flop per 16 KB = 256 flop/B, half the fill
+// bytes of filter_gemm_kernel.  DMA through a per-step buffer descriptor (uniform
+// base, 32-bit lane offsets) keeps addresses out of the VGPR budget.
+// MFMA roles as above (A = index rows, B = queries): lane (li, g) of acc[rf][qt]
+// holds rows 16·rf + 4g + j of query 16·qt + li.  Same thresholds, candidate
+// appends and exactness argument as filter_gemm_kernel.
+constexpr int QS_RT = 128, QS_NS = 8, QS_QT = 2, QS_WAVES = 8;
+#ifndef QS_STAGGER
+#define QS_STAGGER 0
+#endif
+
+// ABL (A/B diagnostics, RC_FILTER_ABL; 0 in production): bit0 no DMA in the loop,
+// bit1 no MFMA, bit2 no fragment reads (MFMAs on the query registers).
+template <typename T, int NKT, int ABL = 0>
+__global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
+    using Op = MfmaOp<T>;
+    using v8 = typename Op::v8;
+    constexpr int STEP_BYTES = QS_RT * 128;  // 16 KB
+    __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+
+    const int b = blockIdx.x, xcd = b & 7, jx = b >> 3;
+    const int qb = jx % a.nqb;
+    const int64_t chunk = (int64_t)(jx / a.nqb) * 8 + xcd;
+    const int64_t rt_total = (a.r_end - a.r_begin + QS_RT - 1) / QS_RT;
+    const int64_t rt0 = chunk * a.tiles_per_chunk;
+    const int64_t rt1 = min(rt_total, rt0 + a.tiles_per_chunk);
+    if (rt0 >= rt1) return;  // block-uniform
+    const int64_t ld = a.ld;
+    const int ntiles = (int)(rt1 - rt0);  // per-block counters in 32 bits: uniform SALU compares
+    const int nsteps = ntiles * NKT;
+    const uint16_t *Rg = (const uint16_t *)a.rows + (a.r_begin + rt0 * QS_RT) * ld;
+
+    // this lane's query fragments for the whole K: qf[qt][kk], kk = 32-wide k chunk
+    v8 qf[QS_QT][2 * NKT];
+    const int q0 = qb * SB_TILE + wave * 16 * QS_QT;
+#pragma unroll
+    for (int qt = 0; qt < QS_QT; ++qt)
+#pragma unroll
+        for (int kk = 0; kk < 2 * NKT; ++kk)
+            qf[qt][kk] = *reinterpret_cast<const v8 *>((const uint16_t *)a.qh + (int64_t)(q0 + qt * 16 + li) * ld +
+                                                       kk * 32 + g * 8);
+    float thr[QS_QT];
+#pragma unroll
+    for (int qt = 0; qt < QS_QT; ++qt) thr[qt] = a.thr[q0 + qt * 16 + li];
+    // consume the query loads here, so the compiler's vmcnt waits for them sit
+    // before the K loop instead of inside it (where they would drain the DMA ring)
+#pragma unroll
+    for (int qt = 0; qt < QS_QT; ++qt) {
+        asm volatile("" ::"v"(thr[qt]));
+#pragma unroll
+        for (int kk = 0; kk < 2 * NKT; ++kk) asm volatile("" ::"v"(qf[qt][kk]));
+    }
+
+    // step t = (tile, k-step): 16 pieces of 1 KB (8 rows x 128 B); wave w issues pieces w + 8i.
+    constexpr int PPW = 16 / QS_WAVES;
+    uint32_t loff[PPW];  // byte offset of this lane's 16 B within the step's rows
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int r = (wave + QS_WAVES * i) * 8 + (lane >> 3);
+        loff[i] = (uint32_t)(r * (int)ld + (((lane & 7) ^ ((r >> 1) & 7)) << 3)) * 2u;
+    }
+    auto issue = [&](int t) {
+        const int tile = t / NKT;
+        const int ks = (int)(t - tile * NKT);
+        uint8_t *base = smem + (int)(t % QS_NS) * STEP_BYTES;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Rg + (int64_t)tile * QS_RT * ld + ks * 64), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PPW; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(base + (wave + QS_WAVES * i) * 1024), 16, loff[i],
+                                                     0, 0, 0);
+    };
+    // one barrier per PAIR of k-steps (nsteps is even): steps t, t+1 land together,
+    // steps t+6, t+7 go into the two slots freed by t-2, t-1; 6 steps in flight
+    for (int t = 0; t < min(QS_NS - 2, nsteps); ++t) issue(t);
+
+    f32x4_t acc[8][QS_QT];
+    for (int tile = 0; tile < ntiles; ++tile) {
+#pragma unroll
+        for (int rf = 0; rf < 8; ++rf)
+#pragma unroll
+            for (int qt = 0; qt < QS_QT; ++qt) acc[rf][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kp = 0; kp < NKT / 2; ++kp) {
+            const int t = tile * NKT + 2 * kp;
+            // steps t, t+1 landed: the 4 younger steps t+2..t+5 (PPW = 2 DMAs each) may be in flight
+            static_assert(PPW == 2 && NKT % 2 == 0, "vmcnt below assumes 2 DMAs per wave per step, paired steps");
+            if (t + QS_NS - 3 < nsteps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave's DMA of t, t+1 landed; slots of t-2, t-1 are free
+            asm volatile("" ::: "memory");
+            if (QS_STAGGER && wave >= 4) __builtin_amdgcn_s_sleep(QS_STAGGER);  // SIMD partners out of phase
+            if (!(ABL & 1) && t + QS_NS - 2 < nsteps) issue(t + QS_NS - 2);
+            if (!(ABL & 1) && t + QS_NS - 1 < nsteps) issue(t + QS_NS - 1);
+            // per k-step and k half: 2 groups of 4 row fragments (4 reads in flight, then
+            // their 8 MFMAs with counted lgkmcnt waits; the SIMD partner wave's MFMAs cover
+            // the rest).  Row r = 16 rf + li: its swizzle (r >> 1) & 7 = (li >> 1) & 7 does
+            // not depend on rf.
+#pragma unroll
+            for (int kl = 0; kl < 2; ++kl) {
+                const uint8_t *S = smem + ((t + kl) % QS_NS) * STEP_BYTES;
+                const int ks = 2 * kp + kl;
+#pragma unroll
+                for (int sh = 0; sh < 2; ++sh) {
+                    const uint8_t *Sr = S + li * 128 + (((sh * 4 + g) ^ ((li >> 1) & 7)) << 4);
+#pragma unroll
+                    for (int rh = 0; rh < 2; ++rh) {
+                        v8 rfr[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            rfr[i] = (ABL & 4) ? qf[i & 1][(ks * 2 + sh + i) % (2 * NKT)]
+                                               : *reinterpret_cast<const v8 *>(Sr + (rh * 4 + i) * 2048);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+#pragma unroll
+                            for (int qt = 0; qt < QS_QT; ++qt)
+                                if constexpr (!(ABL & 2))
+                                    acc[rh * 4 + i][qt] = Op::mma(rfr[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
+                                else
+                                    asm volatile("" ::"v"(rfr[i]));
+                        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                    }
+                }
+            }
+        }
+        // ---- epilogue of row tile rt0 + tile: candidates s' >= thr[q]
+        const int64_t rbase = a.r_begin + (rt0 + tile) * QS_RT + 4 * g;
+#pragma unroll
+        for (int qt = 0; qt < QS_QT; ++qt) {
+            const float th = thr[qt];
+            float m = -INFINITY;
+#pragma unroll
+            for (int rf = 0; rf < 8; ++rf) {
+                const f32x4_t v = acc[rf][qt];
+                m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+            }
+            if (__ballot(m >= th) == 0) continue;  // wave-uniform: the common case
+            if (m >= th) {
+                const int q = q0 + qt * 16 + li;
+#pragma unroll
+                for (int rf = 0; rf < 8; ++rf)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t row = rbase + rf * 16 + j;
+                        if (acc[rf][qt][j] >= th && row < a.r_end) {
+                            const uint32_t pos = atomicAdd(&a.cnt[q], 1u);
+                            if ((int)pos < a.cap) a.cand[(int64_t)q * a.cap + pos] = (uint32_t)row;
+                        }
+                    }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------- exact rescoring --
 // One block per query.  Candidates are scored exactly as scan_topk_kernel
 // scores a row (16 lanes per row, 16-B chunks, f32 FMA in chunk order, DPP
@@ -403,6 +572,16 @@ void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipSt
     }
 }
 
+// Filter kernel choice: 0 = auto (query-stationary for ld <= 512), 1 = the
+// two-operand-streaming kernel (RC_FILTER_VARIANT, read once; A/B runs).
+inline int filter_variant() {
+    static const int v = [] {
+        const char *d = std::getenv("RC_FILTER_VARIANT");
+        return d ? std::atoi(d) : 0;
+    }();
+    return v;
+}
+
 int batch_stage_ratio(int k, int cap) {
     const int g = cap / (5 * k / 2 + 1);
     return std::max(2, std::min(64, g));
@@ -429,7 +608,24 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
         const int64_t tpc = (rt_total + nchunk - 1) / nchunk;
         FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), b0, b1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
         const int slot = timer ? timer->begin(s) : -1;
-        hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
+        const int nkt = (int)(p.ld / 64);
+        if (filter_variant() != 1 && (nkt == 2 || nkt == 4 || nkt == 8)) {
+            fa.tiles_per_chunk = ((b1 - b0 + QS_RT - 1) / QS_RT + nchunk - 1) / nchunk;
+            const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * QS_WAVES);
+            static const int abl = [] {
+                const char *d = std::getenv("RC_FILTER_ABL");
+                return d ? std::atoi(d) : 0;
+            }();
+            if (nkt == 8 && abl == 1) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 1>), gr, bl, 0, s, fa);
+            else if (nkt == 8 && abl == 2) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 2>), gr, bl, 0, s, fa);
+            else if (nkt == 8 && abl == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 4>), gr, bl, 0, s, fa);
+            else if (nkt == 8 && abl == 6) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 6>), gr, bl, 0, s, fa);
+            else if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8>), gr, bl, 0, s, fa);
+            else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4>), gr, bl, 0, s, fa);
+            else hipLaunchKernelGGL((filter_qs_kernel<T, 2>), gr, bl, 0, s, fa);
+        } else {
+            hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
+        }
         RC_LAUNCH_CHECK();
         if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(b1 - b0) * (double)p.ld);
         launch_rescore<T>(p, ws, b1 == p.n_rows ? 1 : 0, s);
