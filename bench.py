@@ -443,7 +443,7 @@ def main():
             "value": nqb * args.batch_reps / bel,
             "unit": "queries/s",
             "ms_per_batch": bel / args.batch_reps * 1e3,
-            "roofline": {"kernel": "filter_gemm_kernel<f16> (256q x 256 rows x 64 MFMA tiles, candidate epilogue)",
+            "roofline": {"kernel": "filter_qs_kernel<f16,8> (256 queries in registers x 128-row tiles, 8-deep LDS ring, candidate epilogue)",
                          "bound": "mfma", "achieved": g_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": g_tf / PEAK_BF16_TFLOPS, "traffic": load_profile_traffic("filter_f16"),
                          "avg_launch_ms": g_ms / max(g_n, 1), "launches": g_n,

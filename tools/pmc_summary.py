@@ -65,7 +65,7 @@ def main():
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
     if "--latest" in sys.argv:
         keys = {"fc1": "gemm_pp_kernel<1, 0>", "scan_f16": "scan_topk_kernel<f16_t, 4, 1, 128>",
-                "filter_f16": "filter_gemm_kernel<f16_t>"}
+                "filter_f16": "filter_qs_kernel<f16_t, 8, 0>"}
         latest = {}
         for key, kname in keys.items():
             recs = [r for r in out.values() if r["kernel"] == kname]
