@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--batch-reps", type=int, default=3)
     ap.add_argument("--roofline-steps", type=int, default=5)
     ap.add_argument("--parts", type=int, default=3, help="concurrent batch slices per GPU (rc_model_set_parts)")
+    ap.add_argument("--full-last-layer", action="store_true",
+                    help="run the last encoder layer on every row (default: CLS rows only, rc_model_set_last_layer)")
     ap.add_argument("--ingest-images", type=int, default=16384, help="config 5 sample per GPU (0 = skip)")
     ap.add_argument("--jpeg-images", type=int, default=256, help="JPEG decode sample per GPU (0 = skip)")
     ap.add_argument("--no-search", action="store_true")
@@ -207,6 +209,7 @@ def main():
     B = args.batch
     model = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=local, max_batch=B)
     model.set_parts(args.parts)
+    model.set_last_layer(not args.full_last_layer)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     images = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
     raw = torch.empty((B, 768), dtype=torch.float32, device=dev)
@@ -245,7 +248,9 @@ def main():
     fc1_avg_ms = fc1_ms / max(fc1_n, 1)
     fc1_flops_launch = fc1_flops / max(fc1_n, 1)
     achieved = fc1_flops_launch / (fc1_avg_ms / 1e3) / 1e12
-    gflop = vit.gflop_per_image()
+    # FLOPs rc_embed executes per image (the CLS-only last layer skips the rows
+    # /embed never returns); the full-model figure is reported beside it
+    gflop = vit.gflop_per_image(cls_only_last=not args.full_last_layer)
     model_tflops = imgs_per_s / world * gflop / 1e3
 
     # ------------------------------------ config 5: end-to-end ingest + retrieve --
@@ -371,6 +376,10 @@ def main():
             "concurrent_avg_launch_ms": fc1c_ms / max(fc1c_n, 1),
         },
         "embed_parts": args.parts,
+        "last_layer": "full" if args.full_last_layer else
+        "CLS rows only after QKV (the rows /embed returns, embedding/main.py:113)",
+        "gflop_per_image_executed": gflop,
+        "gflop_per_image_full_model": vit.gflop_per_image(),
         "model_tflops_per_gpu": model_tflops,
         "model_mfma_frac": model_tflops / PEAK_BF16_TFLOPS,
     }

@@ -1164,18 +1164,73 @@ struct SkWorkspace {
     }
 };
 
+// Skinny GEMM for M <= 256 (the last layer's CLS rows: O-proj, fc1, fc2 with
+// M = images in the slice).  A 256-row tile kernel would put the whole launch on
+// N/256 CUs with the full K loop on each (fc2: 3 CUs x 3072-deep); here every
+// wave owns 16 rows x 16·NI columns over the whole K, operands straight from
+// global memory (W is 1.2-4.7 MB, L2-resident after the first row tile), so the
+// launch spreads over ceil(M/16)·N/(16·NI) waves.  Swapped operands as in the
+// tiled kernels: the A-operand is 16 weight rows, so lane (g, li) ends with
+// activation row li, output columns 4g..4g+3 of each 16-column group.
+template <int EPI, int NI>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nct * nrt) return;
+    const int ct = w % nct, rt = w / nct;
+    const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
+    const uint16_t *Ar = a.A + (int64_t)row * K + 8 * g;
+    const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
+    f32x4 acc[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int k0 = 0; k0 < K; k0 += 32) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8 *>(Ar + k0);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+            const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(Wr + (int64_t)ni * 16 * K + k0);
+            acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af, acc[ni], 0, 0, 0);
+        }
+    }
+    if (row >= a.M) return;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+        const int c = n0 + ni * 16 + 4 * g;
+        const float4 b = *reinterpret_cast<const float4 *>(a.bias + c);
+        float v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
+        if constexpr (EPI == EPI_RESID_F32) {
+            float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + c);
+            const float4 r = *o;
+            *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
+        } else {
+            if constexpr (EPI == EPI_GELU_BF16) {
+                const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
+                v0 = lo.x;
+                v1 = lo.y;
+                v2 = hi.x;
+                v3 = hi.y;
+            }
+            *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * a.N + c) =
+                make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        }
+    }
+}
+
 // Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
 // 3 = 128x256 8-wave, 4 = ping-pong, 5 = persistent, 6 = Stream-K, 7 = deferred
-// stores, 8 = two-workgroup 128x256, 0 = auto.  Auto follows interleaved A/B
+// stores, 8 = two-workgroup 128x256, 9 = skinny (M <= 256), 0 = auto.  Auto follows interleaved A/B
 // timings on the batch-256 shapes (tools/gemm_calib.py): ping-pong everywhere
 // except the short square projections (gemm_pick).
 enum GemmVariant {
     GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4, GEMM_PERSIST = 5, GEMM_STREAMK = 6,
-    GEMM_DEFERRED = 7, GEMM_W2 = 8
+    GEMM_DEFERRED = 7, GEMM_W2 = 8, GEMM_SKINNY = 9
 };
 
-inline int gemm_pick(const GemmArgs &a, int variant) {
+inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL: ablation builds, RC_GEMM_ABLATION)
+    if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
     if (a.N % G2_BN != 0) return GEMM_V1;
     // Short square projections (O-proj, patch embed: N = K = 768) finish in
     // ~2.3 rounds of 256x256 tiles and carry a heavy f32 epilogue (residual /
@@ -1234,7 +1289,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
         gm_override = variant / 1000;
         variant %= 1000;
     }
-    switch (gemm_pick(a, variant)) {
+    switch (gemm_pick(a, variant, EPI == EPI_PATCH_F32)) {
         case GEMM_V1: {
             RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
             const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
@@ -1288,6 +1343,13 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
             RC_REQUIRE(a.K % 32 == 0, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 32");
             const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
             hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3(ntm * ntn), dim3(256), 0, s, a);
+            break;
+        }
+        case GEMM_SKINNY: {
+            RC_REQUIRE(EPI != EPI_PATCH_F32 && a.N % 32 == 0 && a.M >= 1, RC_ERR_UNSUPPORTED,
+                       "skinny GEMM: bf16 / GELU / residual epilogues, N a multiple of 32");
+            const int waves = ((a.M + 15) / 16) * (a.N / 32);
+            hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
             break;
         }
         case GEMM_PINGPONG: {

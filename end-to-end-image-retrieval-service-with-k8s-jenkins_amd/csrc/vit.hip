@@ -127,6 +127,10 @@ struct rc_model {
     int Mp = 0, Pp = 0;
     uint16_t *patches = nullptr, *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
+    // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
+    bool cls_only_last = true;     // rc_model_set_last_layer / RC_EMBED_FULL_LAST=1
+    float *cls_hidden = nullptr;
+    uint16_t *cls_ln = nullptr, *cls_attn = nullptr, *cls_mlp = nullptr;
     uint8_t *resized = nullptr, *resize_tmp = nullptr;
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
@@ -331,6 +335,33 @@ void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint
     m->timers[T_LN].end(t, s, (double)M * m->cfg.hidden * 6.0);
 }
 
+// Last encoder layer after its QKV GEMM, for the CLS rows only (see
+// attention_cls_kernel): gather the n CLS rows of the residual stream into
+// cls_hidden[i0 ..], CLS-query attention, then O-proj (+residual), LN2, fc1+GELU
+// and fc2 (+residual) as M = n GEMMs on the compact rows.  The kernels are the
+// full-batch ones (a GEMM row's result does not depend on M), so a CLS row gets
+// the same arithmetic as in the full layer except attention's summation order.
+void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *qkv, const float *hidden, float scale,
+                    hipStream_t s) {
+    const auto &c = m->cfg;
+    const int H = c.hidden, T = m->tokens;
+    float *hc = m->cls_hidden + (int64_t)i0 * H;
+    uint16_t *ac = m->cls_attn + (int64_t)i0 * H, *lc = m->cls_ln + (int64_t)i0 * H;
+    uint16_t *mc = m->cls_mlp + (int64_t)i0 * c.mlp;
+    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, T, hc);
+    RC_LAUNCH_CHECK();
+    const int ta = m->timers[T_ATTN].begin(s);
+    const int items = n * c.heads;
+    hipLaunchKernelGGL(attention_cls_kernel, dim3((items + 3) / 4), dim3(256), 0, s, qkv, ac, T, c.heads, items,
+                       scale * 1.4426950408889634f);
+    RC_LAUNCH_CHECK();
+    m->timers[T_ATTN].end(ta, s, 4.0 * items * (double)T * (H / c.heads));
+    gemm<EPI_RESID_F32>(m, GemmArgs{ac, L.w_o, L.b_o, n, H, H, nullptr, hc, nullptr, 1}, s);
+    layernorm(m, hc, L.ln2_w, L.ln2_b, lc, n, s);
+    gemm<EPI_GELU_BF16>(m, GemmArgs{lc, L.w_fc1, L.b_fc1, n, c.mlp, H, mc, nullptr, nullptr, 1}, s);
+    gemm<EPI_RESID_F32>(m, GemmArgs{mc, L.w_fc2, L.b_fc2, n, H, c.mlp, nullptr, hc, nullptr, 1}, s);
+}
+
 // Encoder for images [i0, i0 + n) of the batch (their patches already built):
 // CLS + pos, patch GEMM, 12 layers, final LN on the CLS rows.  Every buffer is
 // addressed from the first image's rows, so two parts of a batch can run on two
@@ -357,6 +388,10 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
         const Layer &L = m->layers[l];
         layernorm(m, hidden, L.ln1_w, L.ln1_b, ln, M, s);
         gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
+        if (m->cls_only_last && l == c.layers - 1) {
+            last_layer_cls(m, L, i0, n, qkv, hidden, scale, s);
+            break;
+        }
         const int ta = m->timers[T_ATTN].begin(s);
         if (m->attn_variant == 1 || T > ATT2_ROWS)
             hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads, scale);
@@ -374,7 +409,9 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
         gemm<EPI_RESID_F32>(m, GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T}, s);
     }
     // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
-    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, hidden, T, m->lnf_w, m->lnf_b, c.ln_eps,
+    const float *fin = m->cls_only_last ? m->cls_hidden + (int64_t)i0 * H : hidden;
+    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, fin, m->cls_only_last ? 1 : T, m->lnf_w, m->lnf_b,
+                       c.ln_eps,
                        raw + (int64_t)i0 * H, normed ? normed + (int64_t)i0 * H : nullptr);
     RC_LAUNCH_CHECK();
 }
@@ -442,6 +479,16 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->attn = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->mlp = (uint16_t *)m->alloc((size_t)m->Mp * cfg->mlp * 2);
             m->resized = (uint8_t *)m->alloc((size_t)B * cfg->image_size * cfg->image_size * 3);
+            const int Cp = B + gemm_row_pad();  // compact CLS streams (+ the rows a tile reads past n)
+            m->cls_hidden = (float *)m->alloc((size_t)Cp * H * 4);
+            m->cls_ln = (uint16_t *)m->alloc((size_t)Cp * H * 2);
+            m->cls_attn = (uint16_t *)m->alloc((size_t)Cp * H * 2);
+            m->cls_mlp = (uint16_t *)m->alloc((size_t)Cp * cfg->mlp * 2);
+            RC_HIP(hipMemset(m->cls_hidden, 0, (size_t)Cp * H * 4));
+            RC_HIP(hipMemset(m->cls_ln, 0, (size_t)Cp * H * 2));
+            RC_HIP(hipMemset(m->cls_attn, 0, (size_t)Cp * H * 2));
+            RC_HIP(hipMemset(m->cls_mlp, 0, (size_t)Cp * cfg->mlp * 2));
+            if (const char *fl = std::getenv("RC_EMBED_FULL_LAST")) m->cls_only_last = std::atoi(fl) == 0;
             // pad rows are read by the GEMM tiles: keep them finite (zero) forever
             RC_HIP(hipMemset(m->patches, 0, (size_t)m->Pp * m->kpatch * 2));
             RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
@@ -612,6 +659,14 @@ int rc_model_set_parts(rc_model *m, int parts) {
         RC_REQUIRE(parts >= 1 && parts <= kMaxParts, RC_ERR_INVALID, "parts must be in [1, 4]");
         std::lock_guard<std::mutex> lk(m->mu);
         m->split = parts;
+    });
+}
+
+int rc_model_set_last_layer(rc_model *m, int cls_only) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->cls_only_last = cls_only != 0;
     });
 }
 

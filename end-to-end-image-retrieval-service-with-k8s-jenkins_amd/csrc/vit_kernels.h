@@ -523,6 +523,101 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const uint16_t *__res
     }
 }
 
+// ------------------------------------------------- last layer, CLS rows only
+// /embed returns last_hidden_state[:, 0, :] (embedding/main.py:113-114), and in
+// the last encoder layer (modeling_vit_msn.py:254-283) row 0 of an image depends
+// only on its own query row plus every token's K and V.  So the last layer runs
+// LN1 + QKV over all rows, then attention for the CLS query alone and O-proj /
+// LN2 / MLP on the n CLS rows gathered into a compact [n][768] stream.
+
+// hc[i][:] = hidden[i * tokens][:]   (one block of 192 lanes per image, float4)
+__global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict__ hidden, int tokens,
+                                                        float *__restrict__ hc) {
+    constexpr int H = 768;
+    const int img = blockIdx.x;
+    reinterpret_cast<float4 *>(hc + (int64_t)img * H)[threadIdx.x] =
+        reinterpret_cast<const float4 *>(hidden + (int64_t)img * tokens * H)[threadIdx.x];
+}
+
+// CLS-query attention, one wave per (image, head), tokens <= 256, head dim 64.
+// Numerics follow attention_v2_kernel: f32 dot products of the bf16 q/k rows,
+// p = exp2(s·c − max·c) with c = log2(e)/8, P rounded to bf16 for P·V, f32 sum
+// of the unrounded p, out = (P·V)·(1/sum) rounded to bf16.
+// Scores: lane j owns keys j, j+64, j+128, j+192 (16-B loads of its key row);
+// P·V: lane d owns output dim d (one coalesced 128-B V row read per key).
+__global__ __launch_bounds__(256) void attention_cls_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+                                                           int tokens, int heads, int items, float scale_log2e) {
+    constexpr int HD = 64, MAXT = 256;
+    __shared__ float ps[4][MAXT];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int item = blockIdx.x * 4 + w;
+    const bool live = item < items;
+    const int img = live ? item / heads : 0, h = live ? item % heads : 0;
+    const int H = heads * HD, H3 = 3 * H;
+    const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD;
+    float sum = 0.f;
+    if (live) {
+        float q[HD];
+        const uint4 *q4 = reinterpret_cast<const uint4 *>(base);
+#pragma unroll
+        for (int i = 0; i < HD / 8; ++i) {
+            const uint4 u = q4[i];
+            const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                q[8 * i + 2 * j] = __uint_as_float(wv[j] << 16);
+                q[8 * i + 2 * j + 1] = __uint_as_float(wv[j] & 0xffff0000u);
+            }
+        }
+        float s[MAXT / 64];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < MAXT / 64; ++j) {
+            const int t = lane + 64 * j;
+            s[j] = -INFINITY;
+            if (t < tokens) {
+                const uint4 *k4 = reinterpret_cast<const uint4 *>(base + (int64_t)t * H3 + H);
+                float acc = 0.f;
+#pragma unroll
+                for (int i = 0; i < HD / 8; ++i) {
+                    const uint4 u = k4[i];
+                    const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        acc = fmaf(q[8 * i + 2 * e], __uint_as_float(wv[e] << 16), acc);
+                        acc = fmaf(q[8 * i + 2 * e + 1], __uint_as_float(wv[e] & 0xffff0000u), acc);
+                    }
+                }
+                s[j] = acc;
+                mx = fmaxf(mx, acc);
+            }
+        }
+        mx = wave_max(mx);
+        const float nmc = -mx * scale_log2e;
+#pragma unroll
+        for (int j = 0; j < MAXT / 64; ++j) {
+            const int t = lane + 64 * j;
+            if (t < tokens) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[j], scale_log2e, nmc));
+                sum += p;
+                ps[w][t] = (float)(__bf16)p;
+            }
+        }
+        sum = wave_sum(sum);
+    }
+    __syncthreads();
+    if (!live) return;
+    const uint16_t *vcol = base + 2 * H + lane;
+    float o0 = 0.f, o1 = 0.f;
+    int t = 0;
+    for (; t + 1 < tokens; t += 2) {
+        o0 = fmaf(ps[w][t], bf16_to_f32(vcol[(int64_t)t * H3]), o0);
+        o1 = fmaf(ps[w][t + 1], bf16_to_f32(vcol[(int64_t)(t + 1) * H3]), o1);
+    }
+    if (t < tokens) o0 = fmaf(ps[w][t], bf16_to_f32(vcol[(int64_t)t * H3]), o0);
+    out[(int64_t)img * H + h * HD + lane] = f32_to_bf16((o0 + o1) * (1.0f / sum));
+}
+
 // ---------------------------------------------------------------- preprocess
 // Pillow 8bpc separable resample (horizontal then vertical), fixed point 22 bits.
 __device__ __forceinline__ uint8_t clip8_fixed(int acc) {

@@ -245,6 +245,10 @@ class VitMsnEmbedder:
         """Encode batches as ``parts`` concurrent slices on separate streams (1 = one stream)."""
         check(self.lib.rc_model_set_parts(self._h, int(parts)))
 
+    def set_last_layer(self, cls_only: bool) -> None:
+        """Run the last encoder layer on the CLS rows only (default) or on every row."""
+        check(self.lib.rc_model_set_last_layer(self._h, int(bool(cls_only))))
+
     def timing_reset(self) -> None:
         check(self.lib.rc_model_timing_reset(self._h))
 
@@ -256,15 +260,23 @@ class VitMsnEmbedder:
         return ms.value, n.value, w.value
 
 
-def gflop_per_image(cfg: dict = VIT_MSN_BASE) -> float:
-    """Algorithmic FLOPs (2 x MACs) of one ViT forward incl. attention (35.126 GFLOP)."""
+def gflop_per_image(cfg: dict = VIT_MSN_BASE, cls_only_last: bool = False) -> float:
+    """FLOPs (2 x MACs) of one ViT forward incl. attention (35.126 GFLOP).
+
+    ``cls_only_last``: the FLOPs ``rc_embed`` executes when the last layer runs
+    attention / O-proj / MLP for the CLS row only (rc_model_set_last_layer):
+    LN1 + QKV stay on all T rows, the rest shrinks to one row (32.93 GFLOP).
+    """
     H, F, L = cfg["hidden_size"], cfg["intermediate_size"], cfg["num_hidden_layers"]
     P = cfg["patch_size"]
     np_ = (cfg["image_size"] // P) ** 2
     T = np_ + 1
     patch = np_ * H * 3 * P * P
     per_layer = T * (3 * H * H + H * H + 2 * H * F) + 2 * T * T * H
-    return 2.0 * (patch + L * per_layer) / 1e9
+    if not cls_only_last:
+        return 2.0 * (patch + L * per_layer) / 1e9
+    last = T * 3 * H * H + (H * H + 2 * H * F) + 2 * T * H
+    return 2.0 * (patch + (L - 1) * per_layer + last) / 1e9
 
 
 def random_state_dict(seed: int = 0, num_layers: int = 12, cfg: dict = VIT_MSN_BASE) -> dict[str, np.ndarray]:

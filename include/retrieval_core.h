@@ -182,6 +182,15 @@ int rc_preprocess(rc_model *m, const uint8_t *images, int n, int h, int w, float
  * other slices' MFMA main loops.  rc_embed still returns ordered on `stream`. */
 int rc_model_set_parts(rc_model *m, int parts);
 
+/* Last encoder layer on the CLS rows only (default 1).  /embed returns
+ * last_hidden_state[:, 0, :] (embedding/main.py:113-114), and row 0 of the last
+ * layer (modeling_vit_msn.py:254-283) reads only its own query row plus every
+ * token's K/V: with cls_only = 1 the last layer runs LN1 + QKV on all rows, then
+ * CLS-query attention, O-proj, LN2 and the MLP on the CLS rows alone.
+ * cls_only = 0 runs the whole layer (A/B and parity tests).  Env override at
+ * create: RC_EMBED_FULL_LAST=1. */
+int rc_model_set_last_layer(rc_model *m, int cls_only);
+
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM (dominant), 2 = attention,
  * 3 = layernorm, 4 = preprocess; `mask` bit i enables id i (-1 = all, 0 = off). */

@@ -166,3 +166,33 @@ def test_embed_split_streams_bitwise_equal(vitmod, cuda, parts, monkeypatch):
     assert torch.equal(a, b) and torch.equal(an, bn)
     m1.close()
     mp.close()
+
+
+def test_cls_only_last_layer_matches_full_layer(vitmod, weights12, cuda):
+    """The CLS-only last layer (default) agrees with the whole last layer and with the oracle.
+
+    Only attention's summation order differs (attention_cls_kernel vs the MFMA
+    kernel), so the two paths agree far inside the bf16 bar; both stay within
+    BF16_COS_TOL of the fp32 reference.
+    """
+    import torch
+
+    rng = np.random.default_rng(11)
+    imgs = rng.integers(0, 256, (40, 224, 224, 3), dtype=np.uint8)
+    m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=40)
+    m.set_last_layer(False)
+    full, _ = m.embed(torch.from_numpy(imgs))
+    m.set_last_layer(True)
+    cls, cls_n = m.embed(torch.from_numpy(imgs))
+    torch.cuda.synchronize()
+    full, cls = full.cpu().numpy(), cls.cpu().numpy()
+    assert np.isfinite(cls).all()
+    for i in range(40):
+        assert 1.0 - cosine(cls[i], full[i]) <= 1e-4
+    assert np.abs(cls - full).max() <= 2e-2 * np.abs(full).max()
+    pick = [0, 39]
+    ref = embed_cls(np.stack([preprocess(imgs[i]) for i in pick]), weights12)
+    for j, i in enumerate(pick):
+        assert 1.0 - cosine(cls[i], ref[j]) <= BF16_COS_TOL
+        assert 1.0 - cosine(full[i], ref[j]) <= BF16_COS_TOL
+    m.close()

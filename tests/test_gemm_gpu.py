@@ -54,6 +54,14 @@ def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
         assert bool((out[M:].float() == 7.0).all())
 
 
+@pytest.mark.parametrize("variant", [0, 9])
+@pytest.mark.parametrize("M,N,K", [(1, 768, 768), (85, 3072, 768), (86, 768, 3072), (256, 2304, 768), (17, 32, 64)])
+@pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
+def test_skinny_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
+    """M <= 256 (the CLS rows of the last layer): auto picks the skinny kernel (variant 9)."""
+    test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi)
+
+
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_patch_epilogue_scatter(cuda, variant):
     import torch
