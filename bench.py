@@ -169,7 +169,7 @@ def main():
     ap.add_argument("--batch-queries", type=int, default=1024)
     ap.add_argument("--batch-reps", type=int, default=3)
     ap.add_argument("--roofline-steps", type=int, default=5)
-    ap.add_argument("--parts", type=int, default=3, help="concurrent batch slices per GPU (rc_model_set_parts)")
+    ap.add_argument("--parts", type=int, default=2, help="concurrent batch slices per GPU (rc_model_set_parts)")
     ap.add_argument("--full-last-layer", action="store_true",
                     help="run the last encoder layer on every row (default: CLS rows only, rc_model_set_last_layer)")
     ap.add_argument("--ingest-images", type=int, default=16384, help="config 5 sample per GPU (0 = skip)")

@@ -137,7 +137,8 @@ struct rc_model {
     int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
     int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
     SkWorkspace sk;                // Stream-K partials/flags of this model's GEMMs
-    int split = 3;                 // batch parts encoded concurrently (RC_EMBED_SPLIT / rc_model_set_parts)
+    int split = 2;                 // batch parts encoded concurrently (RC_EMBED_SPLIT / rc_model_set_parts);
+                                   // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
     hipStream_t sp[4] = {};        // streams of parts 1..3 (part 0 runs on the caller's stream)
     hipEvent_t ev_fork = nullptr, ev_join[4] = {};
