@@ -260,8 +260,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 
     const int nk = K / BK;
-    stage4(0, 0, 0);
-    stage4(0, 0, 4);
+    // K order: with grouped tiles, the tile one XCD round later (32 tiles on)
+    // reuses this tile's A rows at column tile tn + 4; sweeping K the other way
+    // there starts on the K-slices still in L2 (krev = 4; ascending otherwise)
+    const bool rev = a.krev > 0 && ((tn / a.krev) & 1);
+    auto kofs = [&](int kt) { return (rev ? nk - 1 - kt : kt) * BK; };
+    stage4(0, kofs(0), 0);
+    stage4(0, kofs(0), 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     if (grp == 1) bar();  // stagger: G1 one segment behind
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                     const int c = s * 4 + g;
                     wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                 }
-            if (!(ABL & 1) && more && p < 2) stage4(cur ^ 1, (kt + 1) * BK, p * 4);
+            if (!(ABL & 1) && more && p < 2) stage4(cur ^ 1, kofs(kt + 1), p * 4);
             if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             bar();
@@ -1265,6 +1270,19 @@ inline int gemm_group_m(const GemmArgs &a) {
     return a.N / 256 >= 6 ? 8 : 0;
 }
 
+// Ping-pong K order for grouped tile orders (GemmArgs::krev); RC_GEMM_KREV (read
+// once) sets R, 0 = every tile sweeps K upwards.  Off by default: alternating the
+// sweep did not pay at batch 256 (R = 4: fc1 264 -> 267 us, QKV 171 -> 173 us; R = 2
+// neutral; profiles/gemm/r01k_ab_krev.jsonl), so the A re-reads fc1's PMC traffic
+// shows are not the L2-LRU round-boundary misses this targets.
+inline int gemm_krev() {
+    static const int r = [] {
+        const char *d = std::getenv("RC_GEMM_KREV");
+        return d ? std::atoi(d) : 0;
+    }();
+    return r;
+}
+
 // compute units of the current device (one persistent block per CU)
 inline int gemm_num_cus() {
     static thread_local int dev = -1, cus = 256;
@@ -1355,6 +1373,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
         case GEMM_PINGPONG: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             a.group_m = gm_override >= 0 ? gm_override : gemm_group_m(a);
+            a.krev = a.group_m > 0 ? gemm_krev() : 0;
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(ntm * ntn), dim3(512), 0, s, a);
             break;

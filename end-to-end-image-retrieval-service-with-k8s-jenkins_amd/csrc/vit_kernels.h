@@ -43,6 +43,7 @@ struct GemmArgs {
     uint32_t sk_epoch = 0;           // this launch's flag value (never 0)
     int sk_debug = 0;                // diagnostic bits (gemm_debug_bits), 0 in production
     int group_m = 0;                 // ping-pong tile order: 0 = row-major, G = groups of G row tiles
+    int krev = 0;                    // ping-pong K order: R > 0 = column tiles with (tn / R) odd sweep K downwards
 };
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;
