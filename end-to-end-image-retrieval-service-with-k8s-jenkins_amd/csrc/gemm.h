@@ -1392,6 +1392,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
         }
         case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
         case 100 + 8: case 100 + 16: case 100 + 24: {
+            a.group_m = gm_override >= 0 ? gm_override : gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
             switch (variant - 100) {
