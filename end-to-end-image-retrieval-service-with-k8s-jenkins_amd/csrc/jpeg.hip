@@ -21,6 +21,7 @@
 // HWC u8 RGB straight into the caller's buffer (the input of rc_embed's resize).
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -644,6 +645,20 @@ extern "C" int rc_jpeg_decoder_destroy(rc_jpeg_decoder *h) {
     });
 }
 
+// Host Huffman workers per call: RC_JPEG_THREADS if set, else min(16, cores).  In the
+// pipelined ingest (embed_jpeg_stream) these threads share the host with the thread
+// launching the embed kernels, so fewer than the core count can be faster there.
+static int huffman_threads() {
+    static const int n = [] {
+        if (const char *e = std::getenv("RC_JPEG_THREADS")) {
+            const int v = std::atoi(e);
+            if (v > 0) return std::min(v, 64);
+        }
+        return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    }();
+    return n;
+}
+
 extern "C" int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens,
                               uint8_t *rgb, const int64_t *rgb_offsets, void *stream) {
     return guard([&] {
@@ -674,7 +689,7 @@ extern "C" int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *j
                 errs[i] = e.what();
             }
         };
-        const int nthreads = std::max(1, std::min<int>(n, std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
+        const int nthreads = std::max(1, std::min<int>(n, huffman_threads()));
         if (nthreads == 1) {
             for (int i = 0; i < n; ++i) work(i);
         } else {

@@ -104,5 +104,22 @@ class JpegDecoder:
                 outs.append(buf[o:o + z].view(inf.height, inf.width, 3))
         return outs
 
+    def decode_batch(self, datas: Sequence[bytes], stream=None) -> torch.Tensor:
+        """Equal-size JPEGs -> one device u8 [n, H, W, 3] tensor.  Within one chunk the
+        images are packed back to back, so the batch is a view of the decode buffer
+        (no stack copy); mixed sizes raise ValueError."""
+        imgs = self.decode(datas, stream=stream)
+        if not imgs:
+            raise ValueError("empty batch")
+        shape = imgs[0].shape
+        if any(im.shape != shape for im in imgs):
+            raise ValueError("decode_batch needs equal-size images")
+        first = imgs[0]
+        packed = (len(imgs) <= self.max_images
+                  and all(im.data_ptr() == first.data_ptr() + i * first.numel() for i, im in enumerate(imgs)))
+        if packed:
+            return first.as_strided((len(imgs),) + tuple(shape), (first.numel(),) + tuple(first.stride()))
+        return torch.stack(imgs)
+
 
 __all__ = ["JpegDecoder", "JpegUnsupported", "probe", "is_gpu_decodable", "decode_coefficients", "RetrievalCoreError"]

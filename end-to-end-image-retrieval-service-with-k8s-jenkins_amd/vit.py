@@ -212,8 +212,7 @@ class VitMsnEmbedder:
 
         def decode(datas):
             with torch.cuda.device(self.device), torch.cuda.stream(side):
-                imgs = dec.decode(datas, stream=side)
-                x = torch.stack(imgs)
+                x = dec.decode_batch(datas, stream=side)
                 ev = torch.cuda.Event()
                 ev.record(side)
             return x, ev

@@ -87,3 +87,17 @@ def test_embed_jpeg_stream_matches_unpipelined(cuda):
         ref, _ = m.embed(torch.from_numpy(np.stack([pil_rgb(d) for d in datas])))
         assert torch.equal(got[b], ref)
     m.close()
+
+
+def test_decode_batch_is_a_packed_view(dec):
+    """decode_batch: one chunk of equal-size images is a view of the decode buffer (no stack
+    copy) and bit-exact with PIL; a batch spanning chunks or mixed sizes is handled loudly."""
+    datas = [synthetic(64, 48, 500 + i, quality=90, subsampling=2) for i in range(6)]
+    x = dec.decode_batch(datas)
+    assert tuple(x.shape) == (6, 48, 64, 3) and x.is_contiguous()
+    assert np.array_equal(x.cpu().numpy(), np.stack([pil_rgb(d) for d in datas]))
+    many = [datas[i % 6] for i in range(dec.max_images + 3)]  # two chunks -> stacked copy
+    y = dec.decode_batch(many)
+    assert np.array_equal(y[dec.max_images + 1].cpu().numpy(), pil_rgb(datas[(dec.max_images + 1) % 6]))
+    with pytest.raises(ValueError):
+        dec.decode_batch([datas[0], synthetic(32, 32, 1)])
