@@ -534,10 +534,11 @@ __device__ __forceinline__ int upsampled(const uint8_t *__restrict__ planes, con
 __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t *__restrict__ planes, const Desc *__restrict__ descs,
                                                         uint8_t *__restrict__ rgb) {
     const Desc d = descs[blockIdx.y];
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= (int64_t)d.W * d.H) return;
-    const int y = (int)(p / d.W), x = (int)(p - (int64_t)y * d.W);
-    uint8_t *o = rgb + d.rgb_off + p * 3;
+    // W*H < 2^31 (checked at decode): 32-bit index math, no emulated 64-bit divide
+    const int p = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (p >= d.W * d.H) return;
+    const int y = p / d.W, x = p - y * d.W;
+    uint8_t *o = rgb + d.rgb_off + (int64_t)p * 3;
     const int Y = upsampled(planes, d, 0, x, y);
     if (d.ncomp == 1) {
         o[0] = o[1] = o[2] = (uint8_t)Y;
