@@ -101,6 +101,16 @@ SIGNATURES = {
     "rc_index_gemm_timing_read": (C.c_int, [_vp, _pd, _pi64, _pd, _pi64]),
     "rc_index_fill_random": (C.c_int, [_vp, C.c_uint64, _i64, _i64, _vp]),
     "rc_topk_merge": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "rc_index_set_row_map": (C.c_int, [_vp, _i64, _i64]),
+    "rc_index_grow": (C.c_int, [_vp, _i64, _vp]),
+    "rc_sharded_create": (C.c_int, [_i32, _pi32, _i32, _i32, _i64, C.POINTER(_vp)]),
+    "rc_sharded_destroy": (C.c_int, [_vp]),
+    "rc_sharded_info": (C.c_int, [_vp, _pi32, _pi64, _pi64]),
+    "rc_sharded_shard": (C.c_int, [_vp, _i32, C.POINTER(_vp)]),
+    "rc_sharded_grow": (C.c_int, [_vp, _i64]),
+    "rc_sharded_upsert": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
+    "rc_sharded_fetch": (C.c_int, [_vp, _vp, _i64, _vp, _i32]),
+    "rc_sharded_search": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _i32, _vp]),
     "rc_index_timing": (C.c_int, [_vp, _i32]),
     "rc_index_timing_read": (C.c_int, [_vp, _pd, _pi64, _pd]),
     "rc_model_create": (C.c_int, [_i32, C.POINTER(VitConfig), C.POINTER(_vp)]),

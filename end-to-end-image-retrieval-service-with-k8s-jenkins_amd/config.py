@@ -24,11 +24,17 @@ class Config:
     EMBEDDING_SERVICE_URL = os.getenv("EMBEDDING_SERVICE_URL", "http://localhost:5000/embed")
     # build-side knobs
     INDEX_DTYPE = os.getenv("RC_INDEX_DTYPE", "float32")
-    INDEX_CAPACITY = int(os.getenv("RC_INDEX_CAPACITY", str(1 << 20)))
+    INDEX_CAPACITY = int(os.getenv("RC_INDEX_CAPACITY", str(1 << 20)))  # initial rows; grows on demand
+    # index shards: RC_INDEX_DEVICES = "all" (one shard per visible GPU) or a comma list
+    # of device ordinals ("0,1,2,3"); otherwise RC_INDEX_SHARDS shards on the current GPU
+    INDEX_DEVICES = os.getenv("RC_INDEX_DEVICES", "")
+    INDEX_SHARDS = int(os.getenv("RC_INDEX_SHARDS", "1"))
     EMBED_MAX_BATCH = int(os.getenv("RC_EMBED_MAX_BATCH", "32"))
     MODEL_PATH = os.getenv("RC_MODEL_PATH", "")  # local checkpoint dir (config.json + weights)
     WEIGHT_SEED = int(os.getenv("RC_WEIGHT_SEED", "1907"))
     GPU_JPEG = os.getenv("RC_GPU_JPEG", "1") != "0"  # decode baseline JPEGs on the GPU (bit-exact with PIL)
+    # ingest / retrieve services: embed in process on the GPU (1) or POST to EMBEDDING_SERVICE_URL (0)
+    EMBED_IN_PROCESS = os.getenv("RC_EMBED_IN_PROCESS", "1") != "0"
 
 
 # facebook/vit-msn-base preprocessing (ViTImageProcessor). The checkpoint's

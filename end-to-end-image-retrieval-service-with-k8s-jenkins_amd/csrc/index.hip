@@ -24,14 +24,15 @@ void set_last_error(const std::string &m) { g_last_error = m; }
 
 // ------------------------------------------------------- upsert / fetch --
 // One wave per vector: norm in f32, normalise, cast, scatter to its row slot.
+// src (optional): vector v is read from vecs[src[v]] (a shard's subset of a batch).
 template <typename T>
 __global__ __launch_bounds__(256) void upsert_kernel(T *__restrict__ rows, float *__restrict__ norms, int64_t ld, int dim,
-                                                    const float *__restrict__ vecs, const int64_t *__restrict__ slot,
-                                                    int64_t n) {
+                                                    const float *__restrict__ vecs, const int64_t *__restrict__ src_idx,
+                                                    const int64_t *__restrict__ slot, int64_t n) {
     const int lane = threadIdx.x & 63;
     const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (v >= n) return;
-    const float *src = vecs + v * dim;
+    const float *src = vecs + (src_idx ? src_idx[v] : v) * dim;
     float ss = 0.f;
     for (int c = lane; c < dim; c += 64) ss = fmaf(src[c], src[c], ss);
     ss = wave_sum(ss);
@@ -103,14 +104,18 @@ __global__ __launch_bounds__(64) void normalize_queries_kernel(const float *__re
 }
 
 // One block per query: top-k over nlist sorted partial lists of k keys each.
+// flags (optional): only queries with flags[q] != 0 are merged (the batched
+// search's exact fallback).  Returned row = row_base + local row * row_stride.
 template <int CAP>
 __global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__restrict__ partial, int nlist,
-                                                            int nq_total, int k, int64_t row_base,
+                                                            int nq_total, int k, int64_t row_base, int64_t row_stride,
+                                                            const int *__restrict__ flags,
                                                             float *__restrict__ out_scores,
                                                             int64_t *__restrict__ out_rows) {
     __shared__ uint64_t lds[4][CAP];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int qi = blockIdx.x;
+    if (flags != nullptr && flags[qi] == 0) return;  // block-uniform
     WaveTopK<CAP> tk;
     tk.init(as_lds(&lds[wave][0]), k);
     const int64_t total = (int64_t)nlist * k;
@@ -148,15 +153,15 @@ __global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__r
             const uint64_t key = tk.buf[j];
             const bool ok = key != KEY_EMPTY;
             out_scores[(int64_t)qi * k + j] = ok ? key_score(key) : -INFINITY;
-            out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) : -1;
+            out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) * row_stride : -1;
         }
     }
 }
 
-// Cross-shard merge: nlists lists of (score, row) per query, each sorted
-// (score desc, row asc), lists in ascending row-range order.  The key's low
-// word is the candidate's position l*k_in + t, which orders equal scores
-// exactly as the global row does.
+// Cross-shard merge: nlists lists of (score, global row) per query.  The key's
+// low word is the global row itself (< 2^32), so equal scores order by row
+// whatever the row → shard routing (contiguous ranges or round-robin).  Rows
+// < 0 are empty slots.
 template <int CAP>
 __global__ __launch_bounds__(256) void merge_lists_kernel(const float *__restrict__ scores,
                                                          const int64_t *__restrict__ rows, int nlists, int nq,
@@ -175,8 +180,9 @@ __global__ __launch_bounds__(256) void merge_lists_kernel(const float *__restric
         if (j < total) {
             const int64_t l = j / k_in, t = j - l * k_in;
             const int64_t src = (l * nq + qi) * k_in + t;
-            ok = rows[src] >= 0;
-            key = make_key(scores[src], (uint32_t)j);
+            const int64_t row = rows[src];
+            ok = row >= 0;
+            key = make_key(scores[src], (uint32_t)row);
         }
         tk.reserve(64);
         tk.push(ok, key);
@@ -194,15 +200,18 @@ __global__ __launch_bounds__(256) void merge_lists_kernel(const float *__restric
         for (int j = lane; j < k; j += 64) {
             const uint64_t key = tk.buf[j];
             const bool ok = key != KEY_EMPTY;
-            int64_t src = 0;
-            if (ok) {
-                const int64_t p = key_idx(key), l = p / k_in, t = p - l * k_in;
-                src = (l * nq + qi) * k_in + t;
-            }
-            out_scores[(int64_t)qi * k + j] = ok ? scores[src] : -INFINITY;
-            out_rows[(int64_t)qi * k + j] = ok ? rows[src] : -1;
+            out_scores[(int64_t)qi * k + j] = ok ? key_score(key) : -INFINITY;
+            out_rows[(int64_t)qi * k + j] = ok ? (int64_t)key_idx(key) : -1;
         }
     }
+}
+
+// Search over zero rows (an empty shard): every slot is (-inf, -1).
+__global__ __launch_bounds__(256) void empty_result_kernel(int64_t n, float *__restrict__ scores, int64_t *__restrict__ rows) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    scores[i] = -INFINITY;
+    rows[i] = -1;
 }
 
 }  // namespace rc
@@ -218,7 +227,8 @@ struct rc_index {
     int nch = 1;  // ld = 128 * nch
     int64_t ld = 0;
     int64_t capacity = 0;
-    int64_t row_base = 0;
+    int64_t row_base = 0;    // a search returns row_base + local row * row_stride (shard → global rows)
+    int64_t row_stride = 1;
     void *rows = nullptr;
     float *norms = nullptr;
     // search workspace
@@ -228,7 +238,6 @@ struct rc_index {
     BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
     KernelTimer timer;   // scan_topk_kernel launches (bytes)
     KernelTimer gtimer;  // filter_gemm_kernel launches (flops)
-    int64_t fallbacks = 0;  // batched searches that needed the exact-scan fallback
 };
 
 namespace {
@@ -259,9 +268,10 @@ void ensure_workspace(rc_index *h, int nq, int k) {
 }
 
 template <typename T>
-void launch_upsert(rc_index *h, const float *vecs, int64_t n, const int64_t *slots, hipStream_t s) {
+void launch_upsert(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *slots, hipStream_t s) {
     const unsigned grid = (unsigned)((n + 3) / 4);
-    hipLaunchKernelGGL(upsert_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, vecs, slots, n);
+    hipLaunchKernelGGL(upsert_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, vecs, src_idx,
+                       slots, n);
     RC_LAUNCH_CHECK();
 }
 
@@ -292,16 +302,19 @@ void launch_scan(rc_index *h, const ScanArgs &a) {
 }
 
 template <int CAP>
-void launch_merge_partials_t(rc_index *h, int nlist, int nq, int nq_stride, int k, float *scores, int64_t *rows, hipStream_t s) {
-    hipLaunchKernelGGL(merge_partials_kernel<CAP>, dim3(nq), dim3(256), 0, s, h->partial, nlist, nq_stride, k, h->row_base, scores, rows);
+void launch_merge_partials_t(rc_index *h, const uint64_t *partial, const int *flags, int nlist, int nq, int nq_stride, int k,
+                             float *scores, int64_t *rows, hipStream_t s) {
+    hipLaunchKernelGGL(merge_partials_kernel<CAP>, dim3(nq), dim3(256), 0, s, partial, nlist, nq_stride, k, h->row_base,
+                       h->row_stride, flags, scores, rows);
     RC_LAUNCH_CHECK();
 }
 
-void launch_merge_partials(rc_index *h, int nlist, int nq, int nq_stride, int k, float *scores, int64_t *rows, hipStream_t s) {
+void launch_merge_partials(rc_index *h, const uint64_t *partial, const int *flags, int nlist, int nq, int nq_stride, int k,
+                           float *scores, int64_t *rows, hipStream_t s) {
     const int cap = topk_cap(k);
-    if (cap <= 128) return launch_merge_partials_t<128>(h, nlist, nq, nq_stride, k, scores, rows, s);
-    if (cap <= 256) return launch_merge_partials_t<256>(h, nlist, nq, nq_stride, k, scores, rows, s);
-    return launch_merge_partials_t<512>(h, nlist, nq, nq_stride, k, scores, rows, s);
+    if (cap <= 128) return launch_merge_partials_t<128>(h, partial, flags, nlist, nq, nq_stride, k, scores, rows, s);
+    if (cap <= 256) return launch_merge_partials_t<256>(h, partial, flags, nlist, nq, nq_stride, k, scores, rows, s);
+    return launch_merge_partials_t<512>(h, partial, flags, nlist, nq, nq_stride, k, scores, rows, s);
 }
 
 template <typename F>
@@ -337,28 +350,51 @@ void scan_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int 
         launch_scan(h, a);
         h->timer.end(slot, s, bytes);
     }
-    launch_merge_partials(h, nblk, nq, nq_pad, k, scores, out_rows, s);
+    launch_merge_partials(h, h->partial, nullptr, nblk, nq, nq_pad, k, scores, out_rows, s);
 }
 
-// Batched MFMA search, then the exact scan for any query whose candidates
-// overflowed (one host sync per call: the flags decide what to re-run).
+// Batched MFMA search, then — still on the device, no host synchronisation —
+// the exact scan for every query whose candidates overflowed: scan_topk_kernel
+// in fallback mode (blocks early-exit for unflagged queries) over the batched
+// path's normalised queries (the same f32 arithmetic as normalize_queries_kernel),
+// and merge_partials_kernel over the flagged queries' partial lists.
 void batched_search_exact(rc_index *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
                           int64_t *out_rows, hipStream_t s) {
     h->bws.ensure(nq, k, h->ld, (int)dtype_size(h->dtype));
-    BatchPlan p{h->rows, h->dtype, h->dim, h->nch, h->ld, n_rows, h->row_base, queries, nq, k, scores, out_rows};
+    BatchPlan p{h->rows, h->dtype, h->dim, h->nch, h->ld, n_rows, h->row_base, h->row_stride, queries, nq, k, scores, out_rows};
     if (h->gtimer.enabled) h->gtimer.create();
     batched_search(p, h->bws, s, h->gtimer.enabled ? &h->gtimer : nullptr);
-    RC_HIP(hipMemcpyAsync(h->bws.ovf_host, h->bws.ovf, sizeof(int), hipMemcpyDeviceToHost, s));
-    RC_HIP(hipStreamSynchronize(s));
-    if (*h->bws.ovf_host == 0) return;
-    std::vector<int> flags(nq);
-    RC_HIP(hipMemcpyAsync(flags.data(), h->bws.flags, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, s));
-    RC_HIP(hipStreamSynchronize(s));
-    for (int q = 0; q < nq; ++q)
-        if (flags[q]) scan_search(h, queries + (int64_t)q * h->dim, 1, n_rows, k, scores + (int64_t)q * k,
-                                  out_rows + (int64_t)q * k, s);
-    h->fallbacks += 1;
+    int nblk = (int)std::min<int64_t>(FB_BLOCKS, std::max<int64_t>(1, (n_rows + 511) / 512));
+    int64_t rpb = (n_rows + nblk - 1) / nblk;
+    rpb = std::max<int64_t>(32, (rpb + 31) / 32 * 32);
+    nblk = (int)std::max<int64_t>(1, (n_rows + rpb - 1) / rpb);
+    ScanArgs a{h->rows, h->ld, h->nch, n_rows, rpb, nblk, h->bws.qn, 0, 1, nq, k, h->bws.fb_partial, s};
+    a.flags = h->bws.flags;
+    a.grid_y = std::min(nq, FB_QSTRIDE);
+    launch_scan(h, a);
+    launch_merge_partials(h, h->bws.fb_partial, h->bws.flags, nblk, nq, nq, k, scores, out_rows, s);
 }
+
+void empty_search(int nq, int k, float *scores, int64_t *out_rows, hipStream_t s) {
+    const int64_t n = (int64_t)nq * k;
+    hipLaunchKernelGGL(empty_result_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, scores, out_rows);
+    RC_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+namespace rc {
+// Internal (sharded.hip): upsert vectors vecs[src_idx[i]] into local rows rows[i].
+void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *rows,
+                         hipStream_t s) {
+    if (n == 0) return;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceScope ds(h->device);
+    dispatch_dtype(h->dtype, [&](auto t) { launch_upsert<decltype(t)>(h, vecs, src_idx, n, rows, s); });
+}
+}  // namespace rc
+
+namespace {
 
 }  // namespace
 
@@ -437,6 +473,50 @@ int rc_index_data(const rc_index *h, void **rows_dev, float **norms_dev) {
     });
 }
 
+int rc_index_set_row_map(rc_index *h, int64_t row_base, int64_t row_stride) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(row_base >= 0 && row_stride >= 1, RC_ERR_INVALID, "row_base must be >= 0 and row_stride >= 1");
+        std::lock_guard<std::mutex> lk(h->mu);
+        h->row_base = row_base;
+        h->row_stride = row_stride;
+    });
+}
+
+int rc_index_grow(rc_index *h, int64_t new_capacity, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(new_capacity < (int64_t(1) << 32), RC_ERR_INVALID, "capacity must be < 2^32");
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (new_capacity <= h->capacity) return;
+        DeviceScope ds(h->device);
+        hipStream_t s = (hipStream_t)stream;
+        const size_t rb = (size_t)h->ld * dtype_size(h->dtype);
+        const int64_t old_pad = (h->capacity + INDEX_ROW_PAD - 1) / INDEX_ROW_PAD * INDEX_ROW_PAD;
+        const int64_t new_pad = (new_capacity + INDEX_ROW_PAD - 1) / INDEX_ROW_PAD * INDEX_ROW_PAD;
+        void *rows = dmalloc((size_t)new_pad * rb);
+        float *norms = nullptr;
+        try {
+            norms = (float *)dmalloc((size_t)new_capacity * sizeof(float));
+            RC_HIP(hipMemcpyAsync(rows, h->rows, (size_t)old_pad * rb, hipMemcpyDeviceToDevice, s));
+            RC_HIP(hipMemsetAsync((uint8_t *)rows + (size_t)old_pad * rb, 0, (size_t)(new_pad - old_pad) * rb, s));
+            RC_HIP(hipMemcpyAsync(norms, h->norms, (size_t)h->capacity * sizeof(float), hipMemcpyDeviceToDevice, s));
+            RC_HIP(hipMemsetAsync(norms + h->capacity, 0, (size_t)(new_capacity - h->capacity) * sizeof(float), s));
+            RC_HIP(hipStreamSynchronize(s));  // work queued earlier on other streams is the caller's to order
+        } catch (...) {
+            dfree(rows);
+            dfree(norms);
+            throw;
+        }
+        RC_HIP(hipDeviceSynchronize());  // no kernel may still read the old buffers
+        dfree(h->rows);
+        dfree(h->norms);
+        h->rows = rows;
+        h->norms = norms;
+        h->capacity = new_capacity;
+    });
+}
+
 int rc_index_reserve(rc_index *h, int max_nq, int max_k) {
     return guard([&] {
         RC_REQUIRE(h, RC_ERR_INVALID, "null index");
@@ -455,7 +535,7 @@ int rc_index_upsert(rc_index *h, const float *vecs, int64_t n, const int64_t *ro
         RC_REQUIRE(vecs && rows, RC_ERR_INVALID, "null buffer");
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceScope ds(h->device);
-        dispatch_dtype(h->dtype, [&](auto t) { launch_upsert<decltype(t)>(h, vecs, n, rows, (hipStream_t)stream); });
+        dispatch_dtype(h->dtype, [&](auto t) { launch_upsert<decltype(t)>(h, vecs, nullptr, n, rows, (hipStream_t)stream); });
     });
 }
 
@@ -542,9 +622,12 @@ int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceScope ds(h->device);
         hipStream_t s = (hipStream_t)stream;
-        const bool mfma_ok = h->dtype != RC_F32 && n_rows > 0;
-        RC_REQUIRE(mode != RC_SEARCH_MFMA || mfma_ok, RC_ERR_UNSUPPORTED,
-                   "batched MFMA search needs an f16/bf16 index with at least one row");
+        if (n_rows == 0) {  // an empty shard answers (-inf, -1) in every mode
+            empty_search(nq, k, scores, out_rows, s);
+            return;
+        }
+        const bool mfma_ok = h->dtype != RC_F32;
+        RC_REQUIRE(mode != RC_SEARCH_MFMA || mfma_ok, RC_ERR_UNSUPPORTED, "batched MFMA search needs an f16/bf16 index");
         const bool use_mfma = mode == RC_SEARCH_MFMA ||
                               (mode == RC_SEARCH_AUTO && mfma_ok && nq >= kBatchMinQueries && n_rows >= kBatchMinRows);
         if (!use_mfma) {
@@ -559,7 +642,6 @@ int rc_topk_merge(const float *scores, const int64_t *rows, int nlists, int nq, 
                   int64_t *out_rows, void *stream) {
     return guard([&] {
         RC_REQUIRE(nlists >= 1 && nq >= 0 && k_in >= 1 && k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "bad merge sizes");
-        RC_REQUIRE((int64_t)nlists * k_in < (int64_t(1) << 32), RC_ERR_INVALID, "too many candidates");
         if (nq == 0) return;
         hipStream_t s = (hipStream_t)stream;
         const int cap = topk_cap(k);
@@ -611,7 +693,15 @@ int rc_index_gemm_timing_read(rc_index *h, double *total_ms, int64_t *launches, 
         if (total_ms) *total_ms = h->gtimer.total_ms;
         if (launches) *launches = h->gtimer.launches;
         if (flops) *flops = h->gtimer.work;
-        if (fallbacks) *fallbacks = h->fallbacks;
+        if (fallbacks) {
+            int ovf = 0;
+            if (h->bws.ovf) {
+                RC_HIP(hipDeviceSynchronize());
+                RC_HIP(hipMemcpy(&ovf, h->bws.ovf, sizeof(int), hipMemcpyDeviceToHost));
+                RC_HIP(hipMemset(h->bws.ovf, 0, sizeof(int)));
+            }
+            *fallbacks = ovf;
+        }
         h->gtimer.total_ms = 0;
         h->gtimer.launches = 0;
         h->gtimer.work = 0;

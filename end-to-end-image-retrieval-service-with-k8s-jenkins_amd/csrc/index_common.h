@@ -77,6 +77,11 @@ struct ScanArgs {
     int k;
     uint64_t *partial;
     hipStream_t stream;
+    // Exact fallback of the batched search: when set, grid.y strides over the
+    // queries [0, nq_total) and only queries with flags[q] != 0 are scanned
+    // (qb = 1; q0 unused); partial is then [nblk][nq_total][k].
+    const int *flags = nullptr;
+    int grid_y = 1;
 };
 
 // largest queries-per-pass for a row width: query registers per lane = QB*nch*8 floats <= 64
@@ -92,6 +97,8 @@ void launch_scan_bf16(const ScanArgs &a);
 // ------------------------------------------- batched MFMA search (search_mfma.hip)
 constexpr int BATCH_CAND_CAP = 4096;  // candidate slots per query per stage
 constexpr int INDEX_ROW_PAD = 256;    // row storage is allocated in whole 256-row tiles
+constexpr int FB_BLOCKS = 256;        // blocks of the on-device exact fallback scan (overflowed queries)
+constexpr int FB_QSTRIDE = 64;        // its grid.y: block (b, y) scans queries y, y + 64, ... that overflowed
 
 struct BatchWs {
     int nq_cap = 0, k_cap = 0;
@@ -105,8 +112,8 @@ struct BatchWs {
     uint32_t *cand = nullptr;   // [nq_cap][cap] candidate rows
     uint64_t *keys = nullptr;   // [nq_cap][k_cap] running top-k keys (sorted)
     int *flags = nullptr;       // [nq_cap] 1 = candidate overflow, exact fallback needed
-    int *ovf = nullptr;         // number of overflowed queries (device)
-    int *ovf_host = nullptr;    // pinned copy
+    int *ovf = nullptr;         // overflowed queries since the last timing read (device counter)
+    uint64_t *fb_partial = nullptr;  // [FB_BLOCKS][nq_cap][k_cap] partial keys of the exact fallback scan
     void ensure(int nq, int k, int64_t ld, int dtype_bytes);
     void release();
 };
@@ -118,7 +125,8 @@ struct BatchPlan {
     int nch;
     int64_t ld;
     int64_t n_rows;
-    int64_t row_base;
+    int64_t row_base;      // returned row = row_base + local row * row_stride
+    int64_t row_stride;
     const float *queries;  // device f32 [nq][dim]
     int nq;
     int k;
@@ -138,10 +146,11 @@ int batch_stage_ratio(int k, int cap);
 // [j*EPC, (j+1)*EPC).  SCAN_U row-groups are loaded before any is consumed.
 constexpr int SCAN_U = 2;
 
+// One block's pass over its row range for queries [q0, q0 + QB): partial top-k keys.
 template <typename T, int NCH, int QB, int CAP>
-__global__ __launch_bounds__(256) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
-                                                       int64_t rows_per_block, const float *__restrict__ qn, int q0,
-                                                       int nq_total, int k, uint64_t *__restrict__ partial) {
+__device__ __forceinline__ void scan_rows(const T *__restrict__ rows, int64_t ld, int64_t n_rows, int64_t rows_per_block,
+                                          const float *__restrict__ qn, int q0, int nq_total, int k,
+                                          uint64_t *__restrict__ partial) {
     constexpr int EPC = 16 / sizeof(T);
     constexpr int CPL = NCH * 128 / (16 * EPC);
     __shared__ uint64_t lds[4][QB][CAP];
@@ -222,9 +231,25 @@ __global__ __launch_bounds__(256) void scan_topk_kernel(const T *__restrict__ ro
 }
 
 template <typename T, int NCH, int QB, int CAP>
+__global__ __launch_bounds__(256) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
+                                                       int64_t rows_per_block, const float *__restrict__ qn, int q0,
+                                                       int nq_total, int k, uint64_t *__restrict__ partial,
+                                                       const int *__restrict__ flags) {
+    if (flags != nullptr) {  // exact fallback: the overflowed queries only (block-uniform branches)
+        for (int qf = blockIdx.y; qf < nq_total; qf += gridDim.y)
+            if (flags[qf]) {
+                scan_rows<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, qn, qf, nq_total, k, partial);
+                __syncthreads();  // the next query reuses the LDS lists
+            }
+        return;
+    }
+    scan_rows<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, qn, q0, nq_total, k, partial);
+}
+
+template <typename T, int NCH, int QB, int CAP>
 void launch_scan_t(const ScanArgs &a) {
-    hipLaunchKernelGGL((scan_topk_kernel<T, NCH, QB, CAP>), dim3(a.nblk), dim3(256), 0, a.stream, (const T *)a.rows, a.ld,
-                       a.n_rows, a.rows_per_block, a.qn, a.q0, a.nq_total, a.k, a.partial);
+    hipLaunchKernelGGL((scan_topk_kernel<T, NCH, QB, CAP>), dim3(a.nblk, a.grid_y), dim3(256), 0, a.stream, (const T *)a.rows,
+                       a.ld, a.n_rows, a.rows_per_block, a.qn, a.q0, a.nq_total, a.k, a.partial, a.flags);
     RC_LAUNCH_CHECK();
 }
 

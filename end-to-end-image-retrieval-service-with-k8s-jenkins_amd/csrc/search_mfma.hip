@@ -23,7 +23,8 @@
 // filter never drops a true member.  The stage ratio g keeps the expected
 // candidates per stage at ≈ k·(g-1) ≪ CAND_CAP.  A query whose candidates
 // overflow CAND_CAP in some stage (adversarial / duplicate-heavy data) is
-// flagged and re-run by the host through the exact scan (index.hip).
+// flagged and re-run on the device through the exact scan (index.hip,
+// scan_topk_kernel's fallback mode): no host synchronisation.
 //
 // HBM layout: rows [cap256][ld] T (capacity rounded up to 256 rows so whole
 // row tiles are readable), queries q̂ [nqb*256][ld] T (zero rows past nq).
@@ -456,7 +457,8 @@ __global__ __launch_bounds__(256) void rescore_kernel(const T *__restrict__ rows
                                                      int cap, uint64_t *__restrict__ keys, const float *__restrict__ eps,
                                                      float *__restrict__ thr, int *__restrict__ flags,
                                                      int *__restrict__ ovf_total, int final_pass, int64_t row_base,
-                                                     float *__restrict__ out_scores, int64_t *__restrict__ out_rows) {
+                                                     int64_t row_stride, float *__restrict__ out_scores,
+                                                     int64_t *__restrict__ out_rows) {
     constexpr int EPC = 16 / sizeof(T);
     constexpr int CPL = NCH * 128 / (16 * EPC);
     constexpr int U = 2;
@@ -528,12 +530,12 @@ __global__ __launch_bounds__(256) void rescore_kernel(const T *__restrict__ rows
             if (final_pass) {
                 const bool ok = key != KEY_EMPTY;
                 out_scores[(int64_t)qi * k + j] = ok ? key_score(key) : -INFINITY;
-                out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) : -1;
+                out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) * row_stride : -1;
             }
         }
         if (lane == 0) {
             thr[qi] = tk.count >= k ? key_score(tk.buf[k - 1]) - eps[qi] : -INFINITY;
-            if (n > (uint32_t)cap) {
+            if (n > (uint32_t)cap && flags[qi] == 0) {
                 flags[qi] = 1;
                 atomicAdd(ovf_total, 1);
             }
@@ -549,7 +551,7 @@ void launch_rescore_cap(const BatchPlan &p, const BatchWs &ws, int final_pass, h
 #define RC_RESCORE(CAPV)                                                                                         \
     hipLaunchKernelGGL((rescore_kernel<T, NCH, CAPV>), dim3(p.nq), dim3(256), 0, s, (const T *)p.rows, p.ld, ws.qn, \
                        p.k, ws.cnt, ws.cand, ws.cap, ws.keys, ws.eps, ws.thr, ws.flags, ws.ovf, final_pass, p.row_base,  \
-                       p.out_scores, p.out_rows)
+                       p.row_stride, p.out_scores, p.out_rows)
     if (cap <= 128) RC_RESCORE(128);
     else if (cap <= 256) RC_RESCORE(256);
     else RC_RESCORE(512);
@@ -597,7 +599,6 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
     RC_HIP(hipMemsetAsync(ws.keys, 0xFF, (size_t)p.nq * p.k * sizeof(uint64_t), s));
     RC_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)nq_pad * sizeof(uint32_t), s));
     RC_HIP(hipMemsetAsync(ws.flags, 0, (size_t)p.nq * sizeof(int), s));
-    RC_HIP(hipMemsetAsync(ws.ovf, 0, sizeof(int), s));
 
     const int g = batch_stage_ratio(p.k, ws.cap);
     int64_t b0 = 0, b1 = std::min<int64_t>(p.n_rows, ws.cap);  // stage 1: every row is a candidate
@@ -658,7 +659,8 @@ void BatchWs::ensure(int nq, int k, int64_t ld, int dtype_bytes) {
     keys = (uint64_t *)dmalloc((size_t)nq_cap * k_cap * sizeof(uint64_t));
     flags = (int *)dmalloc((size_t)nq_cap * sizeof(int));
     ovf = (int *)dmalloc(sizeof(int));
-    RC_HIP(hipHostMalloc((void **)&ovf_host, sizeof(int), hipHostMallocDefault));
+    RC_HIP(hipMemset(ovf, 0, sizeof(int)));
+    fb_partial = (uint64_t *)dmalloc((size_t)FB_BLOCKS * nq_cap * k_cap * sizeof(uint64_t));
 }
 
 void BatchWs::release() {
@@ -671,13 +673,14 @@ void BatchWs::release() {
     dfree(keys);
     dfree(flags);
     dfree(ovf);
-    if (ovf_host) (void)hipHostFree(ovf_host);
+    dfree(fb_partial);
     qn = nullptr;
     qh = nullptr;
     eps = thr = nullptr;
     cnt = cand = nullptr;
     keys = nullptr;
-    flags = ovf = ovf_host = nullptr;
+    flags = ovf = nullptr;
+    fb_partial = nullptr;
     nq_cap = k_cap = 0;
     ld_cap = 0;
 }

@@ -1,0 +1,351 @@
+// sharded.hip — one exact cosine index spread over several shards in ONE process
+// (rc_index_create(dim, dtype, capacity_per_gpu, n_gpus); §8(e)).
+//
+// The Pinecone index the reference opens in get_index (ingesting/utils.py:23-38)
+// is one logical index whatever its size; here it is n shards, each an rc_index
+// on its own GPU (or several on one GPU).  Routing is round-robin on the
+// host-assigned global row g: shard g % n holds it as local row g / n, so rows
+// fill every shard evenly from the first upsert on.  A shard returns global rows
+// directly (rc_index row map: row_base = s, row_stride = n).
+//
+// query (retriever/utils.py:62-64): the leader stream's query batch is handed to
+// every shard's stream (event wait; a peer copy over xGMI when the shard lives
+// on another GPU), each shard runs its own scan / MFMA search over its n_local
+// rows, its top-k lists land in a leader-side gather buffer (peer copies of
+// nq*k*12 B), and merge_lists_kernel (rc_topk_merge) keys candidates by
+// (score desc, global row asc) — the same order a single rc_index gives.
+// A multi-PROCESS deployment (one process per GPU) uses the same shard row map
+// with an RCCL all-gather instead (sharded.py).
+#include <algorithm>
+#include <vector>
+
+#include "index_common.h"
+
+namespace rc {
+void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *rows,
+                         hipStream_t s);
+}
+
+using namespace rc;
+
+struct rc_sharded {
+    std::mutex mu;
+    int n = 0, dim = 0, dtype = 0;
+    int64_t cap = 0;  // rows per shard
+    std::vector<int> dev;
+    std::vector<rc_index *> shard;
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev_done;   // per shard, recorded on st[s]
+    std::vector<hipEvent_t> ev_start;  // per shard, recorded on the caller's (leader) stream
+    // search buffers
+    int nq_cap = 0, k_cap = 0;
+    std::vector<float *> q;       // [nq_cap][dim] query copy on a non-leader shard's device
+    std::vector<float *> s_loc;   // [nq_cap][k_cap] a non-leader shard's own result
+    std::vector<int64_t *> r_loc;
+    float *g_s = nullptr;         // leader [n][nq_cap][k_cap] gathered lists
+    int64_t *g_r = nullptr;
+    // upsert / fetch staging
+    int64_t st_cap = 0;
+    std::vector<int64_t *> idx_d;  // [st_cap] source index per shard
+    std::vector<int64_t *> row_d;  // [st_cap] local row per shard
+    std::vector<float *> vec_d;    // [st_cap][dim] vectors on a non-leader shard's device
+};
+
+namespace {
+
+void free_search(rc_sharded *h) {
+    for (int s = 0; s < h->n; ++s) {
+        DeviceScope ds(h->dev[s]);
+        dfree(h->q[s]);
+        dfree(h->s_loc[s]);
+        dfree(h->r_loc[s]);
+        h->q[s] = nullptr;
+        h->s_loc[s] = nullptr;
+        h->r_loc[s] = nullptr;
+    }
+    DeviceScope ds(h->dev[0]);
+    dfree(h->g_s);
+    dfree(h->g_r);
+    h->g_s = nullptr;
+    h->g_r = nullptr;
+    h->nq_cap = h->k_cap = 0;
+}
+
+void ensure_search(rc_sharded *h, int nq, int k) {
+    if (nq <= h->nq_cap && k <= h->k_cap) return;
+    const int nq2 = std::max(nq, h->nq_cap), k2 = std::max(k, h->k_cap);
+    free_search(h);
+    for (int s = 0; s < h->n; ++s) {
+        if (h->dev[s] == h->dev[0]) continue;
+        DeviceScope ds(h->dev[s]);
+        h->q[s] = (float *)dmalloc((size_t)nq2 * h->dim * sizeof(float));
+        h->s_loc[s] = (float *)dmalloc((size_t)nq2 * k2 * sizeof(float));
+        h->r_loc[s] = (int64_t *)dmalloc((size_t)nq2 * k2 * sizeof(int64_t));
+    }
+    DeviceScope ds(h->dev[0]);
+    h->g_s = (float *)dmalloc((size_t)h->n * nq2 * k2 * sizeof(float));
+    h->g_r = (int64_t *)dmalloc((size_t)h->n * nq2 * k2 * sizeof(int64_t));
+    h->nq_cap = nq2;
+    h->k_cap = k2;
+}
+
+void free_staging(rc_sharded *h) {
+    for (int s = 0; s < h->n; ++s) {
+        DeviceScope ds(h->dev[s]);
+        dfree(h->idx_d[s]);
+        dfree(h->row_d[s]);
+        dfree(h->vec_d[s]);
+        h->idx_d[s] = h->row_d[s] = nullptr;
+        h->vec_d[s] = nullptr;
+    }
+    h->st_cap = 0;
+}
+
+void ensure_staging(rc_sharded *h, int64_t m) {
+    if (m <= h->st_cap) return;
+    const int64_t m2 = std::max<int64_t>(m, 2 * h->st_cap);
+    free_staging(h);
+    for (int s = 0; s < h->n; ++s) {
+        DeviceScope ds(h->dev[s]);
+        h->idx_d[s] = (int64_t *)dmalloc((size_t)m2 * sizeof(int64_t));
+        h->row_d[s] = (int64_t *)dmalloc((size_t)m2 * sizeof(int64_t));
+        if (h->dev[s] != h->dev[0]) h->vec_d[s] = (float *)dmalloc((size_t)m2 * h->dim * sizeof(float));
+    }
+    h->st_cap = m2;
+}
+
+// rows of the global range [0, n_rows) that shard s holds
+int64_t shard_rows(const rc_sharded *h, int s, int64_t n_rows) { return n_rows > s ? (n_rows - s + h->n - 1) / h->n : 0; }
+
+void destroy(rc_sharded *h) {
+    free_search(h);
+    free_staging(h);
+    for (int s = 0; s < h->n; ++s) {
+        DeviceScope ds(h->dev[s]);
+        if (h->st[s]) (void)hipStreamDestroy(h->st[s]);
+        if (h->ev_done[s]) (void)hipEventDestroy(h->ev_done[s]);
+        if (h->ev_start[s]) (void)hipEventDestroy(h->ev_start[s]);
+        if (h->shard[s]) (void)rc_index_destroy(h->shard[s]);
+    }
+    delete h;
+}
+
+void check_status(int st) {
+    if (st != RC_OK) throw Error(st, rc_last_error());
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int64_t capacity_per_shard, rc_sharded **out) {
+    return guard([&] {
+        RC_REQUIRE(out && devices, RC_ERR_INVALID, "null argument");
+        RC_REQUIRE(n_shards >= 1 && n_shards <= 64, RC_ERR_INVALID, "n_shards must be in [1, 64]");
+        RC_REQUIRE(capacity_per_shard > 0 && (double)capacity_per_shard * n_shards < 4294967296.0, RC_ERR_INVALID,
+                   "total capacity must be in [1, 2^32) rows (global rows key the cross-shard merge)");
+        auto *h = new rc_sharded();
+        h->n = n_shards;
+        h->dim = dim;
+        h->dtype = dtype;
+        h->cap = capacity_per_shard;
+        h->dev.assign(devices, devices + n_shards);
+        h->shard.assign(n_shards, nullptr);
+        h->st.assign(n_shards, nullptr);
+        h->ev_done.assign(n_shards, nullptr);
+        h->ev_start.assign(n_shards, nullptr);
+        h->q.assign(n_shards, nullptr);
+        h->s_loc.assign(n_shards, nullptr);
+        h->r_loc.assign(n_shards, nullptr);
+        h->idx_d.assign(n_shards, nullptr);
+        h->row_d.assign(n_shards, nullptr);
+        h->vec_d.assign(n_shards, nullptr);
+        try {
+            for (int s = 0; s < n_shards; ++s) {
+                check_status(rc_index_create(h->dev[s], dim, dtype, capacity_per_shard, s, &h->shard[s]));
+                check_status(rc_index_set_row_map(h->shard[s], s, n_shards));
+                DeviceScope ds(h->dev[s]);
+                RC_HIP(hipStreamCreateWithFlags(&h->st[s], hipStreamNonBlocking));
+                RC_HIP(hipEventCreateWithFlags(&h->ev_done[s], hipEventDisableTiming));
+                if (h->dev[s] != h->dev[0]) {  // direct xGMI peer copies where the platform allows them
+                    if (hipDeviceEnablePeerAccess(h->dev[0], 0) != hipSuccess) (void)hipGetLastError();
+                    DeviceScope dl(h->dev[0]);
+                    if (hipDeviceEnablePeerAccess(h->dev[s], 0) != hipSuccess) (void)hipGetLastError();
+                }
+            }
+            DeviceScope dl(h->dev[0]);
+            for (int s = 0; s < n_shards; ++s) RC_HIP(hipEventCreateWithFlags(&h->ev_start[s], hipEventDisableTiming));
+        } catch (...) {
+            destroy(h);
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int rc_sharded_destroy(rc_sharded *h) {
+    return guard([&] {
+        if (h) destroy(h);
+    });
+}
+
+int rc_sharded_info(const rc_sharded *h, int *n_shards, int64_t *capacity_per_shard, int64_t *ld) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        if (n_shards) *n_shards = h->n;
+        if (capacity_per_shard) *capacity_per_shard = h->cap;
+        if (ld) check_status(rc_index_info(h->shard[0], nullptr, nullptr, nullptr, ld));
+    });
+}
+
+int rc_sharded_shard(rc_sharded *h, int s, rc_index **out) {
+    return guard([&] {
+        RC_REQUIRE(h && out, RC_ERR_INVALID, "null argument");
+        RC_REQUIRE(s >= 0 && s < h->n, RC_ERR_INVALID, "shard out of range");
+        *out = h->shard[s];
+    });
+}
+
+int rc_sharded_grow(rc_sharded *h, int64_t new_capacity_per_shard) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE((double)new_capacity_per_shard * h->n < 4294967296.0, RC_ERR_INVALID, "total capacity must be < 2^32 rows");
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (new_capacity_per_shard <= h->cap) return;
+        for (int s = 0; s < h->n; ++s) check_status(rc_index_grow(h->shard[s], new_capacity_per_shard, h->st[s]));
+        h->cap = new_capacity_per_shard;
+    });
+}
+
+int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t *rows, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
+        if (n == 0) return;
+        RC_REQUIRE(vecs && rows, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        std::vector<std::vector<int64_t>> src(h->n), loc(h->n);
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t g = rows[i];
+            RC_REQUIRE(g >= 0 && g / h->n < h->cap, RC_ERR_INVALID, "row out of capacity");
+            src[g % h->n].push_back(i);
+            loc[g % h->n].push_back(g / h->n);
+        }
+        int64_t m = 0;
+        for (int s = 0; s < h->n; ++s) m = std::max<int64_t>(m, (int64_t)src[s].size());
+        ensure_staging(h, std::max<int64_t>(m, n));
+        hipStream_t ls = (hipStream_t)stream;
+        {
+            DeviceScope dl(h->dev[0]);
+            for (int s = 0; s < h->n; ++s) RC_HIP(hipEventRecord(h->ev_start[s], ls));
+        }
+        for (int s = 0; s < h->n; ++s) {
+            if (src[s].empty()) continue;
+            DeviceScope ds(h->dev[s]);
+            const int64_t ms = (int64_t)src[s].size();
+            RC_HIP(hipStreamWaitEvent(h->st[s], h->ev_start[s], 0));
+            RC_HIP(hipMemcpyAsync(h->idx_d[s], src[s].data(), ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
+            RC_HIP(hipMemcpyAsync(h->row_d[s], loc[s].data(), ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
+            const float *v = vecs;
+            if (h->dev[s] != h->dev[0]) {
+                RC_HIP(hipMemcpyPeerAsync(h->vec_d[s], h->dev[s], vecs, h->dev[0], (size_t)n * h->dim * sizeof(float), h->st[s]));
+                v = h->vec_d[s];
+            }
+            index_upsert_gather(h->shard[s], v, h->idx_d[s], ms, h->row_d[s], h->st[s]);
+        }
+        // the host index lists must outlive their async copies: finish here (upsert is synchronous,
+        // like the Pinecone call it replaces)
+        for (int s = 0; s < h->n; ++s) {
+            DeviceScope ds(h->dev[s]);
+            RC_HIP(hipStreamSynchronize(h->st[s]));
+        }
+    });
+}
+
+int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, int stored) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
+        if (n == 0) return;
+        RC_REQUIRE(rows && out, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        std::vector<std::vector<int64_t>> dst(h->n), loc(h->n);
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t g = rows[i];
+            RC_REQUIRE(g >= 0 && g / h->n < h->cap, RC_ERR_INVALID, "row out of capacity");
+            dst[g % h->n].push_back(i);
+            loc[g % h->n].push_back(g / h->n);
+        }
+        int64_t m = 0;
+        for (int s = 0; s < h->n; ++s) m = std::max<int64_t>(m, (int64_t)dst[s].size());
+        ensure_staging(h, m);
+        std::vector<float> tmp;
+        for (int s = 0; s < h->n; ++s) {
+            if (dst[s].empty()) continue;
+            DeviceScope ds(h->dev[s]);
+            const int64_t ms = (int64_t)dst[s].size();
+            float *buf = (float *)dmalloc((size_t)ms * h->dim * sizeof(float));
+            try {
+                RC_HIP(hipMemcpyAsync(h->row_d[s], loc[s].data(), ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
+                check_status(stored ? rc_index_fetch_stored(h->shard[s], h->row_d[s], ms, buf, h->st[s])
+                                    : rc_index_fetch(h->shard[s], h->row_d[s], ms, buf, h->st[s]));
+                tmp.resize((size_t)ms * h->dim);
+                RC_HIP(hipMemcpyAsync(tmp.data(), buf, tmp.size() * sizeof(float), hipMemcpyDeviceToHost, h->st[s]));
+                RC_HIP(hipStreamSynchronize(h->st[s]));
+            } catch (...) {
+                dfree(buf);
+                throw;
+            }
+            dfree(buf);
+            for (int64_t j = 0; j < ms; ++j)
+                std::memcpy(out + dst[s][j] * h->dim, tmp.data() + j * h->dim, (size_t)h->dim * sizeof(float));
+        }
+    });
+}
+
+int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
+                      int64_t *out_rows, int mode, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(nq >= 0, RC_ERR_INVALID, "negative query count");
+        RC_REQUIRE(k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "top_k must be in [1, 256]");
+        RC_REQUIRE(n_rows >= 0 && n_rows <= h->cap * h->n, RC_ERR_INVALID, "n_rows out of range");
+        if (nq == 0) return;
+        RC_REQUIRE(queries && scores && out_rows, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        hipStream_t ls = (hipStream_t)stream;
+        if (h->n == 1) {
+            check_status(rc_index_search_ex(h->shard[0], queries, nq, n_rows, k, scores, out_rows, mode, stream));
+            return;
+        }
+        ensure_search(h, nq, k);
+        const int64_t slice = (int64_t)nq * k;
+        {
+            DeviceScope dl(h->dev[0]);
+            for (int s = 0; s < h->n; ++s) RC_HIP(hipEventRecord(h->ev_start[s], ls));
+        }
+        for (int s = 0; s < h->n; ++s) {
+            DeviceScope ds(h->dev[s]);
+            RC_HIP(hipStreamWaitEvent(h->st[s], h->ev_start[s], 0));
+            const bool local = h->dev[s] == h->dev[0];
+            const float *q = queries;
+            if (!local) {
+                RC_HIP(hipMemcpyPeerAsync(h->q[s], h->dev[s], queries, h->dev[0], (size_t)nq * h->dim * sizeof(float), h->st[s]));
+                q = h->q[s];
+            }
+            float *so = local ? h->g_s + s * slice : h->s_loc[s];
+            int64_t *ro = local ? h->g_r + s * slice : h->r_loc[s];
+            check_status(rc_index_search_ex(h->shard[s], q, nq, shard_rows(h, s, n_rows), k, so, ro, mode, h->st[s]));
+            if (!local) {
+                RC_HIP(hipMemcpyPeerAsync(h->g_s + s * slice, h->dev[0], so, h->dev[s], slice * sizeof(float), h->st[s]));
+                RC_HIP(hipMemcpyPeerAsync(h->g_r + s * slice, h->dev[0], ro, h->dev[s], slice * sizeof(int64_t), h->st[s]));
+            }
+            RC_HIP(hipEventRecord(h->ev_done[s], h->st[s]));
+        }
+        DeviceScope dl(h->dev[0]);
+        for (int s = 0; s < h->n; ++s) RC_HIP(hipStreamWaitEvent(ls, h->ev_done[s], 0));
+        check_status(rc_topk_merge(h->g_s, h->g_r, h->n, nq, k, k, scores, out_rows, stream));
+    });
+}
+
+}  // extern "C"

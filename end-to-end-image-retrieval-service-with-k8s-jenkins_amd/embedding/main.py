@@ -67,25 +67,38 @@ def _gpu_jpeg(data: bytes) -> bool:
     return is_gpu_decodable(data)
 
 
-def embed_many(blobs: List[bytes]) -> list[list[float]]:
-    """Image bytes → raw CLS vectors: GPU JPEG decode where it applies, PIL otherwise."""
+def decode_many(blobs: List[bytes]) -> list:
+    """Image bytes → u8 HWC RGB images, validated as the reference validates them: baseline
+    JPEGs decoded on the GPU (device tensors, bit-exact with PIL), anything else — and any
+    stream the GPU decoder rejects — through PIL on the host (``UnidentifiedImageError`` → 400)."""
+    import numpy as np
+
     out: list = [None] * len(blobs)
     gpu = [i for i, b in enumerate(blobs) if _gpu_jpeg(b)]
-    host = [i for i in range(len(blobs)) if i not in set(gpu)]
-    images = {i: decode_image(blobs[i]) for i in host}  # validate before touching the model (400 needs no GPU)
-    emb = get_embedder()
+    gset = set(gpu)
+    host = [i for i in range(len(blobs)) if i not in gset]
+    for i in host:  # validate before touching the model (400 needs no GPU)
+        out[i] = np.asarray(decode_image(blobs[i]), dtype=np.uint8)
     if gpu:
         try:
-            for i, v in zip(gpu, emb.embed_jpeg([blobs[i] for i in gpu])):
-                out[i] = v
+            for i, im in zip(gpu, get_embedder().decode_jpeg([blobs[i] for i in gpu])):
+                out[i] = im
         except ValueError:  # a damaged stream: the reference's host decode decides (image or 400)
             for i in gpu:
-                images[i] = decode_image(blobs[i])
-            host = sorted(images)
-    if host:
-        for i, v in zip(host, emb.embed_pil([images[i] for i in host])):
-            out[i] = v
+                out[i] = np.asarray(decode_image(blobs[i]), dtype=np.uint8)
     return out
+
+
+def embed_many_device(blobs: List[bytes], normalized: bool = False):
+    """Image bytes → (raw [n,768], normed or None) device tensors (the batched ingest path)."""
+    images = decode_many(blobs)
+    return get_embedder().embed_images(images, normalized=normalized)
+
+
+def embed_many(blobs: List[bytes]) -> list[list[float]]:
+    """Image bytes → raw CLS vectors: GPU JPEG decode where it applies, PIL otherwise."""
+    raw, _ = embed_many_device(blobs)
+    return raw.cpu().tolist()
 
 
 def embed_bytes(data: bytes) -> list[float]:

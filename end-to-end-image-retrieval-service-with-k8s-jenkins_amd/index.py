@@ -37,21 +37,32 @@ def _device_index(device) -> int:
 
 
 class DeviceIndex:
-    """One ``rc_index`` handle: a contiguous block of row slots on one GPU (a shard)."""
+    """One ``rc_index`` handle: a block of row slots on one GPU (a shard).
 
-    def __init__(self, dim: int, dtype: str = "float32", capacity: int = 1 << 20, device=None, row_base: int = 0):
+    A search returns ``row_base + local_row * row_stride`` (``set_row_map``):
+    the global rows of a round-robin shard."""
+
+    def __init__(self, dim: int, dtype: str = "float32", capacity: int = 1 << 20, device=None, row_base: int = 0,
+                 row_stride: int = 1, _handle=None):
         self.lib = _lib.load()
         if dtype not in _lib.DTYPES:
             raise ValueError(f"unknown index dtype {dtype!r}")
         self.dim = int(dim)
         self.dtype = dtype
-        self.capacity = int(capacity)
         self.device_index = _device_index(device)
         self.device = torch.device("cuda", self.device_index)
         self.row_base = int(row_base)
-        h = _lib.C.c_void_p()
-        check(self.lib.rc_index_create(self.device_index, self.dim, _lib.DTYPES[dtype], self.capacity, self.row_base, _lib.C.byref(h)))
-        self._h = h
+        self.row_stride = int(row_stride)
+        self._owned = _handle is None
+        if _handle is None:
+            h = _lib.C.c_void_p()
+            check(self.lib.rc_index_create(self.device_index, self.dim, _lib.DTYPES[dtype], int(capacity), self.row_base,
+                                           _lib.C.byref(h)))
+            self._h = h
+            if self.row_stride != 1:
+                self.set_row_map(self.row_base, self.row_stride)
+        else:  # a shard borrowed from an rc_sharded handle (owned there)
+            self._h = _handle
 
     @property
     def handle(self):
@@ -59,9 +70,16 @@ class DeviceIndex:
             raise RuntimeError("index is closed")
         return self._h
 
+    @property
+    def capacity(self) -> int:
+        cap = _lib.C.c_int64()
+        check(self.lib.rc_index_info(self.handle, None, None, _lib.C.byref(cap), None))
+        return cap.value
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:
-            check(self.lib.rc_index_destroy(self._h))
+            if self._owned:
+                check(self.lib.rc_index_destroy(self._h))
             self._h = None
 
     def __del__(self):
@@ -75,6 +93,13 @@ class DeviceIndex:
         ld = _lib.C.c_int64()
         check(self.lib.rc_index_info(self.handle, None, None, None, _lib.C.byref(ld)))
         return ld.value
+
+    def set_row_map(self, row_base: int, row_stride: int = 1) -> None:
+        check(self.lib.rc_index_set_row_map(self.handle, int(row_base), int(row_stride)))
+        self.row_base, self.row_stride = int(row_base), int(row_stride)
+
+    def grow(self, new_capacity: int, stream=None) -> None:
+        check(self.lib.rc_index_grow(self.handle, int(new_capacity), stream_ptr(stream)))
 
     def reserve(self, max_nq: int, max_k: int) -> None:
         check(self.lib.rc_index_reserve(self.handle, int(max_nq), int(max_k)))
@@ -192,38 +217,197 @@ def _as_vector(values: Any, dim: int) -> list[float]:
     return vals
 
 
+class ShardSet:
+    """One ``rc_sharded`` handle: ``n`` shards (``rc_index`` each) in this process.
+
+    Global row g lives on shard ``g % n`` as local row ``g // n`` (round-robin,
+    SURVEY §8(e)); ``devices[s]`` is shard s's GPU (entries may repeat), and
+    ``devices[0]`` (the leader) holds queries and merged results."""
+
+    def __init__(self, dim: int, dtype: str = "float32", capacity_per_shard: int = 1 << 20, devices=None):
+        self.lib = _lib.load()
+        if dtype not in _lib.DTYPES:
+            raise ValueError(f"unknown index dtype {dtype!r}")
+        devs = [_device_index(d) for d in (devices if devices is not None else [None])]
+        if not devs:
+            raise ValueError("a sharded index needs at least one device")
+        self.dim = int(dim)
+        self.dtype = dtype
+        self.devices = devs
+        self.n = len(devs)
+        self.device = torch.device("cuda", devs[0])
+        arr = (_lib.C.c_int * self.n)(*devs)
+        h = _lib.C.c_void_p()
+        check(self.lib.rc_sharded_create(self.n, arr, self.dim, _lib.DTYPES[dtype], int(capacity_per_shard),
+                                         _lib.C.byref(h)))
+        self._h = h
+        self._shards = []
+        for sh in range(self.n):
+            ih = _lib.C.c_void_p()
+            check(self.lib.rc_sharded_shard(h, sh, _lib.C.byref(ih)))
+            self._shards.append(DeviceIndex(dim, dtype=dtype, device=devs[sh], row_base=sh, row_stride=self.n, _handle=ih))
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("index is closed")
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            for d in self._shards:
+                d.close()
+            check(self.lib.rc_sharded_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def capacity_per_shard(self) -> int:
+        cap = _lib.C.c_int64()
+        check(self.lib.rc_sharded_info(self.handle, None, _lib.C.byref(cap), None))
+        return cap.value
+
+    @property
+    def capacity(self) -> int:
+        return self.capacity_per_shard * self.n
+
+    @property
+    def ld(self) -> int:
+        ld = _lib.C.c_int64()
+        check(self.lib.rc_sharded_info(self.handle, None, None, _lib.C.byref(ld)))
+        return ld.value
+
+    def shard(self, s: int) -> DeviceIndex:
+        return self._shards[s]
+
+    def shard_rows(self, s: int, n_rows: int) -> int:
+        """How many of the global rows [0, n_rows) shard s holds."""
+        return (n_rows - s + self.n - 1) // self.n if n_rows > s else 0
+
+    def grow(self, new_capacity_per_shard: int) -> None:
+        check(self.lib.rc_sharded_grow(self.handle, int(new_capacity_per_shard)))
+
+    def upsert_rows(self, vecs: torch.Tensor, rows) -> None:
+        """vecs f32 [n, dim] (any device; moved to the leader), rows: global rows (host)."""
+        if vecs.dim() == 1:
+            vecs = vecs[None]
+        if vecs.shape[-1] != self.dim:
+            raise ValueError(f"Vector dimension {vecs.shape[-1]} does not match the dimension of the index {self.dim}")
+        vecs = vecs.to(device=self.device, dtype=torch.float32).contiguous()
+        rows = torch.as_tensor(rows, dtype=torch.int64).cpu().contiguous()
+        if rows.numel() != vecs.shape[0]:
+            raise ValueError("rows and vectors differ in length")
+        check(self.lib.rc_sharded_upsert(self.handle, ptr(vecs), vecs.shape[0], ptr(rows), stream_ptr(None)))
+
+    def fetch_rows(self, rows, stored: bool = False) -> torch.Tensor:
+        """Host f32 [n, dim]: the upserted values (or, ``stored``, the normalised stored rows)."""
+        rows = torch.as_tensor(rows, dtype=torch.int64).cpu().contiguous()
+        out = torch.empty((rows.numel(), self.dim), dtype=torch.float32)
+        if rows.numel():
+            check(self.lib.rc_sharded_fetch(self.handle, ptr(rows), rows.numel(), ptr(out), 1 if stored else 0))
+        return out
+
+    def search(self, queries: torch.Tensor, k: int, n_rows: int, mode: str = "auto", stream=None):
+        """Exact cosine top-k over global rows [0, n_rows): (scores f32 [nq,k], rows i64 [nq,k]) on the leader."""
+        if mode not in _lib.SEARCH_MODES:
+            raise ValueError(f"unknown search mode {mode!r}")
+        if queries.dim() == 1:
+            queries = queries[None]
+        q = queries.to(device=self.device, dtype=torch.float32).contiguous()
+        nq = q.shape[0]
+        scores = torch.empty((nq, k), dtype=torch.float32, device=self.device)
+        rows = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+        check(self.lib.rc_sharded_search(self.handle, ptr(q), nq, int(n_rows), int(k), ptr(scores), ptr(rows),
+                                         _lib.SEARCH_MODES[mode], stream_ptr(stream)))
+        return scores, rows
+
+    # raw stored rows in GLOBAL row order (the snapshot layout, independent of the shard count)
+    def export_rows(self, n_rows: int):
+        import numpy as np
+
+        el = 4 if self.dtype in ("float32", "f32") else 2
+        rows = np.zeros((n_rows, self.ld * el), dtype=np.uint8)
+        norms = np.zeros((n_rows,), dtype=np.float32)
+        for s in range(self.n):
+            m = self.shard_rows(s, n_rows)
+            if m == 0:
+                continue
+            r, nr = self._shards[s].export_rows(0, m)
+            torch.cuda.synchronize(self._shards[s].device)
+            rows[s::self.n] = r.cpu().numpy()
+            norms[s::self.n] = nr.cpu().numpy()
+        return rows, norms
+
+    def import_rows(self, rows, norms) -> None:
+        n_rows = len(norms)
+        for s in range(self.n):
+            if self.shard_rows(s, n_rows) == 0:
+                continue
+            self._shards[s].import_rows(0, torch.from_numpy(rows[s::self.n].copy()),
+                                        torch.from_numpy(norms[s::self.n].copy()))
+            torch.cuda.synchronize(self._shards[s].device)
+
+
 class Index:
     """Pinecone-shaped index (what ``get_index`` returns), cosine metric only.
 
     ``upsert(vectors)`` accepts ``(id, values)``, ``(id, values, metadata)``
     tuples or ``{"id", "values", "metadata"}`` dicts and overwrites existing
-    ids; ``query`` returns ``{"matches": [{"id", "score", ["values"],
-    ["metadata"]}], "namespace": ""}`` best first; ``fetch`` returns
-    ``{"vectors": {id: {"id", "values", "metadata"}}, "namespace": ""}``.
+    ids (within one call the last occurrence of an id wins); ``query`` returns
+    ``{"matches": [{"id", "score", ["values"], ["metadata"]}], "namespace": ""}``
+    best first; ``fetch`` returns ``{"vectors": {id: {"id", "values",
+    "metadata"}}, "namespace": ""}``.
+
+    The rows live on ``shards`` shards (``devices``: one GPU per shard, entries
+    may repeat; default one shard on ``device``), routed round-robin by the
+    row number the host assigns each new id, and searched as ONE exact index
+    (``rc_sharded``): results are identical to a single-shard index holding the
+    same vectors.  Capacity grows on demand (doubling), as a Pinecone index
+    has no fixed size.
     """
 
     def __init__(self, name: str, dimension: int = 768, metric: str = "cosine", dtype: str = "float32",
-                 capacity: int = 1 << 20, device=None):
+                 capacity: int = 1 << 20, device=None, shards: int | None = None, devices=None):
         if metric != "cosine":
             raise ValueError("only metric='cosine' is supported")
+        if devices is None:
+            devices = [device] * int(shards or 1)
         self.name = name
         self.dimension = int(dimension)
         self.metric = metric
-        self._dev = DeviceIndex(self.dimension, dtype=dtype, capacity=capacity, device=device)
+        n = len(devices)
+        self._set = ShardSet(self.dimension, dtype=dtype, capacity_per_shard=max(1, -(-int(capacity) // n)),
+                             devices=devices)
         self._rows: dict[str, int] = {}
         self._ids: list[str] = []
         self._meta: dict[str, dict] = {}
         self._mu = threading.Lock()
 
     @property
-    def device_index(self) -> DeviceIndex:
-        return self._dev
+    def shard_set(self) -> ShardSet:
+        return self._set
+
+    @property
+    def dtype(self) -> str:
+        return self._set.dtype
+
+    @property
+    def capacity(self) -> int:
+        return self._set.capacity
 
     def __len__(self) -> int:
         return len(self._ids)
 
+    def close(self) -> None:
+        self._set.close()
+
     def _normalize_items(self, vectors: Iterable) -> list[tuple[str, list[float], dict]]:
-        items = []
+        items: dict[str, tuple[str, list[float], dict]] = {}
         for v in vectors:
             if isinstance(v, dict):
                 vid, vals, md = v["id"], v["values"], v.get("metadata") or {}
@@ -238,93 +422,154 @@ class Index:
                     raise ValueError("vectors must be (id, values[, metadata]) tuples or dicts")
             if not isinstance(vid, str) or not vid:
                 raise ValueError("vector id must be a non-empty string")
-            items.append((vid, _as_vector(vals, self.dimension), dict(md)))
-        return items
+            # one row per id: a repeated id in one call keeps its LAST values (two
+            # writes of one row slot in the same launch would interleave)
+            items[vid] = (vid, _as_vector(vals, self.dimension), dict(md))
+        return list(items.values())
+
+    def _ensure_capacity(self, n_total: int) -> None:
+        if n_total <= self._set.capacity:
+            return
+        per = self._set.capacity_per_shard
+        need = -(-n_total // self._set.n)
+        while per < need:
+            per *= 2
+        self._set.grow(per)
 
     def upsert(self, vectors: Sequence, namespace: str = "") -> dict:
         items = self._normalize_items(vectors)
         if not items:
             return {"upserted_count": 0}
+        vecs = torch.tensor([it[1] for it in items], dtype=torch.float32)
         with self._mu:
-            rows = []
-            for vid, _, md in items:
-                r = self._rows.get(vid)
-                if r is None:
-                    r = len(self._ids)
-                    if r >= self._dev.capacity:
-                        raise ValueError(f"index {self.name!r} is full ({self._dev.capacity} vectors)")
-                    self._rows[vid] = r
-                    self._ids.append(vid)
-                rows.append(r)
-                self._meta[vid] = md
-            vecs = torch.tensor([it[1] for it in items], dtype=torch.float32).to(self._dev.device)
-            rows_t = torch.tensor(rows, dtype=torch.int64).to(self._dev.device)
-            self._dev.upsert_rows(vecs, rows_t)
-            torch.cuda.current_stream(self._dev.device).synchronize()
+            self._upsert_locked(items, vecs)
         return {"upserted_count": len(items)}
+
+    def upsert_tensor(self, ids: Sequence[str], vecs: torch.Tensor, metadata: Sequence[dict] | None = None) -> dict:
+        """Batched upsert of device-resident vectors (the ingest path: embeddings never leave HBM).
+
+        Same semantics as ``upsert`` (overwrite by id, last occurrence wins)."""
+        if vecs.dim() != 2 or vecs.shape[0] != len(ids) or vecs.shape[1] != self.dimension:
+            raise ValueError("vecs must be [len(ids), dimension]")
+        metadata = list(metadata) if metadata is not None else [{}] * len(ids)
+        if len(metadata) != len(ids):
+            raise ValueError("metadata and ids differ in length")
+        last: dict[str, int] = {}
+        for i, vid in enumerate(ids):
+            if not isinstance(vid, str) or not vid:
+                raise ValueError("vector id must be a non-empty string")
+            last[vid] = i
+        keep = list(last.values())
+        if len(keep) != len(ids):
+            vecs = vecs[torch.tensor(keep, dtype=torch.int64, device=vecs.device)]
+        if not bool((vecs != 0).any(dim=1).all()):
+            raise ValueError("Dense vectors must contain at least one non-zero value for the cosine metric")
+        items = [(ids[i], None, dict(metadata[i] or {})) for i in keep]
+        with self._mu:
+            self._upsert_locked(items, vecs)
+        return {"upserted_count": len(items)}
+
+    def _upsert_locked(self, items, vecs: torch.Tensor) -> None:
+        new = sum(1 for vid, _, _ in items if vid not in self._rows)
+        self._ensure_capacity(len(self._ids) + new)
+        rows = []
+        for vid, _, md in items:
+            r = self._rows.get(vid)
+            if r is None:
+                r = len(self._ids)
+                self._rows[vid] = r
+                self._ids.append(vid)
+            rows.append(r)
+            self._meta[vid] = md
+        self._set.upsert_rows(vecs, rows)
 
     def query(self, vector=None, top_k: int = 10, include_values: bool = False, include_metadata: bool = False,
               id: str | None = None, namespace: str = "", **_: Any) -> dict:
         if vector is None and id is None:
             raise ValueError("query needs a vector or an id")
-        if top_k < 1:
+        if isinstance(top_k, bool) or int(top_k) != top_k or top_k < 1:
             raise ValueError("top_k must be a positive integer")
+        top_k = int(top_k)
+        if top_k > _lib.RC_TOPK_MAX:
+            raise ValueError(f"top_k must be <= {_lib.RC_TOPK_MAX}")
         with self._mu:
             if vector is None:
-                vec = self.fetch([id])["vectors"].get(id)
-                if vec is None:
+                r = self._rows.get(id)
+                if r is None:
                     return {"matches": [], "namespace": namespace}
-                vector = vec["values"]
-            q = torch.tensor([_as_vector(vector, self.dimension)], dtype=torch.float32).to(self._dev.device)
-            n = len(self._ids)
-            k = min(int(top_k), _lib.RC_TOPK_MAX)
+                vector = self._set.fetch_rows([r])[0]
+            q = torch.tensor([_as_vector(vector, self.dimension)], dtype=torch.float32)
+            res = self._query_locked(q, top_k, include_values, include_metadata)[0]
+        return {"matches": res, "namespace": namespace}
+
+    def query_batch(self, vectors, top_k: int = 10, include_values: bool = False,
+                    include_metadata: bool = False, mode: str = "auto") -> list[dict]:
+        """Batched form of ``query`` (f16/bf16 shards run the MFMA path for >= 8 queries)."""
+        if top_k < 1 or top_k > _lib.RC_TOPK_MAX:
+            raise ValueError(f"top_k must be in [1, {_lib.RC_TOPK_MAX}]")
+        if isinstance(vectors, torch.Tensor):
+            q = vectors.to(torch.float32)
+            if q.dim() != 2 or q.shape[1] != self.dimension:
+                raise ValueError("queries must be [n, dimension]")
+        else:
+            q = torch.tensor([_as_vector(v, self.dimension) for v in vectors], dtype=torch.float32)
+        with self._mu:
+            res = self._query_locked(q, top_k, include_values, include_metadata, mode)
+        return [{"matches": m, "namespace": ""} for m in res]
+
+    def _query_locked(self, q: torch.Tensor, k: int, include_values: bool, include_metadata: bool,
+                      mode: str = "auto") -> list[list[dict]]:
+        n = len(self._ids)
+        if n == 0 or q.shape[0] == 0:
+            return [[] for _ in range(q.shape[0])]
+        scores, rows = self._set.search(q, k, n, mode=mode)
+        scores = scores.cpu().tolist()
+        rows = rows.cpu().tolist()
+        out = []
+        for sq, rq in zip(scores, rows):
+            sel = [(s, r) for s, r in zip(sq, rq) if r >= 0]
+            vals = self._set.fetch_rows([r for _, r in sel]).tolist() if include_values and sel else None
             matches = []
-            if n > 0:
-                scores, rows = self._dev.search(q, k, n)
-                scores = scores[0].cpu().tolist()
-                rows = rows[0].cpu().tolist()
-                sel = [(s, r) for s, r in zip(scores, rows) if r >= 0]
-                vals = None
-                if include_values and sel:
-                    vals = self._dev.fetch_rows(torch.tensor([r for _, r in sel], dtype=torch.int64)).cpu().tolist()
-                for j, (s, r) in enumerate(sel):
-                    m = {"id": self._ids[r], "score": float(s)}
-                    if include_values:
-                        m["values"] = vals[j]
-                    if include_metadata:
-                        m["metadata"] = dict(self._meta.get(self._ids[r], {}))
-                    matches.append(m)
-        return {"matches": matches, "namespace": namespace}
+            for j, (s, r) in enumerate(sel):
+                m = {"id": self._ids[r], "score": float(s)}
+                if include_values:
+                    m["values"] = vals[j]
+                if include_metadata:
+                    m["metadata"] = dict(self._meta.get(self._ids[r], {}))
+                matches.append(m)
+            out.append(matches)
+        return out
 
     def fetch(self, ids: Sequence[str], namespace: str = "") -> dict:
-        found = [(i, self._rows[i]) for i in ids if i in self._rows]
-        vectors = {}
-        if found:
-            vals = self._dev.fetch_rows(torch.tensor([r for _, r in found], dtype=torch.int64)).cpu().tolist()
-            for (vid, _), v in zip(found, vals):
-                vectors[vid] = {"id": vid, "values": v, "metadata": dict(self._meta.get(vid, {}))}
+        with self._mu:
+            found = [(i, self._rows[i]) for i in ids if i in self._rows]
+            vectors = {}
+            if found:
+                vals = self._set.fetch_rows([r for _, r in found]).tolist()
+                for (vid, _), v in zip(found, vals):
+                    vectors[vid] = {"id": vid, "values": v, "metadata": dict(self._meta.get(vid, {}))}
         return {"vectors": vectors, "namespace": namespace}
 
     # ---------------------------------------------------------- persistence --
     # Pinecone keeps an index durable server-side (the reference only opens it by
     # name, ingesting/utils.py:23-38); the in-HBM index is saved to a directory:
     # manifest.json (name, dimension, dtype, ids in row order, metadata) +
-    # rows.npy (raw stored bytes, exactly what search scores) + norms.npy.
+    # rows.npy (raw stored bytes in GLOBAL row order, exactly what search scores;
+    # independent of the shard count) + norms.npy.
     SNAPSHOT_FORMAT = 1
 
     def save(self, path: str) -> None:
+        import numpy as np
+
         with self._mu:
             os.makedirs(path, exist_ok=True)
             n = len(self._ids)
-            rows, norms = self._dev.export_rows(0, n)
-            torch.cuda.current_stream(self._dev.device).synchronize()
-            import numpy as np
-
-            np.save(os.path.join(path, "rows.npy"), rows.cpu().numpy())
-            np.save(os.path.join(path, "norms.npy"), norms.cpu().numpy())
+            rows, norms = self._set.export_rows(n)
+            np.save(os.path.join(path, "rows.npy"), rows)
+            np.save(os.path.join(path, "norms.npy"), norms)
             manifest = {"format": self.SNAPSHOT_FORMAT, "name": self.name, "dimension": self.dimension,
-                        "metric": self.metric, "dtype": self._dev.dtype, "ld": self._dev.ld, "count": n,
-                        "capacity": self._dev.capacity,
+                        "metric": self.metric, "dtype": self._set.dtype, "ld": self._set.ld, "count": n,
+                        "capacity": self._set.capacity,
                         "ids": list(self._ids), "metadata": {i: self._meta.get(i, {}) for i in self._ids}}
             tmp = os.path.join(path, "manifest.json.tmp")
             with open(tmp, "w") as f:
@@ -332,7 +577,8 @@ class Index:
             os.replace(tmp, os.path.join(path, "manifest.json"))  # the manifest lands last
 
     @classmethod
-    def load(cls, path: str, capacity: int | None = None, device=None) -> "Index":
+    def load(cls, path: str, capacity: int | None = None, device=None, shards: int | None = None,
+             devices=None) -> "Index":
         import numpy as np
 
         with open(os.path.join(path, "manifest.json")) as f:
@@ -341,21 +587,22 @@ class Index:
             raise ValueError(f"unsupported snapshot format {man.get('format')!r}")
         n = int(man["count"])
         idx = cls(man["name"], dimension=man["dimension"], metric=man["metric"], dtype=man["dtype"],
-                  capacity=max(int(capacity or man.get("capacity", 0)), n, 1), device=device)
-        if idx._dev.ld != man["ld"]:
+                  capacity=max(int(capacity or man.get("capacity", 0)), n, 1), device=device, shards=shards,
+                  devices=devices)
+        if idx._set.ld != man["ld"]:
             raise ValueError("snapshot row layout does not match this build")
         rows = np.load(os.path.join(path, "rows.npy"), allow_pickle=False)
         norms = np.load(os.path.join(path, "norms.npy"), allow_pickle=False)
         if rows.shape[0] != n or norms.shape[0] != n or len(man["ids"]) != n:
             raise ValueError("snapshot files disagree on the vector count")
         if n:
-            idx._dev.import_rows(0, torch.from_numpy(rows), torch.from_numpy(norms))
-            torch.cuda.current_stream(idx._dev.device).synchronize()
+            idx._set.import_rows(rows, norms)
         idx._ids = list(man["ids"])
         idx._rows = {vid: r for r, vid in enumerate(idx._ids)}
         idx._meta = {vid: dict(man["metadata"].get(vid, {})) for vid in idx._ids}
         return idx
 
     def describe_index_stats(self) -> dict:
-        return {"dimension": self.dimension, "index_fullness": len(self._ids) / self._dev.capacity,
-                "total_vector_count": len(self._ids), "namespaces": {"": {"vector_count": len(self._ids)}}}
+        return {"dimension": self.dimension, "index_fullness": len(self._ids) / self._set.capacity,
+                "total_vector_count": len(self._ids), "namespaces": {"": {"vector_count": len(self._ids)}},
+                "shards": self._set.n}

@@ -1,0 +1,121 @@
+"""Batched ingest core: N images → validate → GPU decode → ONE batched embed → ONE upsert.
+
+Reference: ``push_image`` (``ingesting/main.py:101-168``) ingests one image per
+request — extension check (``:111-115``), validation decode (``:116-119``),
+``get_feature_vector`` over HTTP (``:124``), a uuid4 id (``:127-128``), GCS
+upload + signed URL (``:130-151``), ``index.upsert([(file_id, feature,
+{"gcs_path", "filename"})])`` (``:156-158``) and the 4-key response
+(``:163-168``).  ``ingest_many`` keeps every one of those steps and their order
+per image, but the arithmetic runs batched on the GPU: baseline JPEGs are
+decoded on the device (bit-exact with the reference's PIL decode), every image
+is embedded in ``rc_embed`` batches, and the raw CLS vectors go straight from
+HBM into one ``Index.upsert_tensor`` call (normalised on the device, as
+Pinecone's cosine index normalises server-side).  The result for image i equals
+what a single ``/push_image`` of image i returns (modulo the random uuid).
+
+Blob storage (GCS upload / signed URL) is out of scope: it is a hook
+(``StorageHook``) whose default does nothing but name the object.  A real
+deployment passes an object that uploads and signs.
+"""
+from __future__ import annotations
+
+import uuid
+from typing import Callable, Sequence
+
+from fastapi import HTTPException
+
+from ..config import Config
+
+ALLOWED_EXTENSIONS = {"jpg", "jpeg", "png"}  # ingesting/main.py:112
+
+
+class StorageHook:
+    """No-op stand-in for the reference's GCS bucket (``ingesting/main.py:130-151``)."""
+
+    def __init__(self, bucket: str = Config.GCS_BUCKET_NAME):
+        self.bucket = bucket
+
+    def upload(self, gcs_path: str, data: bytes, content_type: str | None) -> None:
+        return None
+
+    def signed_url(self, gcs_path: str, filename: str | None) -> str:
+        return f"https://storage.googleapis.com/{self.bucket}/{gcs_path}"
+
+
+def file_extension(filename: str | None) -> str:
+    """``file.filename.split(".")[-1].lower()`` (ingesting/main.py:111)."""
+    return (filename or "").split(".")[-1].lower()
+
+
+def validate_extension(filename: str | None) -> str:
+    ext = file_extension(filename)
+    if ext not in ALLOWED_EXTENSIONS:
+        raise HTTPException(status_code=400, detail="Only .jpg/.jpeg/.png allowed")
+    return ext
+
+
+def ingest_many(files: Sequence[tuple], index, storage: StorageHook | None = None,
+                id_factory: Callable[[], str] | None = None) -> list[dict]:
+    """files: ``(filename, bytes[, content_type])`` per image → one response dict per image.
+
+    Every image is validated before anything is embedded or stored (a bad file
+    fails the whole call with the reference's 400, and nothing is ingested).
+    ``index`` may be a zero-argument callable (opened only once the batch is valid)."""
+    from ..embedding import main as emb
+
+    storage = storage or StorageHook()
+    id_factory = id_factory or (lambda: str(uuid.uuid4()))
+    names, blobs, ctypes_, exts = [], [], [], []
+    for f in files:
+        filename, data = f[0], f[1]
+        exts.append(validate_extension(filename))
+        names.append(filename)
+        blobs.append(data)
+        ctypes_.append(f[2] if len(f) > 2 else None)
+    if not blobs:
+        return []
+    try:  # validation decode (ingesting/main.py:116-119), on the GPU for baseline JPEGs
+        images = emb.decode_many(blobs)
+    except HTTPException as e:
+        if e.status_code == 400:
+            raise HTTPException(status_code=400, detail="Invalid image file")
+        raise
+    raw, _ = emb.get_embedder().embed_images(images)
+    ids = [id_factory() for _ in blobs]
+    paths = [f"images/{fid}.{ext}" for fid, ext in zip(ids, exts)]
+    urls = []
+    for p, data, ct, name in zip(paths, blobs, ctypes_, names):
+        storage.upload(p, data, ct)
+        urls.append(storage.signed_url(p, name))
+    index = index() if callable(index) else index
+    index.upsert_tensor(ids, raw, [{"gcs_path": p, "filename": n} for p, n in zip(paths, names)])
+    return [{"message": "Successfully!", "file_id": fid, "gcs_path": p, "signed_url": u}
+            for fid, p, u in zip(ids, paths, urls)]
+
+
+def push_one(filename: str, data: bytes, index, content_type: str | None = None, storage: StorageHook | None = None,
+             feature_fn: Callable[[bytes], list] | None = None, id_factory: Callable[[], str] | None = None) -> dict:
+    """The single-image ``/push_image`` flow (ingesting/main.py:101-168), step for step:
+    ext check → validation decode → feature vector (``feature_fn``, default the in-process
+    embed; the reference POSTs to /embed) → uuid → storage hook → ``index.upsert``.
+    ``index`` may be a zero-argument callable (opened only once the image is valid)."""
+    from io import BytesIO
+
+    from PIL import Image, UnidentifiedImageError
+
+    ext = validate_extension(filename)
+    try:
+        Image.open(BytesIO(data)).convert("RGB")
+    except UnidentifiedImageError:
+        raise HTTPException(status_code=400, detail="Invalid image file")
+    if feature_fn is None:
+        from ..embedding.main import embed_bytes as feature_fn
+    feature = feature_fn(data)
+    file_id = (id_factory or (lambda: str(uuid.uuid4())))()
+    gcs_path = f"images/{file_id}.{ext}"
+    storage = storage or StorageHook()
+    storage.upload(gcs_path, data, content_type)
+    signed_url = storage.signed_url(gcs_path, filename)
+    index = index() if callable(index) else index
+    index.upsert([(file_id, feature, {"gcs_path": gcs_path, "filename": filename})])
+    return {"message": "Successfully!", "file_id": file_id, "gcs_path": gcs_path, "signed_url": signed_url}

@@ -28,14 +28,31 @@ _indexes: dict = {}
 _lock = threading.Lock()
 
 
-def get_index(index_name: str, dimension: int | None = None, dtype: str | None = None, capacity: int | None = None):
+def index_devices(spec: str | None = None, shards: int | None = None) -> list:
+    """Shard placement for ``get_index``: "all" = one shard per visible GPU, "0,2,4" = those
+    GPUs, "" = ``shards`` shards on the current GPU."""
+    import torch
+
+    spec = Config.INDEX_DEVICES if spec is None else spec
+    if spec.strip() == "all":
+        return list(range(torch.cuda.device_count()))
+    if spec.strip():
+        return [int(x) for x in spec.split(",") if x.strip()]
+    return [None] * int(shards or Config.INDEX_SHARDS)
+
+
+def get_index(index_name: str, dimension: int | None = None, dtype: str | None = None, capacity: int | None = None,
+              devices: list | None = None):
+    """Open or create the named index (reference ``:23-38``): one logical cosine index of
+    ``Config.INPUT_RESOLUTION`` dims, row-sharded over ``devices`` (default: ``Config.INDEX_DEVICES``)."""
     from ..index import Index
 
     with _lock:
         idx = _indexes.get(index_name)
         if idx is None:
             idx = Index(index_name, dimension=dimension or Config.INPUT_RESOLUTION, metric="cosine",
-                        dtype=dtype or Config.INDEX_DTYPE, capacity=capacity or Config.INDEX_CAPACITY)
+                        dtype=dtype or Config.INDEX_DTYPE, capacity=capacity or Config.INDEX_CAPACITY,
+                        devices=devices if devices is not None else index_devices())
             _indexes[index_name] = idx
             logger.info("Created in-HBM index: %s", index_name)
         return idx

@@ -1,15 +1,21 @@
 """Row-sharded exact cosine index across the GPUs of one node (one process per GPU).
 
-SURVEY §8(e): rows split contiguously — rank r owns global rows
-[r*C, (r+1)*C) of a per-rank capacity C.  A query batch (identical on every
-rank) is scanned by each rank's HIP kernel over its shard → local top-k
-``(f32 score, i64 global row)``; one ``all_gather_into_tensor`` per output
-(RCCL over xGMI; Q*k*12 B per rank) brings every rank's list to every rank, and
-``rc_topk_merge`` merges them on the device with the same tie rule (score desc,
-row asc).  Upserts need no collective: a row is written only by its owner.
+SURVEY §8(e): global row g lives on rank ``g % W`` as local row ``g // W``
+(round-robin routing, so every rank's shard fills from the first upsert); the
+shard reports global rows itself (``rc_index_set_row_map(rank, W)``).  A query
+batch (identical on every rank) is searched by each rank's HIP kernels over its
+shard → local top-k ``(f32 score, i64 global row)``; one
+``all_gather_into_tensor`` per output (RCCL over xGMI under the ``nccl``
+backend, Q*k*12 B per rank; host tensors under ``gloo``) brings every rank's
+list to every rank, and ``rc_topk_merge`` merges them on the device keyed by
+(score desc, global row asc) — the order one index over all rows gives.  An
+empty shard answers ``(-inf, -1)`` lists, so every rank always reaches the
+collective.  Upserts need no collective: a row is written only by its owner.
 
 Pinecone does the cross-partition merge server-side (the reference only sees
 ``index.query`` at ``retriever/utils.py:62``); this is the MI355X equivalent.
+The single-process form (several shards driven by one process, peer copies
+instead of a collective) is ``index.ShardSet`` / ``rc_sharded``.
 """
 from __future__ import annotations
 
@@ -27,35 +33,55 @@ class ShardedIndex:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.host_exchange = dist.is_initialized() and dist.get_backend(group) == "gloo"
         self.dim = int(dim)
         self.capacity = int(capacity_per_rank)
-        self.row_base = self.rank * self.capacity
         if backend_factory is None:
             from .index import DeviceIndex, topk_merge
 
             backend_factory = lambda: DeviceIndex(dim, dtype=dtype, capacity=capacity_per_rank, device=device,
-                                                  row_base=self.row_base)
+                                                  row_base=self.rank, row_stride=self.world)
             merge_fn = merge_fn or topk_merge
         self.local = backend_factory()
         self.merge = merge_fn
-        self.n_local = 0  # rows [0, n_local) of the shard hold data
+        self.n_rows = 0  # global rows [0, n_rows) hold data (the same value on every rank)
+
+    @property
+    def n_local(self) -> int:
+        """Rows of the global range [0, n_rows) this rank holds."""
+        return (self.n_rows - self.rank + self.world - 1) // self.world if self.n_rows > self.rank else 0
 
     def owner(self, global_rows: torch.Tensor) -> torch.Tensor:
-        return torch.div(global_rows, self.capacity, rounding_mode="floor")
+        return torch.remainder(global_rows, self.world)
 
     def upsert_rows(self, vecs: torch.Tensor, global_rows: torch.Tensor) -> int:
         """Called with the same (vecs, global_rows) on every rank; each rank writes the rows it owns."""
-        mine = self.owner(global_rows.cpu()) == self.rank
+        gr = torch.as_tensor(global_rows, dtype=torch.int64).cpu()
+        if gr.numel() == 0:
+            return 0
+        if int(gr.min()) < 0 or int(gr.max()) // self.world >= self.capacity:
+            raise ValueError("row out of capacity")
+        mine = self.owner(gr) == self.rank
         if bool(mine.any()):
             idx = torch.nonzero(mine).reshape(-1)
-            local_rows = global_rows.cpu()[idx] - self.row_base
-            self.local.upsert_rows(vecs[idx.to(vecs.device)], local_rows)
-            self.n_local = max(self.n_local, int(local_rows.max()) + 1)
+            self.local.upsert_rows(vecs[idx.to(vecs.device)], torch.div(gr[idx], self.world, rounding_mode="floor"))
+        self.n_rows = max(self.n_rows, int(gr.max()) + 1)
         return int(mine.sum())
 
+    def upsert_local(self, vecs: torch.Tensor, local_rows: torch.Tensor) -> None:
+        """Rank-local ingest (data-parallel embed → own shard, no collective): vecs go to this
+        rank's local rows, i.e. global rows local * W + rank.  Call ``set_rows`` once every
+        rank has ingested to publish the global row count."""
+        self.local.upsert_rows(vecs, local_rows)
+
+    def set_rows(self, n_rows: int) -> None:
+        self.n_rows = int(n_rows)
+
     def fill_random(self, seed: int, n_local: int) -> None:
+        """Synthetic shard (benchmarks): every rank fills n_local rows, so the index holds
+        n_local * W global rows."""
         self.local.fill_random(seed, 0, n_local)
-        self.n_local = n_local
+        self.n_rows = n_local * self.world
 
     def search(self, queries: torch.Tensor, k: int, **kw):
         """Exact global top-k for the (replicated) queries: (scores [nq,k], global rows [nq,k]) on every rank.
@@ -65,10 +91,14 @@ class ShardedIndex:
         if self.world == 1:
             return s, r
         nq = s.shape[0]
+        dev = s.device
+        if self.host_exchange:  # gloo: the exchange runs on host copies
+            s, r = s.cpu(), r.cpu()
         gs = torch.empty((self.world * nq, k), dtype=s.dtype, device=s.device)
         gr = torch.empty((self.world * nq, k), dtype=r.dtype, device=r.device)
         dist.all_gather_into_tensor(gs, s.contiguous(), group=self.group)
         dist.all_gather_into_tensor(gr, r.contiguous(), group=self.group)
+        gs, gr = gs.to(dev), gr.to(dev)
         return self.merge(gs.view(self.world, nq, k), gr.view(self.world, nq, k), k)
 
     # ---------------------------------------------------------- persistence --
@@ -85,8 +115,8 @@ class ShardedIndex:
         np.save(os.path.join(d, "rows.npy"), rows.cpu().numpy())
         np.save(os.path.join(d, "norms.npy"), norms.cpu().numpy())
         with open(os.path.join(d, "manifest.json"), "w") as f:
-            json.dump({"format": 1, "rank": self.rank, "world": self.world, "dim": self.dim,
-                       "capacity_per_rank": self.capacity, "n_local": self.n_local}, f)
+            json.dump({"format": 2, "rank": self.rank, "world": self.world, "dim": self.dim,
+                       "routing": "round-robin", "capacity_per_rank": self.capacity, "n_rows": self.n_rows}, f)
 
     def load(self, path: str) -> None:
         import numpy as np
@@ -94,13 +124,15 @@ class ShardedIndex:
         d = os.path.join(path, f"shard{self.rank}")
         with open(os.path.join(d, "manifest.json")) as f:
             man = json.load(f)
+        if man.get("format") != 2:
+            raise ValueError(f"unsupported shard snapshot format {man.get('format')!r}")
         if (man["world"], man["capacity_per_rank"], man["dim"]) != (self.world, self.capacity, self.dim):
             raise ValueError("snapshot was taken with a different world size, capacity or dimension")
         rows = np.load(os.path.join(d, "rows.npy"), allow_pickle=False)
         norms = np.load(os.path.join(d, "norms.npy"), allow_pickle=False)
-        if man["n_local"]:
+        self.n_rows = int(man["n_rows"])
+        if self.n_local:
             self.local.import_rows(0, torch.from_numpy(rows), torch.from_numpy(norms))
-        self.n_local = int(man["n_local"])
 
     def close(self) -> None:
         close = getattr(self.local, "close", None)

@@ -157,43 +157,48 @@ class VitMsnEmbedder:
         check(self.lib.rc_preprocess(self._h, ptr(x), n, h, w, ptr(out), stream_ptr(stream)))
         return out
 
-    def embed_pil(self, images: Sequence) -> list[list[float]]:
-        """Host PIL RGB images (any sizes) → raw CLS vectors as Python lists (the /embed body)."""
-        out: list[list[float] | None] = [None] * len(images)
+    def embed_images(self, images: Sequence, normalized: bool = False):
+        """u8 HWC RGB images of any sizes (device tensors or host arrays) → (raw [n,H], normed [n,H]
+        or None) f32 device tensors in input order; equal-size images share ``rc_embed`` batches."""
+        n = len(images)
+        raw = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device)
+        nrm = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device) if normalized else None
         groups: dict[tuple[int, int], list[int]] = {}
         for i, im in enumerate(images):
-            groups.setdefault((im.size[1], im.size[0]), []).append(i)
-        for (h, w), idx in groups.items():
-            for s in range(0, len(idx), self.max_batch):
-                chunk = idx[s:s + self.max_batch]
-                arr = np.stack([np.asarray(images[i].convert("RGB"), dtype=np.uint8) for i in chunk])
-                raw, _ = self.embed(torch.from_numpy(arr), normalized=False)
-                vals = raw.cpu().tolist()
-                for j, i in enumerate(chunk):
-                    out[i] = vals[j]
-        return out  # type: ignore[return-value]
+            groups.setdefault((int(im.shape[0]), int(im.shape[1])), []).append(i)
+        for idx in groups.values():
+            for s0 in range(0, len(idx), self.max_batch):
+                chunk = idx[s0:s0 + self.max_batch]
+                if isinstance(images[chunk[0]], torch.Tensor):
+                    x = torch.stack([images[i] for i in chunk])
+                else:
+                    x = torch.from_numpy(np.stack([np.asarray(images[i], dtype=np.uint8) for i in chunk]))
+                r, m = self.embed(x, normalized=normalized)
+                sel = torch.tensor(chunk, dtype=torch.int64, device=self.device)
+                raw.index_copy_(0, sel, r)
+                if normalized:
+                    nrm.index_copy_(0, sel, m)
+        return raw, nrm
 
-    def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
-        """Baseline-JPEG byte strings → raw CLS vectors, decoded on the GPU (rc_jpeg_decode,
-        bit-exact with the reference's PIL decode) and embedded without a host RGB copy.
-        Raises jpeg.JpegUnsupported for streams the GPU decoder does not handle."""
+    def embed_pil(self, images: Sequence) -> list[list[float]]:
+        """Host PIL RGB images (any sizes) → raw CLS vectors as Python lists (the /embed body)."""
+        raw, _ = self.embed_images([np.asarray(im.convert("RGB"), dtype=np.uint8) for im in images])
+        return raw.cpu().tolist()
+
+    def decode_jpeg(self, datas: Sequence[bytes]) -> list[torch.Tensor]:
+        """Baseline-JPEG byte strings → device HWC RGB u8 images (rc_jpeg_decode, bit-exact with
+        the reference's PIL decode).  Raises jpeg.JpegUnsupported / ValueError like the decoder."""
         from .jpeg import JpegDecoder
 
         if self._jpeg is None:
             self._jpeg = JpegDecoder(self.device, max_images=max(self.max_batch, 32), max_pixels=1 << 24)
-        imgs = self._jpeg.decode(datas)
-        out: list[list[float] | None] = [None] * len(imgs)
-        groups: dict[tuple[int, int], list[int]] = {}
-        for i, im in enumerate(imgs):
-            groups.setdefault(tuple(im.shape[:2]), []).append(i)
-        for idx in groups.values():
-            for s in range(0, len(idx), self.max_batch):
-                chunk = idx[s:s + self.max_batch]
-                raw, _ = self.embed(torch.stack([imgs[i] for i in chunk]), normalized=False)
-                vals = raw.cpu().tolist()
-                for j, i in enumerate(chunk):
-                    out[i] = vals[j]
-        return out  # type: ignore[return-value]
+        return self._jpeg.decode(datas)
+
+    def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
+        """Baseline-JPEG byte strings → raw CLS vectors, decoded on the GPU and embedded without a
+        host RGB copy.  Raises jpeg.JpegUnsupported for streams the GPU decoder does not handle."""
+        raw, _ = self.embed_images(self.decode_jpeg(datas))
+        return raw.cpu().tolist()
 
     def embed_jpeg_stream(self, batches: Iterable[Sequence[bytes]], normalized: bool = True):
         """Pipelined JPEG bytes → embeddings for a stream of equal-size-image batches

@@ -49,6 +49,7 @@ extern "C" {
 #define RC_TOPK_MAX 256 /* largest k a single search call accepts */
 
 typedef struct rc_index rc_index;
+typedef struct rc_sharded rc_sharded;
 typedef struct rc_model rc_model;
 
 const char *rc_last_error(void);
@@ -62,8 +63,9 @@ int rc_abi_version(void);
  *   index.fetch(ids)           retriever/main.py:142
  * Rows are stored L2-normalised in `dtype`, row-major with leading dimension
  * ld = round_up(dim, 128) (zero padded).  String ids and metadata stay on the
- * host; the device only knows row numbers.  `row_base` is added to every row
- * a search returns (shard offset in a multi-GPU index).
+ * host; the device only knows row numbers.  A search returns
+ * row_base + local_row * row_stride (row_stride = 1 unless rc_index_set_row_map
+ * says otherwise): the global row of a shard in a multi-GPU index.
  * ---------------------------------------------------------------------- */
 
 /* replaces pc.create_index(metric="cosine", dimension=dim) — ingesting/utils.py:29-36 */
@@ -72,6 +74,17 @@ int rc_index_destroy(rc_index *h);
 int rc_index_info(const rc_index *h, int *dim, int *dtype, int64_t *capacity, int64_t *ld);
 /* device pointer to row 0 of the stored (normalised, cast) rows */
 int rc_index_data(const rc_index *h, void **rows_dev, float **norms_dev);
+
+/* Shard row map: local row l is reported as row_base + l * row_stride (a
+ * round-robin shard s of n uses row_base = s, row_stride = n). */
+int rc_index_set_row_map(rc_index *h, int64_t row_base, int64_t row_stride);
+
+/* Grow the row capacity in place (rows and norms are copied to a larger
+ * allocation; new slots are zero).  Pinecone indexes have no fixed capacity
+ * (ingesting/utils.py:29-36 creates one without a size); the host layer grows
+ * on demand.  The caller orders earlier work on other streams; the call
+ * synchronises the device before releasing the old buffers. */
+int rc_index_grow(rc_index *h, int64_t new_capacity, void *stream);
 
 /* Size the search workspace for up to max_nq queries and k <= max_k.  Called
  * once before the hot loop; search grows it on demand otherwise. */
@@ -102,8 +115,9 @@ int rc_index_import(rc_index *h, int64_t row0, int64_t n, const void *rows_in, c
 /* replaces index.query(vector, top_k) — retriever/utils.py:62-64.
  * queries: device f32 [nq, dim] (normalised inside); rows [0, n_rows) are searched.
  * scores: device f32 [nq, k] cosine, descending; out_rows: device i64 [nq, k]
- * = row_base + local row.  Ties: score desc, then row asc.  Slots beyond n_rows
- * get score -inf and row -1.  1 <= k <= RC_TOPK_MAX. */
+ * (global rows, see the row map).  Ties: score desc, then row asc.  Slots beyond
+ * n_rows get score -inf and row -1 (n_rows = 0, an empty shard, is valid in
+ * every mode).  1 <= k <= RC_TOPK_MAX; a larger top_k is RC_ERR_INVALID. */
 int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int k,
                     float *scores, int64_t *out_rows, void *stream);
 
@@ -112,7 +126,8 @@ int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, i
  *   RC_SEARCH_MFMA — batched: query-block x row-tile MFMA GEMM (f16/bf16 index only)
  *                    whose epilogue keeps candidates within a proven error bound
  *                    of the running kth score, exact f32 rescoring of candidates;
- *                    blocks the calling thread once (overflow check);
+ *                    a query whose candidates overflow is re-run through the
+ *                    exact scan ON THE DEVICE (no host synchronisation);
  *   RC_SEARCH_AUTO — MFMA for >= 8 queries on an f16/bf16 index of >= 64k rows.
  * This is the batched form of index.query (retriever/utils.py:62-64) that
  * BASELINE config 4 (1024 queries, top-100) exercises. */
@@ -127,12 +142,44 @@ int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows
  * (seed, row, col), normalised and cast like an upsert. */
 int rc_index_fill_random(rc_index *h, uint64_t seed, int64_t row0, int64_t n, void *stream);
 
-/* Merge nlists sorted top-k lists per query into one (cross-shard merge after
- * the all-gather; no reference counterpart — Pinecone merges server-side).
- * scores/rows: device [nlists, nq, k_in] (each list sorted score desc, row asc,
- * lists ordered by ascending row range); out: device [nq, k]. */
+/* Merge nlists top-k lists per query into one (cross-shard merge after the
+ * all-gather; no reference counterpart — Pinecone merges server-side).
+ * scores/rows: device [nlists, nq, k_in] of (score, global row); rows < 0 are
+ * empty slots; global rows must be < 2^32.  Result ordered score desc, then
+ * row asc — whatever the routing of rows to lists.  out: device [nq, k]. */
 int rc_topk_merge(const float *scores, const int64_t *rows, int nlists, int nq, int k_in, int k,
                   float *out_scores, int64_t *out_rows, void *stream);
+
+/* ------------------------------------------------------------------------
+ * One index over several shards in one process (SURVEY §8(b):
+ * rc_index_create(dim, dtype, capacity_per_gpu, n_gpus)).  Shard s is an
+ * rc_index on devices[s] (devices may repeat: several shards on one GPU);
+ * global row g lives on shard g % n_shards as local row g / n_shards
+ * (round-robin, so every shard fills from the first upsert).  Queries and
+ * results live on devices[0] (the leader); shards search concurrently on their
+ * own streams and their lists are merged on the leader (rc_topk_merge).
+ * Total capacity < 2^32 rows.
+ * ---------------------------------------------------------------------- */
+int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int64_t capacity_per_shard,
+                      rc_sharded **out);
+int rc_sharded_destroy(rc_sharded *h);
+int rc_sharded_info(const rc_sharded *h, int *n_shards, int64_t *capacity_per_shard, int64_t *ld);
+/* Borrowed handle of shard s (persistence, parity tests); owned by h. */
+int rc_sharded_shard(rc_sharded *h, int s, rc_index **out);
+int rc_sharded_grow(rc_sharded *h, int64_t new_capacity_per_shard);
+/* replaces index.upsert — ingesting/main.py:156-158.  vecs: leader-device f32
+ * [n, dim]; rows: HOST i64 [n] global rows.  Synchronous (ordered after work
+ * already queued on `stream`). */
+int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t *rows, void *stream);
+/* replaces index.fetch — retriever/main.py:142.  rows: HOST i64 [n] global rows;
+ * out: HOST f32 [n, dim] (stored = 0: the upserted values; 1: the normalised
+ * stored rows the search scores).  Synchronous. */
+int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, int stored);
+/* replaces index.query — retriever/utils.py:62-64.  queries: leader-device f32
+ * [nq, dim]; n_rows: global rows [0, n_rows) are searched; scores / out_rows:
+ * leader-device [nq, k], identical to one rc_index holding the same rows. */
+int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
+                      int64_t *out_rows, int mode, void *stream);
 
 /* ------------------------------------------------------------------------
  * ViT-MSN image embedding.  Replaces the /embed compute path —
@@ -176,7 +223,7 @@ int rc_embed(rc_model *m, const uint8_t *images, int n, int h, int w,
 int rc_preprocess(rc_model *m, const uint8_t *images, int n, int h, int w, float *pixel_values, void *stream);
 
 /* Encode a batch as `parts` (1..4) concurrent slices on their own HIP streams
- * (default 3; slices below 32 images are merged).  Results are bit-identical
+ * (default 2; slices below 32 images are merged).  Results are bit-identical
  * for every setting: each image's arithmetic is the same.  One slice's memory-
  * bound kernels (LayerNorm, attention) and GEMM store bursts then overlap the
  * other slices' MFMA main loops.  rc_embed still returns ordered on `stream`. */
@@ -211,7 +258,8 @@ int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, con
 int rc_index_timing(rc_index *h, int enable);
 int rc_index_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *bytes);
 /* Same for the batched search's filter GEMM (flops = 2 * query slots * rows * ld per launch);
- * fallbacks = batched calls that re-ran an overflowed query through the exact scan. */
+ * fallbacks = queries re-run through the on-device exact scan since the last
+ * read (candidate overflow; synchronises the device to read the counter). */
 int rc_index_gemm_timing_read(rc_index *h, double *total_ms, int64_t *launches, double *flops, int64_t *fallbacks);
 
 

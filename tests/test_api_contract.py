@@ -188,3 +188,56 @@ def test_embed_gpu_jpeg_path_equals_pil_path(client, test_image_bytes, cuda, mon
     assert r.status_code == 200
     vs = r.json()
     assert len(vs) == 2 and vs[1] == gpu_vec and len(vs[0]) == 768
+
+
+# ------------------------------------------------ ingest / retriever services --
+# reference tests/test_ingesting.py:41-55 and tests/test_retriever.py:40-59 (the
+# success paths need the GPU and run under -m gpu in test_ingest_gpu.py)
+@pytest.fixture(scope="module")
+def ingest_client():
+    return TestClient(import_pkg("ingesting.main").app)
+
+
+@pytest.fixture(scope="module")
+def retriever_client():
+    return TestClient(import_pkg("retriever.main").app)
+
+
+def test_ingest_health_and_root(ingest_client):
+    assert ingest_client.get("/healthz").json() == {"status": "healthy"}
+    assert ingest_client.get("/").json() == {"message": "Welcome to the Image Ingestion API. Visit /docs to test."}
+
+
+def test_push_no_file(ingest_client):
+    assert ingest_client.post("/push_image").status_code == 422
+    assert ingest_client.post("/push_images").status_code == 422
+
+
+def test_push_bad_extension(ingest_client, test_image_bytes):
+    r = ingest_client.post("/push_image", files={"file": ("a.gif", test_image_bytes, "image/gif")})
+    assert r.status_code == 400 and r.json()["detail"] == "Only .jpg/.jpeg/.png allowed"
+    r = ingest_client.post("/push_images", files=[("files", ("a.jpeg", test_image_bytes, "image/jpeg")),
+                                                  ("files", ("b.txt", b"x", "text/plain"))])
+    assert r.status_code == 400 and r.json()["detail"] == "Only .jpg/.jpeg/.png allowed"
+
+
+def test_push_invalid_image(ingest_client):
+    r = ingest_client.post("/push_image", files={"file": ("a.jpg", b"This is not an image.", "image/jpeg")})
+    assert r.status_code == 400 and r.json()["detail"] == "Invalid image file"
+
+
+def test_retriever_health_and_root(retriever_client):
+    assert retriever_client.get("/healthz").json() == {"status": "OK!"}
+    assert retriever_client.get("/").json() == {"message": "Welcome to the Image Retriever API. Visit /docs to test."}
+
+
+def test_search_no_file_and_invalid(retriever_client):
+    assert retriever_client.post("/search_image").status_code == 422
+    r = retriever_client.post("/search_image", files={"file": ("a.jpg", b"This is not an image.", "image/jpeg")})
+    assert r.status_code == 400 and r.json()["detail"] == "Uploaded file is not a valid image."
+
+
+def test_index_devices_spec(monkeypatch):
+    utils = import_pkg("ingesting.utils")
+    assert utils.index_devices("0,2,4") == [0, 2, 4]
+    assert utils.index_devices("", shards=3) == [None, None, None]

@@ -124,25 +124,77 @@ def test_mfma_f32_index_rejected(idxmod, cuda):
 
 
 def test_config4_shard_full_size_properties(idxmod, cuda):
-    """Config 4 per-GPU shape at a reduced row count (20M x 512 fp16, 1024 queries, top-100):
-    planted exact hits come back first at score 1, results are sorted, and a sample
-    of queries matches the exact scan bit for bit."""
+    """Config 4 at its real per-GPU workload: one 125M x 512 fp16 shard (1B rows over 8 GPUs),
+    1024 queries, top-100, batched MFMA path.  Size-independent properties: planted exact hits
+    come back first at score ||x̂||; results sorted; a query sample is bit-identical to the exact
+    scan; and on a random row sample the float64 oracle finds no row that beats the returned
+    kth score without being returned (with the returned rows' scores matching the oracle)."""
     import torch
 
-    n, dim, nq, k = 20_000_000, 512, 1024, 100
+    n, dim, nq, k = 125_000_000, 512, 1024, 100
     dev = idxmod.DeviceIndex(dim, dtype="float16", capacity=n, device=cuda)
     dev.fill_random(4, 0, n)
     g = torch.Generator(device="cuda").manual_seed(5)
     Q = torch.randn((nq, dim), device="cuda", generator=g)
-    planted = torch.tensor([0, 7, 19_999_999, 12_345_678], dtype=torch.int64)
+    planted = torch.tensor([0, 7, 124_999_999, 62_345_678], dtype=torch.int64)
     Q[: len(planted)] = dev.stored_rows(planted)
     s, r = dev.search(Q, k, n, mode="mfma")
     assert r[: len(planted), 0].cpu().tolist() == planted.tolist()
-    # a query equal to a stored row x̂ scores x̂·x̂/||x̂|| = ||x̂|| (≈1 up to the f16 rounding of the row)
     self_score = Q[: len(planted)].double().norm(dim=1).cpu()
     assert torch.allclose(s[: len(planted), 0].cpu().double(), self_score, atol=1e-5)
-    assert (s[:, :-1] >= s[:, 1:]).all() and (r >= 0).all()
+    assert (s[:, :-1] >= s[:, 1:]).all() and (r >= 0).all() and (r < n).all()
     sel = torch.tensor([0, 5, 511, 512, 1023])
     s2, r2 = dev.search(Q[sel], k, n, mode="scan")
     assert torch.equal(r[sel.cuda()], r2) and torch.equal(s[sel.cuda()], s2)
+    # row-sample oracle check (float64 numpy on host over 262144 random stored rows)
+    rng = np.random.default_rng(0)
+    sample = np.unique(rng.integers(0, n, 1 << 18))
+    Xs = dev.stored_rows(torch.from_numpy(sample)).cpu().numpy().astype(np.float64)
+    qs = [1, 100, 700, 1023]
+    Qn = Q[qs].double().cpu().numpy()
+    Qn /= np.linalg.norm(Qn, axis=1, keepdims=True)
+    S = Xs @ Qn.T
+    s_np, r_np = s.cpu().numpy(), r.cpu().numpy()
+    for j, qi in enumerate(qs):
+        kth = float(s_np[qi, -1])
+        returned = set(r_np[qi].tolist())
+        beat = sample[S[:, j] > kth + 1e-5]
+        assert set(beat.tolist()) <= returned, (qi, beat)
+        Xr = dev.stored_rows(torch.from_numpy(r_np[qi])).cpu().numpy().astype(np.float64)
+        assert np.allclose(Xr @ Qn[j], s_np[qi], atol=1e-5, rtol=0)
     dev.close()
+
+
+def test_recall_vs_unquantised_fp32_oracle(idxmod, cuda):
+    """north_star: "recall@k against the fp32 oracle".  The same 1M x 512 rows are held once in
+    f32 (the unquantised rows; exact against the float64 oracle, test_index_gpu.py) and once in
+    f16.  recall@10 of the f16 index against the f32 top-10 is measured and reported; every
+    row the f16 index misses must be explained by storage rounding: its f32 score lies within
+    2 x 2^-11 (the f16 rounding bound of a unit-row score, twice) of the f32 score of the
+    f16 result's 10th row."""
+    import torch
+
+    n, dim, nq, k = 1_000_000, 512, 200, 10
+    f32 = idxmod.DeviceIndex(dim, dtype="float32", capacity=n, device=cuda)
+    f16 = idxmod.DeviceIndex(dim, dtype="float16", capacity=n, device=cuda)
+    f32.fill_random(2, 0, n)
+    f16.fill_random(2, 0, n)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    Q = torch.randn((nq, dim), device="cuda", generator=g)
+    s32, r32 = f32.search(Q, k, n, mode="scan")
+    s16, r16 = f16.search(Q, k, n, mode="mfma")
+    r32c, r16c = r32.cpu().numpy(), r16.cpu().numpy()
+    hits = sum(len(set(a) & set(b)) for a, b in zip(r32c, r16c))
+    recall = hits / (nq * k)
+    print(f"recall@{k} of the f16 index vs the unquantised f32 oracle: {recall:.5f} over {nq} queries")
+    qn = Q.double() / Q.double().norm(dim=1, keepdim=True)
+    for qi in range(nq):
+        missed = set(r32c[qi]) - set(r16c[qi])
+        if not missed:
+            continue
+        x = f32.stored_rows(torch.tensor(sorted(missed) + [int(r16c[qi, -1])])).double()
+        sc = (x @ qn[qi]).cpu().numpy()
+        assert np.all(sc[:-1] - sc[-1] <= 2 * 2.0 ** -11), (qi, sc)
+    assert recall >= 0.98
+    f32.close()
+    f16.close()

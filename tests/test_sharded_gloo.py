@@ -1,9 +1,11 @@
 """World-size-2 (and 4) gloo test of the sharded search orchestration on CPU.
 
-The per-shard scan and the device merge are HIP kernels (covered by -m gpu tests);
-here they are replaced by the CPU oracle so the distributed plumbing — row
-ownership, upsert routing, all_gather of (score, global row) lists, merge order
-across ranks — is checked end to end with real torch.distributed collectives.
+The per-shard scan and the device merge are HIP kernels (covered by -m gpu tests,
+including a world-2 run over real HIP shards in test_sharded_gpu.py); here they
+are replaced by the CPU oracle so the distributed plumbing — round-robin row
+ownership, upsert routing, empty shards, all_gather of (score, global row) lists,
+merge order across ranks — is checked end to end with real torch.distributed
+collectives.
 """
 import os
 import socket
@@ -18,11 +20,13 @@ from conftest import REPO, import_pkg
 
 
 class OracleShard:
-    """CPU stand-in for DeviceIndex: stores normalised rows, exact float64 top-k."""
+    """CPU stand-in for DeviceIndex: stores normalised rows, exact float64 top-k,
+    returns global rows row_base + local * row_stride; an empty shard answers -inf / -1."""
 
-    def __init__(self, dim, capacity, row_base):
+    def __init__(self, dim, capacity, row_base, row_stride):
         self.X = np.zeros((capacity, dim))
         self.row_base = row_base
+        self.row_stride = row_stride
 
     def upsert_rows(self, vecs, rows):
         v = vecs.double().numpy()
@@ -31,29 +35,43 @@ class OracleShard:
     def search(self, queries, k, n_rows):
         from oracle.cosine_topk import cosine_topk
 
+        nq = queries.shape[0]
+        if n_rows == 0:
+            return torch.full((nq, k), -float("inf")), torch.full((nq, k), -1, dtype=torch.int64)
         r, s = cosine_topk(self.X[:n_rows], queries.double().numpy(), k, rows_normalized=True)
+        r = r * self.row_stride + self.row_base
         pad = k - r.shape[1]
         if pad > 0:
-            r = np.pad(r, ((0, 0), (0, pad)), constant_values=-1 - self.row_base)
+            r = np.pad(r, ((0, 0), (0, pad)), constant_values=-1)
             s = np.pad(s, ((0, 0), (0, pad)), constant_values=-np.inf)
-        return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(r + self.row_base)
+        return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(r)
 
 
 def cpu_merge(gs, gr, k):
-    """Restates rc_topk_merge on CPU: key (score desc, list position asc), invalid rows dropped."""
+    """Restates rc_topk_merge on CPU: key (score desc, global row asc), empty slots (row < 0) dropped."""
     W, nq, kin = gs.shape
     out_s = torch.full((nq, k), -float("inf"))
     out_r = torch.full((nq, k), -1, dtype=torch.int64)
     for q in range(nq):
-        cand = [(-float(gs[w, q, t]), w * kin + t) for w in range(W) for t in range(kin) if gr[w, q, t] >= 0]
-        cand.sort()
-        for j, (negs, pos) in enumerate(cand[:k]):
+        cand = sorted((-float(gs[w, q, t]), int(gr[w, q, t])) for w in range(W) for t in range(kin) if gr[w, q, t] >= 0)
+        for j, (negs, row) in enumerate(cand[:k]):
             out_s[q, j] = -negs
-            out_r[q, j] = gr[pos // kin, q, pos % kin]
+            out_r[q, j] = row
     return out_s, out_r
 
 
-def _worker(rank, world, port, result_q):
+def _data(world, n):
+    cap, dim = 300, 64
+    rng = np.random.default_rng(0)  # same data on every rank
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    Q = rng.standard_normal((3, dim)).astype(np.float32)
+    if n > cap + 11:
+        X[5] = X[cap + 11]  # an exact tie across shards (5 % W != (cap + 11) % W for W = 2, 4)
+        Q[0] = X[cap + 11]
+    return X, Q
+
+
+def _worker(rank, world, n, port, result_q):
     import sys
 
     sys.path.insert(0, REPO)
@@ -63,16 +81,11 @@ def _worker(rank, world, port, result_q):
         sharded = import_pkg("sharded")
         cap, dim, k = 300, 64, 7
         idx = sharded.ShardedIndex(dim, capacity_per_rank=cap,
-                                   backend_factory=lambda: OracleShard(dim, cap, rank * cap), merge_fn=cpu_merge)
-        rng = np.random.default_rng(0)  # same data on every rank
-        n = cap * world - 50
-        X = rng.standard_normal((n, dim)).astype(np.float32)
-        X[5] = X[cap + 11]  # cross-shard exact tie
-        Q = rng.standard_normal((3, dim)).astype(np.float32)
-        Q[0] = X[cap + 11]
+                                   backend_factory=lambda: OracleShard(dim, cap, rank, world), merge_fn=cpu_merge)
+        X, Q = _data(world, n)
         owned = idx.upsert_rows(torch.from_numpy(X), torch.arange(n))
         s, r = idx.search(torch.from_numpy(Q), k)
-        result_q.put((rank, owned, s.numpy(), r.numpy()))
+        result_q.put((rank, owned, idx.n_local, s.numpy(), r.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -83,30 +96,31 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_search_equals_global_oracle(world):
+@pytest.mark.parametrize("world,n", [(2, 550), (4, 1150), (4, 2), (2, 1)])
+def test_sharded_search_equals_global_oracle(world, n):
+    """Round-robin shards + all_gather + merge == one exact index; n < world leaves ranks with
+    EMPTY shards, which must still answer (-inf, -1) lists and reach the collective."""
     from oracle.cosine_topk import cosine_topk
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, n, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    cap, dim, k = 300, 64, 7
-    rng = np.random.default_rng(0)
-    n = cap * world - 50
-    X = rng.standard_normal((n, dim)).astype(np.float32)
-    X[5] = X[cap + 11]
-    Q = rng.standard_normal((3, dim)).astype(np.float32)
-    Q[0] = X[cap + 11]
+    cap, k = 300, 7
+    X, Q = _data(world, n)
     ref_r, ref_s = cosine_topk(X, Q, k)
+    kk = min(k, n)
     assert sum(o[1] for o in outs) == n  # every row written by exactly one owner
-    for rank, owned, s, r in outs:
-        assert np.array_equal(r, ref_r), (rank, r, ref_r)  # identical on every rank
-        assert np.allclose(s, ref_s, atol=1e-6)
-    assert outs[0][3][0, :2].tolist() == [5, cap + 11]  # tie → lower global row first
+    for rank, owned, n_local, s, r in outs:
+        assert owned == n_local == len(range(rank, n, world))  # round-robin: rank r owns rows r, r+W, ...
+        assert np.array_equal(r[:, :kk], ref_r), (rank, r, ref_r)  # identical on every rank
+        assert np.allclose(s[:, :kk], ref_s, atol=1e-6)
+        assert np.all(r[:, kk:] == -1) and np.all(np.isneginf(s[:, kk:]))
+    if n > cap + 11:
+        assert outs[0][4][0, :2].tolist() == [5, cap + 11]  # tie → lower global row first
