@@ -227,6 +227,8 @@ def main():
     ap.add_argument("--parts", type=int, default=2, help="concurrent batch slices per GPU (rc_model_set_parts)")
     ap.add_argument("--full-last-layer", action="store_true",
                     help="run the last encoder layer on every row (default: CLS rows only, rc_model_set_last_layer)")
+    ap.add_argument("--no-ln-fold", action="store_true",
+                    help="run the standalone LayerNorm kernel instead of folding LN into QKV / fc1 (A/B)")
     ap.add_argument("--ingest-images", type=int, default=16384, help="config 5 sample per GPU (0 = skip)")
     ap.add_argument("--jpeg-images", type=int, default=256, help="JPEG decode sample per GPU (0 = skip)")
     ap.add_argument("--no-search", action="store_true")
@@ -294,6 +296,7 @@ def main():
     model = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=local, max_batch=B)
     model.set_parts(args.parts)
     model.set_last_layer(not args.full_last_layer)
+    model.set_ln_fold(not args.no_ln_fold)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     images = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
     raw = torch.empty((B, 768), dtype=torch.float32, device=dev)
@@ -477,6 +480,8 @@ def main():
             "concurrent_avg_launch_ms": fc1c_ms / max(fc1c_n, 1),
         },
         "embed_parts": args.parts,
+        "layernorm": "standalone kernel" if args.no_ln_fold else
+        "folded into QKV / fc1 epilogues (producers emit bf16(x) + per-tile mean/M2)",
         "last_layer": "full" if args.full_last_layer else
         "CLS rows only after QKV (the rows /embed returns, embedding/main.py:113)",
         "gflop_per_image_executed": gflop,

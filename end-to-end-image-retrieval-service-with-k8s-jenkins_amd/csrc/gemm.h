@@ -63,116 +63,6 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
     return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
-template <int EPI, int BM>
-__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
-    constexpr int BN = G2_BN, BK = G2_BK;
-    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-    constexpr int MI = BM / 32, NI = 4;
-    constexpr int A_PIECES = A_BYTES / 1024, B_PIECES = B_BYTES / 1024;  // 1-KB LDS-DMA pieces
-    constexpr int PIECES_PER_WAVE = (A_PIECES + B_PIECES) / 8;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int g = lane >> 4, li = lane & 15;
-
-    const int ntn = a.N / BN;
-    const int nwg = gridDim.x, orig = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    const int tm = tile / ntn, tn = tile % ntn;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int K = a.K;
-    const uint16_t *Ag = a.A + (int64_t)m0 * K;
-    const uint16_t *Wg = a.W + (int64_t)n0 * K;
-
-    auto stage = [&](int buf, int k0) {
-        uint8_t *base = smem + buf * STAGE;
-#pragma unroll
-        for (int i = 0; i < PIECES_PER_WAVE; ++i) {
-            const int piece = wave + 8 * i;  // wave-uniform
-            const int r = (piece < A_PIECES ? piece : piece - A_PIECES) * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            const uint16_t *src = piece < A_PIECES ? Ag + (int64_t)r * K : Wg + (int64_t)r * K;
-            __builtin_amdgcn_global_load_lds((const void *)(src + k0 + c * 8), (lds_void_t *)(base + piece * 1024), 16, 0, 0);
-        }
-    };
-
-    f32x4 acc[MI][NI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = K / BK;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-        const uint8_t *As = smem + cur * STAGE;
-        const uint8_t *Ws = As + A_BYTES;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int c = s * 4 + g;
-            bf16x8 wf[NI], af[MI];
-#pragma unroll
-            for (int ni = 0; ni < NI; ++ni) {
-                const int r = wn * 64 + ni * 16 + li;
-                wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int mi = 0; mi < MI; ++mi) {
-                const int r = wm * (BM / 2) + mi * 16 + li;
-                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-                for (int ni = 0; ni < NI; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-
-    // epilogue: acc[mi][ni][j] = C[m0 + wm*BM/2 + mi*16 + li][n0 + wn*64 + ni*16 + 4g + j]
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-        const int col = n0 + wn * 64 + ni * 16 + 4 * g;
-        const float4 bias = *reinterpret_cast<const float4 *>(a.bias + col);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) {
-            const int row = m0 + wm * (BM / 2) + mi * 16 + li;
-            if (row >= a.M) continue;
-            float v0 = acc[mi][ni][0] + bias.x, v1 = acc[mi][ni][1] + bias.y;
-            float v2 = acc[mi][ni][2] + bias.z, v3 = acc[mi][ni][3] + bias.w;
-            if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-                if constexpr (EPI == EPI_GELU_BF16) {
-                    v0 = gelu_fast(v0);
-                    v1 = gelu_fast(v1);
-                    v2 = gelu_fast(v2);
-                    v3 = gelu_fast(v3);
-                }
-                *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * a.N + col) =
-                    make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-            } else if constexpr (EPI == EPI_RESID_F32) {
-                float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + col);
-                const float4 r = *o;
-                *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
-            } else {  // EPI_PATCH_F32
-                const int np = a.tokens - 1;
-                const int img = row / np, p = row - img * np;
-                const float4 ps = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + col);
-                *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + p) * a.N + col) =
-                    make_float4(v0 + ps.x, v1 + ps.y, v2 + ps.z, v3 + ps.w);
-            }
-        }
-    }
-}
-
 // ----------------------------------------------------------- ping-pong GEMM --
 // 256x256x64 tile, 8 waves in two groups: G0 = waves 0-3 (output rows 0-127),
 // G1 = waves 4-7 (rows 128-255); wave w and w+4 share a SIMD.  Each wave owns
@@ -194,7 +84,10 @@ template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     constexpr int BM = 256, BN = 256, BK = 64;
     constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;  // A tile then W tile, 32 KB each
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+    // LayerNorm-fold consumers keep the tile rows' (rstd, -rstd*mu) behind the ring (one
+    // __shared__ array: a second one would make hipcc drain the LDS-DMA queue every K-step)
+    constexpr int LN_LDS = epi_ln(EPI) ? BM * 8 : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + LN_LDS];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -260,13 +153,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 
     const int nk = K / BK;
-    // K order: with grouped tiles, the tile one XCD round later (32 tiles on)
-    // reuses this tile's A rows at column tile tn + 4; sweeping K the other way
-    // there starts on the K-slices still in L2 (krev = 4; ascending otherwise)
-    const bool rev = a.krev > 0 && ((tn / a.krev) & 1);
-    auto kofs = [&](int kt) { return (rev ? nk - 1 - kt : kt) * BK; };
+    auto kofs = [](int kt) { return kt * BK; };
     stage4(0, kofs(0), 0);
     stage4(0, kofs(0), 4);
+    if constexpr (epi_ln(EPI)) {  // LayerNorm fold: this tile's row scales, under the first DMA
+        if (tid < BM)
+            *reinterpret_cast<float2 *>(smem + 2 * STAGE + tid * 8) =
+                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * (2 * LN_TILES), a.ln_eps);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     if (grp == 1) bar();  // stagger: G1 one segment behind
@@ -335,24 +229,47 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 
     // epilogue: acc[mq][nq][mi][ni][j] = C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
-    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+    if constexpr (epi_bf16_out(EPI)) {
         // Stage the 256x256 bf16 tile in LDS (512-B rows, 16-B chunk XOR (row & 31)),
         // then every wave stores whole 512-B row segments with 16-B stores.
         // (The K loop's final barrier retired every ds_read and DMA: LDS is free.)
+        float2 lrs[2][4];  // LayerNorm fold: (rstd, -rstd*mu) of this lane's 8 rows
+        if constexpr (epi_ln(EPI)) {
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    lrs[mq][mi] = *reinterpret_cast<const float2 *>(smem + 2 * STAGE + (grp * 128 + mq * 64 + mi * 16 + li) * 8);
+        }
 #pragma unroll
         for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
                 const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;  // tile-local column
-                const float4 bias = biasr[nq][ni];
+                float4 bias, lc;
+                if constexpr (epi_ln(EPI)) {
+                    bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+                    lc = *reinterpret_cast<const float4 *>(a.ln_c + n0 + cl);
+                } else {
+                    bias = biasr[nq][ni];
+                }
 #pragma unroll
                 for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
                     for (int mi = 0; mi < 4; ++mi) {
                         const int rl = grp * 128 + mq * 64 + mi * 16 + li;
                         const f32x4 v4 = acc[mq][nq][mi][ni];
-                        float v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
-                        if constexpr (EPI == EPI_GELU_BF16 && !(ABL & 16)) {
+                        float v0, v1, v2, v3;
+                        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′
+                            const float2 r = lrs[mq][mi];
+                            v0 = fmaf(r.x, v4[0], fmaf(r.y, lc.x, bias.x));
+                            v1 = fmaf(r.x, v4[1], fmaf(r.y, lc.y, bias.y));
+                            v2 = fmaf(r.x, v4[2], fmaf(r.y, lc.z, bias.z));
+                            v3 = fmaf(r.x, v4[3], fmaf(r.y, lc.w, bias.w));
+                        } else {
+                            v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
+                        }
+                        if constexpr (epi_gelu(EPI) && !(ABL & 16)) {
                             const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
                             v0 = lo.x;
                             v1 = lo.y;
@@ -421,18 +338,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
             const int id = it * 512 + tid;
-            const int rl = id >> 6, ch = id & 63;
+            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
             const int row = m0 + h * 128 + rl;
             const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
             const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
             if (row < a.M) {
-                if constexpr (EPI == EPI_RESID_F32) {
-                    *reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + n0 + ch * 4) = o;
-                } else {
+                int64_t orow = row;
+                if constexpr (EPI == EPI_PATCH_F32) {
                     const int np = a.tokens - 1;
                     const int img = row / np, p = row - img * np;
-                    *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + p) * a.N + n0 + ch * 4) = o;
+                    orow = (int64_t)img * a.tokens + 1 + p;
                 }
+                *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o;
+                if (a.ln_x != nullptr)  // LayerNorm fold producer
+                    ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
             }
         }
         if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
@@ -625,549 +544,26 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
             const int id = it * 256 + tid;
-            const int rl = id >> 6, ch = id & 63;
+            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
             const int row = m0 + h * 64 + rl;
             const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
             const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
             if (row < a.M) {
-                if constexpr (EPI == EPI_RESID_F32) {
-                    *reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + n0 + ch * 4) = o;
-                } else {
+                int64_t orow = row;
+                if constexpr (EPI == EPI_PATCH_F32) {
                     const int np = a.tokens - 1;
                     const int img = row / np, p = row - img * np;
-                    *reinterpret_cast<float4 *>(a.out_f32 + ((int64_t)img * a.tokens + 1 + p) * a.N + n0 + ch * 4) = o;
+                    orow = (int64_t)img * a.tokens + 1 + p;
                 }
+                *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o;
+                if (a.ln_x != nullptr)  // LayerNorm fold producer
+                    ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
             }
         }
         if (h == 0) __syncthreads();  // the second half overwrites the staging rows
     }
 }
 
-
-// ------------------------------------------------------ persistent GEMM ----
-// The ping-pong main loop of gemm_pp_kernel (256x256x64 tiles, G1 one segment
-// behind G0) run persistently: one 512-thread block per CU, with its (tile,
-// K-tile) steps flattened into one sequence so the next tile's first K-tile
-// streams in under the current tile's last MFMAs and no block pays a prologue
-// per tile.  Block slots come from the XCD-aware remap (consecutive slots share
-// an XCD and therefore its L2).
-//   SK = false: slot s owns whole tiles s, s + G, s + 2G, ...
-//   SK = true (Stream-K): the ntiles·nk steps are cut into G equal contiguous
-//     ranges, so every block does the same MFMA work and there is no partial
-//     last round (fc2/O-proj: 591 tiles on 256 CUs would otherwise run 3
-//     rounds for 2.31 rounds of work).  A tile cut by a range boundary is
-//     finished by its OWNER, the block holding its K-tile 0, at the END of the
-//     owner's range; every other block that holds part of it does that part
-//     FIRST in its range, stores the f32 partial accumulators (wave-linear,
-//     16-B write-through sc1 stores), drains and raises a per-wave flag
-//     (= launch epoch).  The owner's waves each poll their counterpart's flag
-//     (bounded spin), acquire at agent scope, and add the partials before the
-//     epilogue.  No block waits before publishing, and all G <= #CU blocks are
-//     resident (128 KB LDS = one block per CU), so the hand-off cannot deadlock.
-// The epilogue works from registers: bias / GELU / residual / position are
-// applied per lane; bf16 results are paired across 16-lane rows with
-// v_permlane16_swap so every lane stores 16 B (8 consecutive columns), one
-// store instruction per 64-B segment of 16 rows; f32 results are 16-B stores.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-template <int EPI, bool SK>
-__global__ __launch_bounds__(512, 1) void gemm_persist_kernel(GemmArgs a) {
-    constexpr int BM = 256, BN = 256, BK = 64;
-    constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    const int g = lane >> 4, li = lane & 15;
-
-    const int ntn = a.N / BN;
-    const int ntiles = ((a.M + BM - 1) / BM) * ntn;
-    const int G = gridDim.x, orig = blockIdx.x;
-    const int q8 = G / 8, r8 = G % 8, xcd = orig % 8;
-    const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    const int K = a.K;
-    const int nk = K / BK;
-    const int64_t total = (int64_t)ntiles * nk;
-    int nsteps, ctile, ck;
-    if constexpr (SK) {
-        const int s0 = (int)((int64_t)slot * total / G), s1 = (int)((int64_t)(slot + 1) * total / G);
-        nsteps = s1 - s0;
-        ctile = s0 / nk;
-        ck = s0 - ctile * nk;
-    } else {
-        nsteps = slot < ntiles ? ((ntiles - slot + G - 1) / G) * nk : 0;
-        ctile = slot;
-        ck = 0;
-    }
-    if (nsteps <= 0) return;  // block-uniform, before any barrier
-    constexpr int TSTEP_SK = 1;
-    const int tstep = SK ? TSTEP_SK : G;
-
-    // 64 pieces of 1 KB per K-tile (A: 0-31, W: 32-63); wave w owns pieces w + 8 i.
-    auto stage4 = [&](int buf, int tile, int k0, int i0) {
-        uint8_t *base = smem + buf * STAGE;
-        const int tm = tile / ntn, tn = tile - tm * ntn;
-        const uint16_t *Ag = a.A + (int64_t)tm * BM * K;
-        const uint16_t *Wg = a.W + (int64_t)tn * BN * K;
-#pragma unroll
-        for (int i = i0; i < i0 + 4; ++i) {
-            const int piece = wave + 8 * i;
-            const bool is_a = i < 4;
-            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
-        }
-    };
-    auto bar = [] {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-
-    f32x4 acc[2][2][4][2];
-    auto zero_acc = [&] {
-#pragma unroll
-        for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-            for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-                for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                    for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    zero_acc();
-
-    stage4(0, ctile, ck * BK, 0);
-    stage4(0, ctile, ck * BK, 4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (grp == 1) bar();  // stagger: G1 one segment behind
-
-    int ltile = ctile, lk = ck + 1;  // load cursor: the step after (ctile, ck)
-    if (lk == nk) { lk = 0; ltile += tstep; }
-    int kb = ck;                     // K-tile at which the current segment started
-    bf16x8 af[4][2], wf[2][2];
-    for (int step = 0; step < nsteps; ++step) {
-        const int cur = step & 1;
-        const uint8_t *As = smem + cur * STAGE;
-        const uint8_t *Ws = As + A_BYTES;
-        const bool more = step + 1 < nsteps;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int mq = p >> 1;
-            const int nq = (p == 1 || p == 2);
-            if (p == 0 || p == 2) {
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
-                        const int c = s * 4 + g;
-                        af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                    }
-            }
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
-                    const int c = s * 4 + g;
-                    wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                }
-            if (more && p < 2) stage4(cur ^ 1, ltile, lk * BK, p * 4);
-            if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            bar();
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < 2; ++ni)
-                        acc[mq][nq][mi][ni] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], acc[mq][nq][mi][ni], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            bar();
-        }
-        if (++lk == nk) { lk = 0; ltile += tstep; }
-        const bool tile_done = ck == nk - 1;
-        if (!tile_done && !(SK && step == nsteps - 1)) {
-            ++ck;
-            continue;
-        }
-
-        if constexpr (SK) {
-            f32x4 *part = reinterpret_cast<f32x4 *>(a.sk_ws);
-            if (kb > 0 && (a.sk_debug & 1)) {
-                zero_acc();
-                kb = 0;
-                ck = 0;
-                ctile += 1;
-                continue;
-            }
-            if (kb > 0) {
-                // ---- contributor: publish this range's share of tile ctile to its owner
-                // write-through (sc1) 16-B stores: visible at agent scope once drained,
-                // so no release fence (an agent release would write back this XCD's L2)
-                const __amdgpu_buffer_rsrc_t rs =
-                    __builtin_amdgcn_make_buffer_rsrc(part + (int64_t)slot * 32 * 512, (short)0, 32 * 512 * 16, 0x00020000);
-#pragma unroll
-                for (int i = 0; i < 32; ++i) {
-                    const f32x4 v = acc[i >> 4][(i >> 3) & 1][(i >> 1) & 3][i & 1];
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (i * 512 + tid) * 16, 0, 16);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store(a.sk_flags + slot * 8 + wave, a.sk_epoch, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                zero_acc();
-                kb = 0;
-                ck = 0;
-                ctile += 1;
-                continue;
-            }
-            if (!tile_done && !(a.sk_debug & 2)) {
-                // ---- owner of a cut tile: add every later range's share
-                const int64_t tile_end = (int64_t)(ctile + 1) * nk;
-                for (int w2 = slot + 1; w2 < G && (int64_t)w2 * total / G < tile_end; ++w2) {
-                    const uint32_t *flag = a.sk_flags + w2 * 8 + wave;
-                    int spins = 0;
-                    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.sk_epoch) {
-                        if (++spins > (1 << 24)) {
-                            if (lane == 0) atomicOr(a.sk_err, 1u);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int i = 0; i < 32; ++i)
-                        acc[i >> 4][(i >> 3) & 1][(i >> 1) & 3][i & 1] += part[((int64_t)w2 * 32 + i) * 512 + tid];
-                }
-            }
-        }
-
-        // ---- epilogue of tile ctile: acc[mq][nq][mi][ni][j] =
-        //      C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
-        const int tm = ctile / ntn, tn = ctile - tm * ntn;
-        const int m0 = tm * BM, n0 = tn * BN;
-        float4 bias[2][2];
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-                bias[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
-#pragma unroll
-        for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
-                if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-#pragma unroll
-                    for (int nq = 0; nq < 2; ++nq) {
-                        uint32_t u[2][2];
-#pragma unroll
-                        for (int ni = 0; ni < 2; ++ni) {
-                            const f32x4 v4 = acc[mq][nq][mi][ni];
-                            const float4 b4 = bias[nq][ni];
-                            f32x2 lo = f32x2{v4[0] + b4.x, v4[1] + b4.y}, hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
-                            if constexpr (EPI == EPI_GELU_BF16) {
-                                lo = gelu_fast2(lo);
-                                hi = gelu_fast2(hi);
-                            }
-                            u[ni][0] = pack_bf16x2(lo.x, lo.y);
-                            u[ni][1] = pack_bf16x2(hi.x, hi.y);
-                        }
-                        // rows of 16 lanes (g): odd rows of u[0] <-> even rows of u[1]
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
-                            u[0][h] = r2[0];
-                            u[1][h] = r2[1];
-                        }
-                        const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
-                        if (row < a.M)
-                            *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * a.N + col) =
-                                make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
-                    }
-                } else if (row < a.M) {
-                    float4 add[2][2];
-                    int64_t dst;
-                    if constexpr (EPI == EPI_RESID_F32) {
-                        dst = (int64_t)row * a.N;
-#pragma unroll
-                        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                            for (int ni = 0; ni < 2; ++ni)
-                                add[nq][ni] = *reinterpret_cast<const float4 *>(a.out_f32 + dst + n0 + wc * 64 + nq * 32 +
-                                                                                ni * 16 + 4 * g);
-                    } else {  // EPI_PATCH_F32
-                        const int np = a.tokens - 1;
-                        const int img = row / np, pp = row - img * np;
-                        dst = ((int64_t)img * a.tokens + 1 + pp) * a.N;
-#pragma unroll
-                        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                            for (int ni = 0; ni < 2; ++ni)
-                                add[nq][ni] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + pp) * a.N + n0 +
-                                                                                wc * 64 + nq * 32 + ni * 16 + 4 * g);
-                    }
-#pragma unroll
-                    for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                        for (int ni = 0; ni < 2; ++ni) {
-                            const f32x4 v4 = acc[mq][nq][mi][ni];
-                            const float4 b4 = bias[nq][ni], r4 = add[nq][ni];
-                            *reinterpret_cast<float4 *>(a.out_f32 + dst + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g) =
-                                make_float4(r4.x + (v4[0] + b4.x), r4.y + (v4[1] + b4.y), r4.z + (v4[2] + b4.z),
-                                            r4.w + (v4[3] + b4.w));
-                        }
-                }
-            }
-        zero_acc();
-        kb = 0;
-        ck = 0;
-        ctile += tstep;
-    }
-    if (grp == 0) bar();  // balance the stagger barrier
-}
-
-// ------------------------------------------------- deferred-store GEMM ----
-// gemm_persist_kernel's loop for the bf16-output epilogues (QKV, fc1+GELU), with
-// the tile's stores taken off the critical path.  On gfx950 stores and LDS-DMA
-// loads share one in-order vmcnt, so a store burst at a tile boundary makes the
-// next K-tile's DMA wait behind it (every CU reaches its tile boundary at about
-// the same time: 256 x 128 KB).  Here the epilogue only computes (bias, GELU,
-// bf16 pack, permlane16 pairing) into 64 VGPRs; the 16 16-B stores are issued in
-// the NEXT tile's first K-step, 4 per phase, each group AFTER that phase's DMA
-// issue, and the phase-3 wait is vmcnt(12): it retires both DMA halves (older)
-// and the first 4 stores while the youngest 12 drain under the next phases'
-// MFMAs.  The first K-step's MFMAs take a zero C operand, so the accumulators
-// are dead between the epilogue and the next tile and share registers with the
-// pending stores.  Stores go through a buffer descriptor bounded at the tile's
-// valid rows: rows >= M are dropped by the hardware, so every wave always
-// issues exactly 16 stores and the counted wait stays exact.
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_ds_kernel(GemmArgs a) {
-    static_assert(EPI == EPI_BF16 || EPI == EPI_GELU_BF16, "bf16-output epilogues only");
-    constexpr int BM = 256, BN = 256, BK = 64;
-    constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    const int g = lane >> 4, li = lane & 15;
-
-    const int N = a.N, K = a.K;
-    const int ntn = N / BN;
-    const int ntiles = ((a.M + BM - 1) / BM) * ntn;
-    const int G = gridDim.x, orig = blockIdx.x;
-    const int q8 = G / 8, r8 = G % 8, xcd = orig % 8;
-    const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    if (slot >= ntiles) return;
-    const int nmine = (ntiles - slot + G - 1) / G;
-    const int nk = K / BK;
-    const int nsteps = nmine * nk;
-
-    auto stage4 = [&](int buf, int tile, int k0, int i0) {
-        uint8_t *base = smem + buf * STAGE;
-        const int tm = tile / ntn, tn = tile - tm * ntn;
-        const uint16_t *Ag = a.A + (int64_t)tm * BM * K;
-        const uint16_t *Wg = a.W + (int64_t)tn * BN * K;
-#pragma unroll
-        for (int i = i0; i < i0 + 4; ++i) {
-            const int piece = wave + 8 * i;
-            const bool is_a = i < 4;
-            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
-        }
-    };
-    auto bar = [] {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-
-    f32x4 acc[2][2][4][2];
-    uint4 pend[2][4][2];                  // packed bf16 results of the previous tile [mq][mi][nq]
-    const uint16_t *pbase = a.out_bf16;   // its output rows (row m0) ...
-    int prec = 0;                         // ... bounded at M (bytes)
-    int pn0 = 0;                          // its first column
-    bool has_pend = false;
-
-    auto store_group = [&](int j0) {      // pending stores j0 .. j0+3, j = (mq, mi, nq)
-        const __amdgpu_buffer_rsrc_t prs =
-            __builtin_amdgcn_make_buffer_rsrc((void *)pbase, (short)0, (a.sk_debug & 16) ? 0 : prec, 0x00020000);
-#pragma unroll
-        for (int j = j0; j < j0 + 4; ++j) {
-            const int mq = j >> 3, mi = (j >> 1) & 3, nq = j & 1;
-            const int rl = grp * 128 + mq * 64 + mi * 16 + li;
-            const int col = pn0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
-            if (a.sk_debug & 32)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[mq][mi][nq]), prs,
-                                                       (rl * N + col) * 2, 0, 2);
-            else
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[mq][mi][nq]), prs,
-                                                       (rl * N + col) * 2, 0, 0);
-        }
-    };
-
-    stage4(0, slot, 0, 0);
-    stage4(0, slot, 0, 4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (grp == 1) bar();  // stagger: G1 one segment behind
-
-    int ltile = slot, lk = 1;  // load cursor: the step after the one being computed
-    if (lk == nk) { lk = 0; ltile += G; }
-    int buf = 0, gstep = 0;
-    bf16x8 af[4][2], wf[2][2];
-
-    auto step = [&](auto first_c) {
-        constexpr bool FIRST = decltype(first_c)::value;
-        const uint8_t *As = smem + buf * STAGE;
-        const uint8_t *Ws = As + A_BYTES;
-        const bool more = gstep + 1 < nsteps;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int mq = p >> 1;
-            const int nq = (p == 1 || p == 2);
-            if (p == 0 || p == 2) {
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
-                        const int c = s * 4 + g;
-                        af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                    }
-            }
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
-                    const int c = s * 4 + g;
-                    wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                }
-            if (more && p < 2) stage4(buf ^ 1, ltile, lk * BK, p * 4);
-            if constexpr (FIRST) {
-                if (has_pend) store_group(4 * p);
-            }
-            if (p == 3) {
-                if (FIRST && has_pend) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            bar();
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < 2; ++ni) {
-                        const f32x4 cin = (FIRST && s == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mq][nq][mi][ni];
-                        acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], cin, 0, 0, 0);
-                    }
-            __builtin_amdgcn_s_setprio(0);
-            bar();
-        }
-        if (++lk == nk) { lk = 0; ltile += G; }
-        buf ^= 1;
-        ++gstep;
-    };
-
-    int tile = slot;
-    for (int t = 0; t < nmine; ++t, tile += G) {
-        step(std::true_type{});
-        for (int k = 1; k < nk; ++k) step(std::false_type{});
-
-        // ---- epilogue math of this tile → pend (stores follow in the next tile's first step)
-        const int tm = tile / ntn, tn = tile - tm * ntn;
-        const int m0 = tm * BM, n0 = tn * BN;
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq) {
-            float4 bias[2];
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-                bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
-#pragma unroll
-            for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi) {
-                    uint32_t u[2][2];
-#pragma unroll
-                    for (int ni = 0; ni < 2; ++ni) {
-                        const f32x4 v4 = acc[mq][nq][mi][ni];
-                        const float4 b4 = bias[ni];
-                        f32x2 lo = f32x2{v4[0] + b4.x, v4[1] + b4.y}, hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
-                        if constexpr (EPI == EPI_GELU_BF16) {
-                            lo = gelu_fast2(lo);
-                            hi = gelu_fast2(hi);
-                        }
-                        u[ni][0] = pack_bf16x2(lo.x, lo.y);
-                        u[ni][1] = pack_bf16x2(hi.x, hi.y);
-                    }
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
-                        u[0][h] = r2[0];
-                        u[1][h] = r2[1];
-                    }
-                    pend[mq][mi][nq] = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
-                }
-        }
-        const int rows_valid = min(BM, a.M - m0);
-        pbase = a.out_bf16 + (int64_t)m0 * N;
-        prec = rows_valid * N * 2;
-        pn0 = n0;
-        has_pend = true;
-    }
-#pragma unroll
-    for (int j0 = 0; j0 < 16; j0 += 4) store_group(j0);
-    if (grp == 0) bar();  // balance the stagger barrier
-}
-
-// Stream-K hand-off state: one partial-accumulator slab (256 KB) and 8 flags
-// per block slot, plus an error word; flags hold the epoch of the launch that
-// last published, so no per-launch reset is needed (epochs count up from 1 per
-// workspace; launches that share a workspace must be stream-ordered, which the
-// per-handle mutex of the callers guarantees).
-struct SkWorkspace {
-    float *ws = nullptr;
-    uint32_t *flags = nullptr;  // flags[0..slots*8) then the error word
-    int slots = 0;
-    uint32_t epoch = 0;
-    void ensure(int blocks) {
-        if (blocks <= slots) return;
-        release();
-        ws = (float *)dmalloc((size_t)blocks * 32 * 512 * 16);
-        flags = (uint32_t *)dmalloc(((size_t)blocks * 8 + 4) * sizeof(uint32_t));
-        RC_HIP(hipMemset(flags, 0, ((size_t)blocks * 8 + 4) * sizeof(uint32_t)));
-        slots = blocks;
-        epoch = 0;
-    }
-    void release() {
-        dfree(ws);
-        dfree(flags);
-        ws = nullptr;
-        flags = nullptr;
-        slots = 0;
-    }
-    uint32_t *err() const { return flags + (size_t)slots * 8; }
-    uint32_t next_epoch() {
-        if (++epoch == 0) epoch = 1;
-        return epoch;
-    }
-};
 
 // Skinny GEMM for M <= 256 (the last layer's CLS rows: O-proj, fc1, fc2 with
 // M = images in the slice).  A 256-row tile kernel would put the whole launch on
@@ -1200,17 +596,28 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
         }
     }
     if (row >= a.M) return;
+    float2 lrs;  // LayerNorm fold: this row's (rstd, -rstd*mu), as gemm_pp_kernel computes it
+    if constexpr (epi_ln(EPI)) lrs = ln_row_scale(a.ln_stats + (int64_t)row * (2 * LN_TILES), a.ln_eps);
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
         const int c = n0 + ni * 16 + 4 * g;
         const float4 b = *reinterpret_cast<const float4 *>(a.bias + c);
-        float v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
+        float v0, v1, v2, v3;
+        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′
+            const float4 lc = *reinterpret_cast<const float4 *>(a.ln_c + c);
+            v0 = fmaf(lrs.x, acc[ni][0], fmaf(lrs.y, lc.x, b.x));
+            v1 = fmaf(lrs.x, acc[ni][1], fmaf(lrs.y, lc.y, b.y));
+            v2 = fmaf(lrs.x, acc[ni][2], fmaf(lrs.y, lc.z, b.z));
+            v3 = fmaf(lrs.x, acc[ni][3], fmaf(lrs.y, lc.w, b.w));
+        } else {
+            v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
+        }
         if constexpr (EPI == EPI_RESID_F32) {
             float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + c);
             const float4 r = *o;
             *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
         } else {
-            if constexpr (EPI == EPI_GELU_BF16) {
+            if constexpr (epi_gelu(EPI)) {
                 const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
                 v0 = lo.x;
                 v1 = lo.y;
@@ -1223,20 +630,31 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
     }
 }
 
-// Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel), 2 = 256x256 8-wave,
-// 3 = 128x256 8-wave, 4 = ping-pong, 5 = persistent, 6 = Stream-K, 7 = deferred
-// stores, 8 = two-workgroup 128x256, 9 = skinny (M <= 256), 0 = auto.  Auto follows interleaved A/B
-// timings on the batch-256 shapes (tools/gemm_calib.py): ping-pong everywhere
-// except the short square projections (gemm_pick).
-enum GemmVariant {
-    GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_256x256 = 2, GEMM_128x256 = 3, GEMM_PINGPONG = 4, GEMM_PERSIST = 5, GEMM_STREAMK = 6,
-    GEMM_DEFERRED = 7, GEMM_W2 = 8, GEMM_SKINNY = 9
-};
+// LayerNorm-fold producer pass for rows a skinny GEMM wrote (M <= 256): one wave per
+// (row, 256-column tile), the same lane -> column map and reductions as the tiled
+// kernels' epilogues (ln_emit_row), so the partials are bit-identical for any M.
+__global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ x, uint16_t *__restrict__ ln_x,
+                                                     float *__restrict__ ln_stats, int M) {
+    const int lane = threadIdx.x & 63;
+    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= M * LN_TILES) return;  // wave-uniform
+    const int row = item / LN_TILES, t = item - row * LN_TILES;
+    const float4 v = reinterpret_cast<const float4 *>(x + (int64_t)row * 256 * LN_TILES + t * 256)[lane];
+    ln_emit_row(v, ln_x + (int64_t)row * 256 * LN_TILES + t * 256, ln_stats + ((int64_t)row * LN_TILES + t) * 2, lane, true);
+}
+
+// Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel, any N % 128 == 0),
+// 4 = ping-pong 256x256, 8 = two-workgroup 128x256, 9 = skinny (M <= 256), 0 = auto.
+// Auto follows interleaved A/B timings on the batch-256 shapes (tools/gemm_calib.py):
+// ping-pong everywhere except the short square projections.  (Round 1 also measured
+// a 256x256 / 128x256 single-barrier kernel, a persistent kernel, Stream-K and a
+// deferred-store persistent kernel: each lost on every shape and was removed.)
+enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9 };
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
-    if (variant != GEMM_AUTO) return variant;  // (100 + ABL: ablation builds, RC_GEMM_ABLATION)
+    if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
-    if (a.N % G2_BN != 0) return GEMM_V1;
+    if (a.N % 256 != 0) return GEMM_V1;
     // Short square projections (O-proj, patch embed: N = K = 768) finish in
     // ~2.3 rounds of 256x256 tiles and carry a heavy f32 epilogue (residual /
     // position read + write): the two-workgroup kernel overlaps that epilogue
@@ -1246,121 +664,40 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
     return GEMM_PINGPONG;
 }
 
-// Diagnostic bits for A/B experiments (RC_GEMM_DEBUG, read once; 0 in production):
-// 1 Stream-K skip publish, 2 skip wait, 16 deferred-store kernel drops its stores,
-// 32 deferred stores non-temporal.
-inline int gemm_debug_bits() {
-    static const int bits = [] {
-        const char *d = std::getenv("RC_GEMM_DEBUG");
-        return d ? std::atoi(d) : 0;
-    }();
-    return bits;
-}
-
 // Ping-pong tile order: groups of 8 row tiles (column-major inside a group) when
 // a row has >= 6 column tiles (QKV: 176 -> 170 us, fc1: 285 -> 274 us at batch
 // 256, interleaved A/B in tools/gemm_calib.py), row-major otherwise (fc2 prefers
-// it by 2 %).  RC_GEMM_GM (read once) overrides for A/B runs.
-inline int gemm_group_m(const GemmArgs &a) {
-    static const int env = [] {
-        const char *d = std::getenv("RC_GEMM_GM");
-        return d ? std::atoi(d) : -1;
-    }();
-    if (env >= 0) return env;
-    return a.N / 256 >= 6 ? 8 : 0;
-}
-
-// Ping-pong K order for grouped tile orders (GemmArgs::krev); RC_GEMM_KREV (read
-// once) sets R, 0 = every tile sweeps K upwards.  Off by default: alternating the
-// sweep did not pay at batch 256 (R = 4: fc1 264 -> 267 us, QKV 171 -> 173 us; R = 2
-// neutral; profiles/gemm/r01k_ab_krev.jsonl), so the A re-reads fc1's PMC traffic
-// shows are not the L2-LRU round-boundary misses this targets.
-inline int gemm_krev() {
-    static const int r = [] {
-        const char *d = std::getenv("RC_GEMM_KREV");
-        return d ? std::atoi(d) : 0;
-    }();
-    return r;
-}
-
-// compute units of the current device (one persistent block per CU)
-inline int gemm_num_cus() {
-    static thread_local int dev = -1, cus = 256;
-    int d = 0;
-    if (hipGetDevice(&d) == hipSuccess && d != dev) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0) cus = v;
-        dev = d;
-    }
-    return cus;
-}
+// it by 2 %).
+inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
 
 // rows the A buffer must provide beyond M (the kernels read whole tiles)
 inline int gemm_row_pad() { return 256; }
 
 template <int EPI>
-void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *sk = nullptr) {
+void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
-    int gm_override = -1;  // A/B hook (rc_gemm_bf16 only): variant + 1000 * G = ping-pong with group_m G
-    if (variant >= 1000) {
-        gm_override = variant / 1000;
-        variant %= 1000;
+    const int pick = gemm_pick(a, variant, EPI == EPI_PATCH_F32);
+    if constexpr (epi_ln(EPI)) {
+        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_SKINNY) && a.ln_c && a.ln_stats, RC_ERR_UNSUPPORTED,
+                   "LayerNorm-fold consumers run on the ping-pong or skinny kernel");
     }
-    switch (gemm_pick(a, variant, EPI == EPI_PATCH_F32)) {
+    switch (pick) {
         case GEMM_V1: {
-            RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
-            const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
-            hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
-            break;
-        }
-        case GEMM_256x256: {
-            RC_REQUIRE(a.N % G2_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            const int ntm = (a.M + 255) / 256, ntn = a.N / G2_BN;
-            hipLaunchKernelGGL((gemm256_kernel<EPI, 256>), dim3(ntm * ntn), dim3(512), 0, s, a);
-            break;
-        }
-        case GEMM_128x256: {
-            RC_REQUIRE(a.N % G2_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            const int ntm = (a.M + 127) / 128, ntn = a.N / G2_BN;
-            hipLaunchKernelGGL((gemm256_kernel<EPI, 128>), dim3(ntm * ntn), dim3(512), 0, s, a);
-            break;
-        }
-        case GEMM_PERSIST: {
-            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
-            hipLaunchKernelGGL((gemm_persist_kernel<EPI, false>), dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
-            break;
-        }
-        case GEMM_DEFERRED: {
-            a.sk_debug = gemm_debug_bits();
-            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
-            if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16)
-                hipLaunchKernelGGL(gemm_ds_kernel<EPI>, dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
-            else  // f32 epilogues: the persistent kernel
-                hipLaunchKernelGGL((gemm_persist_kernel<EPI, false>), dim3(std::min(ntiles, gemm_num_cus())), dim3(512), 0, s, a);
-            break;
-        }
-        case GEMM_STREAMK: {
-            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            RC_REQUIRE(sk != nullptr, RC_ERR_INVALID, "internal: Stream-K GEMM without a workspace");
-            const int64_t steps = (int64_t)((a.M + 255) / 256) * (a.N / 256) * (a.K / 64);
-            const int G = (int)std::min<int64_t>(steps, gemm_num_cus());
-            sk->ensure(G);
-            a.sk_ws = sk->ws;
-            a.sk_flags = sk->flags;
-            a.sk_err = sk->err();
-            a.sk_epoch = sk->next_epoch();
-            a.sk_debug = gemm_debug_bits();
-            hipLaunchKernelGGL((gemm_persist_kernel<EPI, true>), dim3(G), dim3(512), 0, s, a);
+            if constexpr (!epi_ln(EPI)) {
+                RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
+                const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
+                hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
+            }
             break;
         }
         case GEMM_W2: {
-            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            RC_REQUIRE(a.K % 32 == 0, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 32");
-            const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
-            hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3(ntm * ntn), dim3(256), 0, s, a);
+            if constexpr (!epi_ln(EPI)) {
+                RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+                RC_REQUIRE(a.K % 32 == 0, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 32");
+                const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
+                hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3(ntm * ntn), dim3(256), 0, s, a);
+            }
             break;
         }
         case GEMM_SKINNY: {
@@ -1368,12 +705,17 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
                        "skinny GEMM: bf16 / GELU / residual epilogues, N a multiple of 32");
             const int waves = ((a.M + 15) / 16) * (a.N / 32);
             hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+            if (a.ln_x != nullptr) {  // LayerNorm-fold producer: the partials in a second pass
+                RC_LAUNCH_CHECK();
+                RC_REQUIRE(a.N == 256 * LN_TILES, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
+                hipLaunchKernelGGL(ln_emit_kernel, dim3((a.M * LN_TILES + 3) / 4), dim3(256), 0, s, a.out_f32, a.ln_x,
+                                   a.ln_stats, a.M);
+            }
             break;
         }
         case GEMM_PINGPONG: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            a.group_m = gm_override >= 0 ? gm_override : gemm_group_m(a);
-            a.krev = a.group_m > 0 ? gemm_krev() : 0;
+            a.group_m = gemm_group_m(a);
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(ntm * ntn), dim3(512), 0, s, a);
             break;
@@ -1392,7 +734,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s, SkWorkspace *
         }
         case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
         case 100 + 8: case 100 + 16: case 100 + 24: {
-            a.group_m = gm_override >= 0 ? gm_override : gemm_group_m(a);  // the product tile order
+            a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
             switch (variant - 100) {

@@ -96,6 +96,10 @@ struct Layer {
     uint16_t *w_qkv = nullptr, *w_o = nullptr, *w_fc1 = nullptr, *w_fc2 = nullptr;
     float *b_qkv = nullptr, *b_o = nullptr, *b_fc1 = nullptr, *b_fc2 = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+    // LayerNorm folded into QKV / fc1 (vit_kernels.h "LayerNorm fold"): W′ = W·diag(γ) in
+    // bf16, c = Σ_k W′ (of the bf16 values), b′ = b + W·β
+    uint16_t *w_qkv_f = nullptr, *w_fc1_f = nullptr;
+    float *b_qkv_f = nullptr, *c_qkv = nullptr, *b_fc1_f = nullptr, *c_fc1 = nullptr;
 };
 
 constexpr int kMaxParts = 4;
@@ -127,6 +131,8 @@ struct rc_model {
     int Mp = 0, Pp = 0;
     uint16_t *patches = nullptr, *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
+    float *ln_stats = nullptr;     // [Mp][3][2] LayerNorm-fold partials (per 256-column tile: mean, M2)
+    bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
     bool cls_only_last = true;     // rc_model_set_last_layer / RC_EMBED_FULL_LAST=1
     float *cls_hidden = nullptr;
@@ -136,7 +142,6 @@ struct rc_model {
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
     int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
-    SkWorkspace sk;                // Stream-K partials/flags of this model's GEMMs
     int split = 2;                 // batch parts encoded concurrently (RC_EMBED_SPLIT / rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -150,7 +155,6 @@ struct rc_model {
     }
     ~rc_model() {
         for (auto &t : timers) t.destroy();
-        sk.release();
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (auto &e : ev_join)
             if (e) (void)hipEventDestroy(e);
@@ -246,6 +250,34 @@ void build_lut(rc_model *m) {
     RC_HIP(hipMemcpy(m->lut, h, sizeof(h), hipMemcpyHostToDevice));
 }
 
+// LayerNorm fold of one nn.Linear W [N][K] after LayerNorm(γ, β) (vit_kernels.h):
+// W′ = bf16(W·diag(γ)), c_n = Σ_k W′[n][k] (the bf16 values the MFMAs multiply,
+// summed in f64), b′_n = b_n + Σ_k W[n][k]·β_k (f64, from the f32 weights).
+void fold_layernorm(rc_model *m, const std::vector<float> &W, const std::vector<float> &b, const std::vector<float> &g,
+                    const std::vector<float> &beta, uint16_t **w_out, float **b_out, float **c_out) {
+    const size_t K = g.size(), N = b.size();
+    std::vector<float> wf(N * K), bf(N), cf(N);
+    for (size_t n = 0; n < N; ++n) {
+        double cs = 0.0, bs = b[n];
+        for (size_t k = 0; k < K; ++k) {
+            const float w = W[n * K + k] * g[k];
+            uint32_t u;
+            const uint16_t hb = host_f2bf(w);
+            u = (uint32_t)hb << 16;
+            float wr;
+            std::memcpy(&wr, &u, 4);
+            wf[n * K + k] = w;
+            cs += wr;
+            bs += (double)W[n * K + k] * beta[k];
+        }
+        cf[n] = (float)cs;
+        bf[n] = (float)bs;
+    }
+    *w_out = upload_bf16(m, {&wf});
+    *b_out = upload_f32(m, bf);
+    *c_out = upload_f32(m, cf);
+}
+
 const DeviceCoeffs &get_coeffs(rc_model *m, int in_size, int out_size) {
     auto key = std::make_pair(in_size * 8 + m->resample, out_size);
     auto it = m->coeff_cache.find(key);
@@ -324,7 +356,7 @@ void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, bool fc1 = false) {
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = fc1 ? m->timers[T_FC1].begin(s) : -1;
-    launch_gemm<EPI>(a, m->gemm_variant, s, &m->sk);
+    launch_gemm<EPI>(a, m->gemm_variant, s);
     if (fc1) m->timers[T_FC1].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
@@ -376,19 +408,39 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
     float *hidden = m->hidden + r0 * H;
     uint16_t *ln = m->ln + r0 * H, *qkv = m->qkv + r0 * 3 * H, *attn = m->attn + r0 * H;
     uint16_t *mlp = m->mlp + r0 * c.mlp;
+    // LayerNorm fold (vit_kernels.h): every producer of the residual stream also writes
+    // bf16(x) into `ln` and per-tile partials into `st`; QKV and fc1 apply the norm in
+    // their epilogues.  The same arithmetic at every batch size (skinny GEMMs for
+    // M <= 256 included), so an image's embedding does not depend on its batch.
+    const bool fold = m->ln_fold;
+    float *st = m->ln_stats + r0 * 2 * LN_TILES;
+    auto produce = [&](GemmArgs a, bool emit) {
+        if (fold && emit) {
+            a.ln_x = ln;
+            a.ln_stats = st;
+        }
+        return a;
+    };
     // 2. embeddings: CLS + pos, patch GEMM (+bias +pos) into the residual stream
-    hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, hidden, T, H, m->cls, m->pos);
+    hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, hidden, T, H, m->cls, m->pos, fold ? ln : nullptr,
+                       fold ? st : nullptr);
     RC_LAUNCH_CHECK();
-    {
-        GemmArgs a{patches, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden, m->pos, T};
-        gemm<EPI_PATCH_F32>(m, a, s);
-    }
+    gemm<EPI_PATCH_F32>(m, produce(GemmArgs{patches, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden,
+                                            m->pos, T}, true), s);
     // 3. encoder layers
     const float scale = 1.0f / std::sqrt((float)(H / c.heads));
     for (int l = 0; l < c.layers; ++l) {
         const Layer &L = m->layers[l];
-        layernorm(m, hidden, L.ln1_w, L.ln1_b, ln, M, s);
-        gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
+        if (fold) {
+            GemmArgs a{ln, L.w_qkv_f, L.b_qkv_f, M, 3 * H, H, qkv, nullptr, nullptr, T};
+            a.ln_c = L.c_qkv;
+            a.ln_stats = st;
+            a.ln_eps = c.ln_eps;
+            gemm<EPI_BF16_LN>(m, a, s);
+        } else {
+            layernorm(m, hidden, L.ln1_w, L.ln1_b, ln, M, s);
+            gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
+        }
         if (m->cls_only_last && l == c.layers - 1) {
             last_layer_cls(m, L, i0, n, qkv, hidden, scale, s);
             break;
@@ -404,10 +456,20 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
                                scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
-        gemm<EPI_RESID_F32>(m, GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, s);
-        layernorm(m, hidden, L.ln2_w, L.ln2_b, ln, M, s);
-        gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, true);
-        gemm<EPI_RESID_F32>(m, GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T}, s);
+        gemm<EPI_RESID_F32>(m, produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true), s);
+        if (fold) {
+            GemmArgs a{ln, L.w_fc1_f, L.b_fc1_f, M, c.mlp, H, mlp, nullptr, nullptr, T};
+            a.ln_c = L.c_fc1;
+            a.ln_stats = st;
+            a.ln_eps = c.ln_eps;
+            gemm<EPI_GELU_BF16_LN>(m, a, s, true);
+        } else {
+            layernorm(m, hidden, L.ln2_w, L.ln2_b, ln, M, s);
+            gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, true);
+        }
+        // the last layer's fc2 feeds only the final LN of the CLS rows (cls_final_kernel)
+        gemm<EPI_RESID_F32>(m, produce(GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T},
+                                       l + 1 < c.layers), s);
     }
     // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
     const float *fin = m->cls_only_last ? m->cls_hidden + (int64_t)i0 * H : hidden;
@@ -475,6 +537,8 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->Pp = round_up(B * m->npatch, gemm_row_pad()) + gemm_row_pad();
             m->patches = (uint16_t *)m->alloc((size_t)m->Pp * m->kpatch * 2);
             m->hidden = (float *)m->alloc((size_t)m->Mp * H * 4);
+            m->ln_stats = (float *)m->alloc((size_t)m->Mp * 2 * LN_TILES * 4);
+            RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * 2 * LN_TILES * 4));  // pad rows: finite scales
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->qkv = (uint16_t *)m->alloc((size_t)m->Mp * 3 * H * 2);
             m->attn = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
@@ -589,6 +653,16 @@ int rc_model_finalize(rc_model *m) {
             L.ln1_b = upload_f32(m, h[p + "layernorm_before.bias"]);
             L.ln2_w = upload_f32(m, h[p + "layernorm_after.weight"]);
             L.ln2_b = upload_f32(m, h[p + "layernorm_after.bias"]);
+            std::vector<float> wq;
+            for (const char *nm : {"query", "key", "value"}) {
+                const auto &w = h[p + "attention.attention." + nm + ".weight"];
+                wq.insert(wq.end(), w.begin(), w.end());
+            }
+            fold_layernorm(m, wq, bqkv, h[p + "layernorm_before.weight"], h[p + "layernorm_before.bias"], &L.w_qkv_f,
+                           &L.b_qkv_f, &L.c_qkv);
+            fold_layernorm(m, h[p + "intermediate.dense.weight"], h[p + "intermediate.dense.bias"],
+                           h[p + "layernorm_after.weight"], h[p + "layernorm_after.bias"], &L.w_fc1_f, &L.b_fc1_f,
+                           &L.c_fc1);
         }
         m->host.clear();
         m->ready = true;
@@ -663,6 +737,14 @@ int rc_model_set_parts(rc_model *m, int parts) {
     });
 }
 
+int rc_model_set_ln_fold(rc_model *m, int on) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->ln_fold = on != 0;
+    });
+}
+
 int rc_model_set_last_layer(rc_model *m, int cls_only) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
@@ -688,20 +770,13 @@ extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint1
         RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
         GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
         hipStream_t s = (hipStream_t)stream;
-        // one Stream-K workspace per device for this test/benchmark hook, calls serialised
-        static std::mutex mu;
-        static std::map<int, SkWorkspace> sk_by_dev;
-        std::lock_guard<std::mutex> lk(mu);
-        int dev = 0;
-        RC_HIP(hipGetDevice(&dev));
-        SkWorkspace *sk = &sk_by_dev[dev];
         switch (epi) {
-            case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s, sk); break;
-            case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s, sk); break;
-            case EPI_RESID_F32: launch_gemm<EPI_RESID_F32>(a, variant, s, sk); break;
+            case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s); break;
+            case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s); break;
+            case EPI_RESID_F32: launch_gemm<EPI_RESID_F32>(a, variant, s); break;
             case EPI_PATCH_F32:
                 RC_REQUIRE(pos && tokens > 1, RC_ERR_INVALID, "patch epilogue needs pos and tokens");
-                launch_gemm<EPI_PATCH_F32>(a, variant, s, sk);
+                launch_gemm<EPI_PATCH_F32>(a, variant, s);
                 break;
             default: throw Error(RC_ERR_INVALID, "unknown epilogue");
         }

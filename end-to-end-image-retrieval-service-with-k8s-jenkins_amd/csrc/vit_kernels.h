@@ -25,7 +25,11 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
 
-enum GemmEpi { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_PATCH_F32 = 3 };
+// EPI_BF16_LN / EPI_GELU_BF16_LN: the bf16 epilogues as consumers of the LayerNorm fold
+enum GemmEpi { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_PATCH_F32 = 3, EPI_BF16_LN = 4, EPI_GELU_BF16_LN = 5 };
+constexpr bool epi_bf16_out(int e) { return e == EPI_BF16 || e == EPI_GELU_BF16 || e == EPI_BF16_LN || e == EPI_GELU_BF16_LN; }
+constexpr bool epi_gelu(int e) { return e == EPI_GELU_BF16 || e == EPI_GELU_BF16_LN; }
+constexpr bool epi_ln(int e) { return e == EPI_BF16_LN || e == EPI_GELU_BF16_LN; }
 
 struct GemmArgs {
     const uint16_t *A;  // [rows >= roundup(M, BM)][K] bf16, row-major
@@ -36,15 +40,61 @@ struct GemmArgs {
     float *out_f32;     // EPI_RESID_F32 (in place: out += A W^T + b) / EPI_PATCH_F32
     const float *pos;   // EPI_PATCH_F32: position embeddings [tokens][N]
     int tokens;         // EPI_PATCH_F32: tokens per image (patches + 1)
-    // Stream-K hand-off state (gemm_persist_kernel<EPI, true>); see SkWorkspace
-    float *sk_ws = nullptr;          // [blocks][32][512] f32x4 partial accumulators
-    uint32_t *sk_flags = nullptr;    // [blocks][8] per-wave publish flags (= epoch when ready)
-    uint32_t *sk_err = nullptr;      // bit 0: a bounded spin gave up
-    uint32_t sk_epoch = 0;           // this launch's flag value (never 0)
-    int sk_debug = 0;                // diagnostic bits (gemm_debug_bits), 0 in production
     int group_m = 0;                 // ping-pong tile order: 0 = row-major, G = groups of G row tiles
-    int krev = 0;                    // ping-pong K order: R > 0 = column tiles with (tn / R) odd sweep K downwards
+    // LayerNorm folded across a GEMM pair (see "LayerNorm fold" below):
+    //   producer (f32 epilogues): ln_x != null → also write bf16(x) rows and per-(row, 256-column
+    //     tile) partial statistics (mean, M2) into ln_stats[row][N / 256][2]
+    //   consumer (bf16 epilogues): ln_c != null → A is bf16(x), W = W∘γ, bias = b + W·β, and the
+    //     epilogue applies rstd·(acc − μ·c) + bias with μ, rstd from ln_stats[row][3][2]
+    uint16_t *ln_x = nullptr;
+    float *ln_stats = nullptr;
+    const float *ln_c = nullptr;
+    float ln_eps = 1e-6f;
 };
+
+// ------------------------------------------------------------ LayerNorm fold
+// modeling_vit_msn.py:258-259 LayerNorm(768, eps) then nn.Linear:
+//   LN(x)·Wᵀ + b = rstd·(x·W′ᵀ − μ·c) + b′,  W′ = W·diag(γ),  c_n = Σ_k W′[n][k],  b′ = b + W·β.
+// The residual stream's producer epilogue (patch GEMM, O-proj, fc2, cls_init)
+// writes bf16(x) next to the f32 x plus, per 256-column tile of each row, the
+// tile mean and M2 = Σ (x − tile mean)²; the consumer GEMM (QKV, fc1) combines
+// the three tiles by Chan's formula (exact in exact arithmetic, no E[x²] − μ²
+// cancellation) and applies the correction in its epilogue.  What this removes:
+// the standalone LayerNorm pass (f32 read + bf16 write of the whole stream, 24
+// launches per batch).  Accuracy: bf16(x) carries the same relative error as
+// bf16(LN(x)) while |μ| ≲ σ per token; c is summed from the bf16 W′ the MFMAs
+// use, so the μ·c term cancels exactly what the MFMAs add for the mean.
+constexpr int LN_TILES = 3;  // 768 columns / 256
+
+// Chan combination of the LN_TILES partials of one row → (rstd, −rstd·μ)
+__device__ __forceinline__ float2 ln_row_scale(const float *__restrict__ st, float eps) {
+    float m[LN_TILES], M2 = 0.f, mu = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN_TILES; ++t) {
+        m[t] = st[2 * t];
+        M2 += st[2 * t + 1];
+        mu += m[t];
+    }
+    mu *= 1.0f / LN_TILES;
+#pragma unroll
+    for (int t = 0; t < LN_TILES; ++t) M2 = fmaf(256.0f * (m[t] - mu), m[t] - mu, M2);
+    const float rstd = 1.0f / sqrtf(M2 * (1.0f / (256 * LN_TILES)) + eps);
+    return make_float2(rstd, -rstd * mu);
+}
+
+// Producer side, one wave holding one row's 256-column segment as float4 v per
+// lane: write bf16(v) and the tile's (mean, M2).  Wave-collective.
+__device__ __forceinline__ void ln_emit_row(const float4 v, uint16_t *__restrict__ xrow, float *__restrict__ strow,
+                                            int lane, bool store) {
+    const float s = wave_sum((v.x + v.y) + (v.z + v.w));
+    const float mt = s * (1.0f / 256);
+    const float d0 = v.x - mt, d1 = v.y - mt, d2 = v.z - mt, d3 = v.w - mt;
+    const float M2 = wave_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+    if (store) {
+        reinterpret_cast<uint2 *>(xrow)[lane] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+        if (lane == 0) *reinterpret_cast<float2 *>(strow) = make_float2(mt, M2);
+    }
+}
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;
 
@@ -248,11 +298,20 @@ __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__
     }
 }
 
-// hidden[img*tokens + 0] = cls + pos[0]
+// hidden[img*tokens + 0] = cls + pos[0]; with ln_x: also its bf16 copy and LN partials
+// (the LayerNorm fold's producer for the CLS rows; H = 768, one wave per 256 columns)
 __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidden, int tokens, int H,
-                                                      const float *__restrict__ cls, const float *__restrict__ pos) {
+                                                      const float *__restrict__ cls, const float *__restrict__ pos,
+                                                      uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats) {
     const int img = blockIdx.x;
-    for (int c = threadIdx.x; c < H; c += 256) hidden[(int64_t)img * tokens * H + c] = cls[c] + pos[c];
+    const int64_t row = (int64_t)img * tokens;
+    for (int c = threadIdx.x; c < H; c += 256) hidden[row * H + c] = cls[c] + pos[c];
+    if (ln_x != nullptr && threadIdx.x < 64 * LN_TILES) {
+        const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int c = t * 256 + lane * 4;
+        const float4 v = make_float4(cls[c] + pos[c], cls[c + 1] + pos[c + 1], cls[c + 2] + pos[c + 2], cls[c + 3] + pos[c + 3]);
+        ln_emit_row(v, ln_x + row * H + t * 256, ln_stats + (row * LN_TILES + t) * 2, lane, true);
+    }
 }
 
 // Self-attention v2 for one (image, head), tokens <= 208, head dim 64.

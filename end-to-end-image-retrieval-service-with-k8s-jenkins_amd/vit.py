@@ -169,10 +169,14 @@ class VitMsnEmbedder:
         for idx in groups.values():
             for s0 in range(0, len(idx), self.max_batch):
                 chunk = idx[s0:s0 + self.max_batch]
-                if isinstance(images[chunk[0]], torch.Tensor):
-                    x = torch.stack([images[i] for i in chunk])
-                else:
+                if all(isinstance(images[i], torch.Tensor) for i in chunk):
+                    x = torch.stack([images[i].to(self.device) for i in chunk])
+                elif not any(isinstance(images[i], torch.Tensor) for i in chunk):
                     x = torch.from_numpy(np.stack([np.asarray(images[i], dtype=np.uint8) for i in chunk]))
+                else:  # GPU-decoded and host-decoded images of one size
+                    x = torch.stack([torch.as_tensor(np.asarray(images[i], dtype=np.uint8)).to(self.device)
+                                     if not isinstance(images[i], torch.Tensor) else images[i].to(self.device)
+                                     for i in chunk])
                 r, m = self.embed(x, normalized=normalized)
                 sel = torch.tensor(chunk, dtype=torch.int64, device=self.device)
                 raw.index_copy_(0, sel, r)
@@ -248,6 +252,10 @@ class VitMsnEmbedder:
     def set_parts(self, parts: int) -> None:
         """Encode batches as ``parts`` concurrent slices on separate streams (1 = one stream)."""
         check(self.lib.rc_model_set_parts(self._h, int(parts)))
+
+    def set_ln_fold(self, on: bool) -> None:
+        """Fold the LayerNorms into the GEMMs around them (default) or run the LN kernel."""
+        check(self.lib.rc_model_set_ln_fold(self._h, int(bool(on))))
 
     def set_last_layer(self, cls_only: bool) -> None:
         """Run the last encoder layer on the CLS rows only (default) or on every row."""

@@ -238,6 +238,14 @@ int rc_model_set_parts(rc_model *m, int parts);
  * create: RC_EMBED_FULL_LAST=1. */
 int rc_model_set_last_layer(rc_model *m, int cls_only);
 
+/* LayerNorm fold (default 1): the two LayerNorms of each layer
+ * (modeling_vit_msn.py:258-259) are folded into the GEMMs around them — the residual producers (patch embed, O-proj, fc2) also
+ * write bf16(x) and per-256-column (mean, M2) partials, and QKV / fc1 apply
+ * rstd·(x·(W∘γ)ᵀ − μ·Σ_k W∘γ) + (b + W·β) in their epilogues — instead of a
+ * standalone LayerNorm pass over the f32 stream.  0 runs the LN kernel (A/B and
+ * parity tests). */
+int rc_model_set_ln_fold(rc_model *m, int on);
+
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM (dominant), 2 = attention,
  * 3 = layernorm, 4 = preprocess; `mask` bit i enables id i (-1 = all, 0 = off). */
@@ -249,8 +257,8 @@ int rc_model_timing_reset(rc_model *m);
  * inside rc_embed this is every nn.Linear of modeling_vit_msn.py:199-202,243-244).
  * out = epilogue(A[M][K] · W[N][K]ᵀ + bias): epi 0 → bf16 out, 1 → bf16 GELU(out),
  * 2 → f32 out += (residual, in place), 3 → f32 patch scatter (+pos, tokens/image).
- * A must have round_up(M, 256) readable rows.  variant: 0 auto, 1 128x128,
- * 2 256x256, 3 128x256 tiles. */
+ * A must have round_up(M, 256) readable rows.  variant: 0 auto, 1 128x128 tiles,
+ * 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256). */
 int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N, int K,
                  void *out, const float *pos, int tokens, void *stream);
 

@@ -24,13 +24,13 @@ def run(epi, variant, A, W, bias, M, out, pos=None, tokens=0):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [1, 4, 8])
 @pytest.mark.parametrize("M,N,K", [(300, 768, 768), (1000, 2304, 768), (513, 3072, 768), (257, 768, 3072), (64, 256, 64)])
 @pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
 def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
     import torch
 
-    if variant in (2, 3, 4, 5, 6, 7, 8) and N % 256:
+    if variant in (4, 8) and N % 256:
         pytest.skip("256-wide tiles need N % 256 == 0")
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     Mp = (M + 255) // 256 * 256
@@ -62,7 +62,7 @@ def test_skinny_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
     test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [1, 4, 8])
 def test_patch_epilogue_scatter(cuda, variant):
     import torch
 
@@ -81,30 +81,3 @@ def test_patch_epilogue_scatter(cuda, variant):
     got = hidden.reshape(n_img, T, H)
     assert torch.allclose(got[:, 1:], ref, atol=1e-4, rtol=1e-4)
     assert bool((got[:, 0] == -3.0).all())  # CLS rows are not the GEMM's
-
-
-def test_streamk_back_to_back_launches(cuda):
-    """Stream-K hand-offs across many queued launches of different shapes (epoch flags reused)."""
-    import torch
-
-    g = torch.Generator(device=cuda).manual_seed(7)
-    cases = []
-    for M, N, K in [(300, 768, 768), (50, 256, 128), (2000, 768, 3072), (700, 2304, 768)] * 3:
-        Mp = (M + 255) // 256 * 256
-        A = (torch.randn(Mp, K, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
-        W = (torch.randn(N, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
-        bias = torch.randn(N, device=cuda, generator=g) * 0.1
-        resid = torch.randn(Mp, N, device=cuda, generator=g)
-        out = resid.clone()
-        cases.append((A, W, bias, M, resid, out))
-    L = import_pkg("_lib")
-    lib = L.load()
-    s = torch.cuda.current_stream().cuda_stream
-    for A, W, bias, M, resid, out in cases:  # no sync in between
-        N, K = W.shape
-        L.check(lib.rc_gemm_bf16(EPI_RESID, 6, A.data_ptr(), W.data_ptr(), bias.data_ptr(), M, N, K, out.data_ptr(),
-                                 None, 0, s))
-    torch.cuda.synchronize()
-    for A, W, bias, M, resid, out in cases:
-        ref = resid[:M] + A[:M].float() @ W.float().T + bias
-        assert torch.allclose(out[:M], ref, atol=1e-4, rtol=1e-4)

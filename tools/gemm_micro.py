@@ -12,7 +12,7 @@ lib = L.load()
 dev = torch.device("cuda", 0)
 M = 256 * 197
 shapes = {"qkv": (2304, 768, 0), "o": (768, 768, 2), "fc1": (3072, 768, 1), "fc2": (768, 3072, 2)}
-variants = [int(v) for v in os.environ.get("VARIANTS", "4,5,6").split(",")]
+variants = [int(v) for v in os.environ.get("VARIANTS", "4,8").split(",")]
 rounds = int(os.environ.get("ROUNDS", "5"))
 res = {}
 for name, (N, K, epi) in shapes.items():
