@@ -63,6 +63,14 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
     return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
+// 16-B store with the non-temporal (streaming) hint (diagnostic ablations)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ void nt_store16(T *dst, const T &v) {
+    static_assert(sizeof(T) == 16, "16-byte values");
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4 *>(dst));
+}
+
 // ----------------------------------------------------------- ping-pong GEMM --
 // 256x256x64 tile, 8 waves in two groups: G0 = waves 0-3 (output rows 0-127),
 // G1 = waves 4-7 (rows 128-255); wave w and w+4 share a SIMD.  Each wave owns
@@ -229,6 +237,46 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 
     // epilogue: acc[mq][nq][mi][ni][j] = C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
+    if constexpr (epi_bf16_out(EPI) && (ABL & 64) != 0 && !epi_ln(EPI)) {
+        // diagnostic: no LDS staging — bf16 pairs of 16-lane rows swapped with
+        // v_permlane16_swap so each lane stores 16 B (8 consecutive columns)
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+#pragma unroll
+                for (int nq = 0; nq < 2; ++nq) {
+                    uint32_t u[2][2];
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const f32x4 v4 = acc[mq][nq][mi][ni];
+                        const float4 b4 = biasr[nq][ni];
+                        f32x2 lo = f32x2{v4[0] + b4.x, v4[1] + b4.y}, hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
+                        if constexpr (epi_gelu(EPI)) {
+                            lo = gelu_fast2(lo);
+                            hi = gelu_fast2(hi);
+                        }
+                        u[ni][0] = pack_bf16x2(lo.x, lo.y);
+                        u[ni][1] = pack_bf16x2(hi.x, hi.y);
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
+                        u[0][h] = r2[0];
+                        u[1][h] = r2[1];
+                    }
+                    const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
+                    if (row < a.M) {
+                        uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * a.N + col);
+                        const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
+                        if constexpr ((ABL & 32) != 0) nt_store16(dst, val);
+                        else *dst = val;
+                    }
+                }
+            }
+        return;
+    }
     if constexpr (epi_bf16_out(EPI)) {
         // Stage the 256x256 bf16 tile in LDS (512-B rows, 16-B chunk XOR (row & 31)),
         // then every wave stores whole 512-B row segments with 16-B stores.
@@ -289,7 +337,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
             if constexpr ((ABL & 8) != 0) {
                 asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
             } else if (m0 + rl < a.M) {
-                *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+                uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8);
+                if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
+                else *dst = v;
             }
         }
         return;
@@ -349,7 +399,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                     const int img = row / np, p = row - img * np;
                     orow = (int64_t)img * a.tokens + 1 + p;
                 }
-                *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o;
+                float4 *dst = reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4);
+                if constexpr ((ABL & 32) != 0) nt_store16(dst, o);  // diagnostic: streaming store
+                else *dst = o;
                 if (a.ln_x != nullptr)  // LayerNorm fold producer
                     ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
             }
@@ -733,7 +785,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
-        case 100 + 8: case 100 + 16: case 100 + 24: {
+        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: {
             a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
@@ -747,6 +799,9 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 case 8: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 8>), gr, bl, 0, s, a); break;
                 case 16: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 16>), gr, bl, 0, s, a); break;
                 case 24: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 24>), gr, bl, 0, s, a); break;
+                case 32: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 32>), gr, bl, 0, s, a); break;
+                case 64: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 64>), gr, bl, 0, s, a); break;
+                case 96: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 96>), gr, bl, 0, s, a); break;
             }
             break;
         }
