@@ -411,6 +411,104 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 }
 
 
+// Epilogue of a 128 x 256 tile held as acc[mi][ni] by 4 waves (wave w: columns
+// [64w, 64w + 64)): acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + w*64 + ni*16 + 4g + j].
+// Stages through `smem` (>= 64 KB; the caller's main loop must be done with it).
+template <int EPI>
+__device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4], uint8_t *smem, int m0, int n0) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    float4 bias[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
+    __syncthreads();  // every wave's last fragment reads are done: the ring is free
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        // 128 x 256 bf16 tile staged in LDS (512-B rows, 16-B chunk XOR (row & 31)),
+        // stored as whole 512-B row segments, 16 B per lane.
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int cl = wave * 64 + ni * 16 + 4 * g;
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                const int rl = mi * 16 + li;
+                const f32x4 v4 = acc[mi][ni];
+                float v0 = v4[0] + bias[ni].x, v1 = v4[1] + bias[ni].y, v2 = v4[2] + bias[ni].z, v3 = v4[3] + bias[ni].w;
+                if constexpr (EPI == EPI_GELU_BF16) {
+                    const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
+                    v0 = lo.x;
+                    v1 = lo.y;
+                    v2 = hi.x;
+                    v3 = hi.y;
+                }
+                const int off = rl * 512 + (((cl >> 3) ^ (rl & 31)) << 4) + (cl & 7) * 2;
+                *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 256 + tid;
+            const int rl = id >> 5, ch = id & 31;
+            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
+            if (m0 + rl < a.M) *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+        }
+        return;
+    }
+    // f32 epilogues: two halves of 64 rows (64 KB each: 1-KB rows, 16-B chunk XOR
+    // (row & 63)), copied out as whole 1-KB row segments with the residual /
+    // position loads issued back to back before the adds and stores.
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int cl = wave * 64 + ni * 16 + 4 * g;
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq) {
+                const int rl = mq * 16 + li;
+                const f32x4 v4 = acc[h * 4 + mq][ni];
+                *reinterpret_cast<float4 *>(smem + rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4)) =
+                    make_float4(v4[0] + bias[ni].x, v4[1] + bias[ni].y, v4[2] + bias[ni].z, v4[3] + bias[ni].w);
+            }
+        }
+        __syncthreads();
+        float4 add[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 256 + tid;
+            const int rl = id >> 6, ch = id & 63;
+            const int row = m0 + h * 64 + rl;
+            const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
+            if constexpr (EPI == EPI_RESID_F32) {
+                add[it] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
+            } else {
+                const int p = rr % (a.tokens - 1);
+                add[it] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 256 + tid;
+            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
+            const int row = m0 + h * 64 + rl;
+            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
+            const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
+            if (row < a.M) {
+                int64_t orow = row;
+                if constexpr (EPI == EPI_PATCH_F32) {
+                    const int np = a.tokens - 1;
+                    const int img = row / np, p = row - img * np;
+                    orow = (int64_t)img * a.tokens + 1 + p;
+                }
+                *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o;
+                if (a.ln_x != nullptr)  // LayerNorm fold producer
+                    ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
+            }
+        }
+        if (h == 0) __syncthreads();  // the second half overwrites the staging rows
+    }
+}
+
 // ------------------------------------------------- two-workgroup GEMM ----
 // 128 (rows) x 256 (cols) tile per 256-thread workgroup, TWO workgroups per CU.
 // A 256x256 f32 accumulator tile fills half the CU's register file, so with one
@@ -525,97 +623,114 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
             for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
         return;
     }
-    // epilogue: acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + wave*64 + ni*16 + 4g + j]
-    float4 bias[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
-    __syncthreads();  // every wave's last fragment reads are done: the ring is free
-    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-        // 128 x 256 bf16 tile staged in LDS (512-B rows, 16-B chunk XOR (row & 31)),
-        // stored as whole 512-B row segments, 16 B per lane.
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            const int cl = wave * 64 + ni * 16 + 4 * g;
-#pragma unroll
-            for (int mi = 0; mi < 8; ++mi) {
-                const int rl = mi * 16 + li;
-                const f32x4 v4 = acc[mi][ni];
-                float v0 = v4[0] + bias[ni].x, v1 = v4[1] + bias[ni].y, v2 = v4[2] + bias[ni].z, v3 = v4[3] + bias[ni].w;
-                if constexpr (EPI == EPI_GELU_BF16) {
-                    const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
-                    v0 = lo.x;
-                    v1 = lo.y;
-                    v2 = hi.x;
-                    v3 = hi.y;
-                }
-                const int off = rl * 512 + (((cl >> 3) ^ (rl & 31)) << 4) + (cl & 7) * 2;
-                *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 256 + tid;
-            const int rl = id >> 5, ch = id & 31;
-            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
-            if (m0 + rl < a.M) *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
-        }
-        return;
-    }
-    // f32 epilogues: two halves of 64 rows (64 KB each: 1-KB rows, 16-B chunk XOR
-    // (row & 63)), copied out as whole 1-KB row segments with the residual /
-    // position loads issued back to back before the adds and stores.
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            const int cl = wave * 64 + ni * 16 + 4 * g;
-#pragma unroll
-            for (int mq = 0; mq < 4; ++mq) {
-                const int rl = mq * 16 + li;
-                const f32x4 v4 = acc[h * 4 + mq][ni];
-                *reinterpret_cast<float4 *>(smem + rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4)) =
-                    make_float4(v4[0] + bias[ni].x, v4[1] + bias[ni].y, v4[2] + bias[ni].z, v4[3] + bias[ni].w);
-            }
-        }
-        __syncthreads();
-        float4 add[16];
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 256 + tid;
-            const int rl = id >> 6, ch = id & 63;
-            const int row = m0 + h * 64 + rl;
-            const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
-            if constexpr (EPI == EPI_RESID_F32) {
-                add[it] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
-            } else {
-                const int p = rr % (a.tokens - 1);
-                add[it] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 256 + tid;
-            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
-            const int row = m0 + h * 64 + rl;
-            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
-            const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
-            if (row < a.M) {
-                int64_t orow = row;
-                if constexpr (EPI == EPI_PATCH_F32) {
-                    const int np = a.tokens - 1;
-                    const int img = row / np, p = row - img * np;
-                    orow = (int64_t)img * a.tokens + 1 + p;
-                }
-                *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o;
-                if (a.ln_x != nullptr)  // LayerNorm fold producer
-                    ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
-            }
-        }
-        if (h == 0) __syncthreads();  // the second half overwrites the staging rows
-    }
+    w2_epilogue<EPI>(a, acc, smem, m0, n0);
 }
 
+// ------------------------------------------- implicit-GEMM patch embedding ----
+// Conv2d(3, 768, 16, stride 16) (modeling_vit_msn.py:57) as C[m][n] = A[m][k]·W[n][k]ᵀ
+// with m = (image, patch) and A never materialised: the K axis is ordered
+// (ky, kx, c), so the 16 K-values a lane needs per step are 16 CONTIGUOUS bytes of
+// one image row (48 bytes per patch row in HWC), and the weight matrix is permuted
+// to the same order once at finalize (W′[n][(ky·P + kx)·3 + c] = W[n][c][ky][kx]).
+// Each byte becomes the exact f32 of ViTImageProcessor's rescale→normalize rounded
+// to bf16 — a [3][256] LUT in LDS, the values the im2col kernel wrote before.
+// 128 x 256 tile, 4 waves (as gemm_w2_kernel, whose fragment layout and epilogue it
+// shares), two workgroups per CU; both operands register-staged (one 16-B A load
+// and four 16-B W loads per lane per 32-deep K-step, issued before the step's
+// MFMAs and written to the other LDS slot after them).
+template <int P>
+__global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
+    constexpr int BM = 128, BN = 256, BK = 32, KC = 3 * P * P;
+    constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 KB + 16 KB
+    static_assert(2 * SLOT + 3 * 256 * 2 <= 64 * 1024, "ring + LUT within the epilogue's 64 KB");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[64 * 1024];
+    uint16_t *lut = reinterpret_cast<uint16_t *>(smem + 2 * SLOT);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+
+    const int ntn = a.N / BN, ntm = (a.M + BM - 1) / BM;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    constexpr int GM = 8;
+    const int grp_tiles = GM * ntn, grp = t / grp_tiles, in = t - grp * grp_tiles;
+    const int gm = min(GM, ntm - grp * GM);
+    const int tm = grp * GM + in % gm, tn = in / gm;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    for (int i = tid; i < 3 * 256; i += 256) lut[i] = a.lut[i];
+
+    // A: lane pair (row ar, half ah) loads K [32 kt + 16 ah, +16) of patch row m0 + ar
+    const int S = a.img_size, gp = S / P, np = gp * gp;
+    const int ar = tid >> 1, ah = tid & 1;
+    const int m = min(m0 + ar, a.M - 1);  // rows past M re-read the last patch (results unused)
+    const int b = m / np, pi = m - b * np, py = pi / gp, px = pi - py * gp;
+    const uint8_t *abase = a.img + (((int64_t)b * S + py * P) * S + px * P) * 3;
+    const int arow_stride = S * 3;
+    // W: lane = row n0 + tid, its 64 bytes of the step
+    const uint16_t *wrow = a.W + (int64_t)(n0 + tid) * KC;
+    const int asw = ((ar >> 3) & 1) << 1, wsw = ((tid >> 3) & 1) << 1;  // chunk XOR of the fragment layout
+
+    uint4 av, wv[4];
+    auto load = [&](int kt) {
+        const int k0 = kt * BK + 16 * ah;
+        const int ky = k0 / (3 * P), off = k0 - ky * (3 * P);
+        av = *reinterpret_cast<const uint4 *>(abase + ky * arow_stride + off);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wv[c] = *reinterpret_cast<const uint4 *>(wrow + kt * BK + 8 * c);
+    };
+    auto store = [&](int slot, int kt) {
+        uint8_t *As = smem + slot * SLOT;
+        uint8_t *Ws = As + A_BYTES;
+        const int c0 = (kt * BK + 16 * ah) % 3;  // channel of the first byte (k = ky·3P + kx·3 + c)
+        const uint32_t w4[4] = {av.x, av.y, av.z, av.w};
+        uint32_t o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int cA = (c0 + 2 * j) % 3, cB = (c0 + 2 * j + 1) % 3;
+            const uint32_t bA = (w4[j >> 1] >> (16 * (j & 1))) & 0xffu, bB = (w4[j >> 1] >> (16 * (j & 1) + 8)) & 0xffu;
+            o[j] = (uint32_t)lut[cA * 256 + bA] | ((uint32_t)lut[cB * 256 + bB] << 16);
+        }
+        *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah) ^ asw) << 4)) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah + 1) ^ asw) << 4)) = make_uint4(o[4], o[5], o[6], o[7]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4 *>(Ws + tid * 64 + ((c ^ wsw) << 4)) = wv[c];
+    };
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int nk = KC / BK;
+    load(0);
+    __syncthreads();  // the LUT
+    store(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) load(kt + 1);  // in flight under this step's MFMAs
+        const uint8_t *As = smem + (kt & 1) * SLOT;
+        const uint8_t *Ws = As + A_BYTES;
+        bf16x8 wf[4], af[8];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+            wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + (wave * 64 + ni * 16 + li) * 64 + fchunk);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(As + (mi * 16 + li) * 64 + fchunk);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
+        if (kt + 1 < nk) store((kt + 1) & 1, kt + 1);  // the slot step kt - 1 read (closed by the last barrier)
+        __syncthreads();
+    }
+    w2_epilogue<EPI_PATCH_F32>(a, acc, smem, m0, n0);
+}
 
 // Skinny GEMM for M <= 256 (the last layer's CLS rows: O-proj, fc1, fc2 with
 // M = images in the slice).  A 256-row tile kernel would put the whole launch on
@@ -721,6 +836,15 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
 // 256, interleaved A/B in tools/gemm_calib.py), row-major otherwise (fc2 prefers
 // it by 2 %).
 inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
+
+// Implicit-GEMM patch embedding: M = images × patches rows, N = hidden, K = 3·P² (P = 16)
+inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
+    RC_REQUIRE(a.img && a.lut && a.img_size % 16 == 0 && a.N % 256 == 0 && a.K == 3 * 16 * 16 && a.M >= 1,
+               RC_ERR_UNSUPPORTED, "patch GEMM: 16x16 patches, N % 256 == 0");
+    const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
+    hipLaunchKernelGGL(patch_gemm_kernel<16>, dim3(ntm * ntn), dim3(256), 0, s, a);
+    RC_LAUNCH_CHECK();
+}
 
 // rows the A buffer must provide beyond M (the kernels read whole tiles)
 inline int gemm_row_pad() { return 256; }

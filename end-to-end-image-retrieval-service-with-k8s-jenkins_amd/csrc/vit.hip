@@ -4,11 +4,13 @@
 //
 // HBM layout per model (bf16 GEMM operands, f32 residual stream):
 //   weights   W_qkv [3H][H] (q,k,v rows concatenated), W_o [H][H], W_fc1 [MLP][H],
-//             W_fc2 [H][MLP], W_patch [H][3*P*P] — bf16, nn.Linear [out][in];
+//             W_fc2 [H][MLP] — bf16, nn.Linear [out][in]; W_patch [H][P·P·3] bf16 with
+//             K ordered (ky, kx, c) for the implicit-GEMM patch embedding;
 //             biases / LayerNorm params / cls / pos — f32
 //   workspace (sized for max_batch images, rows padded to the GEMM tile):
-//             patches bf16 [Pp][3P²], hidden f32 [Mp][H], ln bf16 [Mp][H],
-//             qkv bf16 [Mp][3H], attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
+//             hidden f32 [Mp][H], ln bf16 [Mp][H] (LayerNorm output, or bf16(x) under
+//             the LayerNorm fold, with ln_stats f32 [Mp][3][2]), qkv bf16 [Mp][3H],
+//             attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -125,17 +127,18 @@ struct rc_model {
     int resample = RC_RESAMPLE_BICUBIC;
     double rescale = 1.0 / 255.0;
     float mean[3] = {0.485f, 0.456f, 0.406f}, std_[3] = {0.229f, 0.224f, 0.225f};
-    float *lut = nullptr;
+    float *lut = nullptr;          // [3][256] f32: rescale→normalize of each u8 (pixel_values)
+    uint16_t *lut16 = nullptr;     // the same rounded to bf16 (the patch GEMM's A operand)
     std::map<std::pair<int, int>, DeviceCoeffs> coeff_cache;  // (in, out) → coeffs
     // workspace
-    int Mp = 0, Pp = 0;
-    uint16_t *patches = nullptr, *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
+    int Mp = 0;
+    uint16_t *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
     float *ln_stats = nullptr;     // [Mp][3][2] LayerNorm-fold partials (per 256-column tile: mean, M2)
     bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
     bool cls_only_last = true;     // rc_model_set_last_layer / RC_EMBED_FULL_LAST=1
-    float *cls_hidden = nullptr;
+    float *cls_hidden = nullptr, *cls_stats = nullptr;
     uint16_t *cls_ln = nullptr, *cls_attn = nullptr, *cls_mlp = nullptr;
     uint8_t *resized = nullptr, *resize_tmp = nullptr;
     size_t resize_tmp_bytes = 0;
@@ -248,6 +251,10 @@ void build_lut(rc_model *m) {
         }
     if (!m->lut) m->lut = (float *)m->alloc(sizeof(h));
     RC_HIP(hipMemcpy(m->lut, h, sizeof(h), hipMemcpyHostToDevice));
+    uint16_t h16[3 * 256];
+    for (int i = 0; i < 3 * 256; ++i) h16[i] = host_f2bf(h[i]);
+    if (!m->lut16) m->lut16 = (uint16_t *)m->alloc(sizeof(h16));
+    RC_HIP(hipMemcpy(m->lut16, h16, sizeof(h16), hipMemcpyHostToDevice));
 }
 
 // LayerNorm fold of one nn.Linear W [N][K] after LayerNorm(γ, β) (vit_kernels.h):
@@ -389,22 +396,35 @@ void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *
                        scale * 1.4426950408889634f);
     RC_LAUNCH_CHECK();
     m->timers[T_ATTN].end(ta, s, 4.0 * items * (double)T * (H / c.heads));
-    gemm<EPI_RESID_F32>(m, GemmArgs{ac, L.w_o, L.b_o, n, H, H, nullptr, hc, nullptr, 1}, s);
-    layernorm(m, hc, L.ln2_w, L.ln2_b, lc, n, s);
-    gemm<EPI_GELU_BF16>(m, GemmArgs{lc, L.w_fc1, L.b_fc1, n, c.mlp, H, mc, nullptr, nullptr, 1}, s);
+    GemmArgs o{ac, L.w_o, L.b_o, n, H, H, nullptr, hc, nullptr, 1};
+    if (m->ln_fold) {  // LN2 folded into fc1, as in the other layers
+        float *st = m->cls_stats + (int64_t)i0 * 2 * LN_TILES;
+        o.ln_x = lc;
+        o.ln_stats = st;
+        gemm<EPI_RESID_F32>(m, o, s);
+        GemmArgs f{lc, L.w_fc1_f, L.b_fc1_f, n, c.mlp, H, mc, nullptr, nullptr, 1};
+        f.ln_c = L.c_fc1;
+        f.ln_stats = st;
+        f.ln_eps = c.ln_eps;
+        gemm<EPI_GELU_BF16_LN>(m, f, s);
+    } else {
+        gemm<EPI_RESID_F32>(m, o, s);
+        layernorm(m, hc, L.ln2_w, L.ln2_b, lc, n, s);
+        gemm<EPI_GELU_BF16>(m, GemmArgs{lc, L.w_fc1, L.b_fc1, n, c.mlp, H, mc, nullptr, nullptr, 1}, s);
+    }
     gemm<EPI_RESID_F32>(m, GemmArgs{mc, L.w_fc2, L.b_fc2, n, H, c.mlp, nullptr, hc, nullptr, 1}, s);
 }
 
-// Encoder for images [i0, i0 + n) of the batch (their patches already built):
-// CLS + pos, patch GEMM, 12 layers, final LN on the CLS rows.  Every buffer is
-// addressed from the first image's rows, so two parts of a batch can run on two
-// streams at once (GEMM A tiles may read up to 255 rows past a part's last row;
-// those rows are allocated and their results are never stored).
-void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s) {
+// Encoder for images [i0, i0 + n) of the batch (u8 S x S x 3 images at `images`,
+// already resized): CLS + pos, implicit-GEMM patch embedding, 12 layers, final LN
+// on the CLS rows.  Every buffer is addressed from the first image's rows, so two
+// parts of a batch can run on two streams at once (GEMM A tiles may read up to 255
+// rows past a part's last row; those rows are allocated and their results are
+// never stored).
+void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float *normed, hipStream_t s) {
     const auto &c = m->cfg;
-    const int H = c.hidden, T = m->tokens, M = n * T;
+    const int H = c.hidden, T = m->tokens, M = n * T, S = c.image_size;
     const int64_t r0 = (int64_t)i0 * T;  // first token row of this part
-    uint16_t *patches = m->patches + (int64_t)i0 * m->npatch * m->kpatch;
     float *hidden = m->hidden + r0 * H;
     uint16_t *ln = m->ln + r0 * H, *qkv = m->qkv + r0 * 3 * H, *attn = m->attn + r0 * H;
     uint16_t *mlp = m->mlp + r0 * c.mlp;
@@ -425,8 +445,16 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
     hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, hidden, T, H, m->cls, m->pos, fold ? ln : nullptr,
                        fold ? st : nullptr);
     RC_LAUNCH_CHECK();
-    gemm<EPI_PATCH_F32>(m, produce(GemmArgs{patches, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden,
-                                            m->pos, T}, true), s);
+    {
+        GemmArgs a = produce(GemmArgs{nullptr, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden, m->pos,
+                                      T}, true);
+        a.img = images + (int64_t)i0 * S * S * 3;
+        a.lut = m->lut16;
+        a.img_size = S;
+        const int t0 = m->timers[T_GEMM].begin(s);
+        launch_patch_gemm(a, s);
+        m->timers[T_GEMM].end(t0, s, 2.0 * a.M * a.N * a.K);
+    }
     // 3. encoder layers
     const float scale = 1.0f / std::sqrt((float)(H / c.heads));
     for (int l = 0; l < c.layers; ++l) {
@@ -482,27 +510,25 @@ void encode(rc_model *m, int i0, int n, float *raw, float *normed, hipStream_t s
 void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw, float *normed, hipStream_t s) {
     const auto &c = m->cfg;
     const int S = c.image_size;
-    // 1. preprocess: resize (if needed) + rescale/normalize/im2col → bf16 patches
+    // 1. preprocess: Pillow-exact resize if needed; rescale/normalize is folded into the
+    //    patch GEMM's A loads (a bf16 LUT), so the u8 images are the GEMM's input
     const int tp = m->timers[T_PRE].begin(s);
     const uint8_t *src = resize_batch(m, images, n, h, w, s);
-    hipLaunchKernelGGL(patchify_kernel<16>, dim3(grid_for((int64_t)n * m->npatch * (m->kpatch / 8))), dim3(256), 0, s, src,
-                       m->lut, m->patches, n, S);
-    RC_LAUNCH_CHECK();
-    m->timers[T_PRE].end(tp, s, (double)n * S * S * 3 + (double)n * m->npatch * m->kpatch * 2);
+    m->timers[T_PRE].end(tp, s, (h == S && w == S) ? 0.0 : (double)n * (h * w + S * S) * 3);
     // 2-4. encoder: one stream, or P parts of the batch on P streams so that one
     // part's memory-bound kernels (LayerNorm, attention) and GEMM epilogue store
     // bursts overlap another part's MFMA main loops
     int parts = std::max(1, std::min(m->split, kMaxParts));
     while (parts > 1 && n < parts * m->split_min) --parts;
     if (parts == 1) {
-        encode(m, 0, n, raw, normed, s);
+        encode(m, src, 0, n, raw, normed, s);
         return;
     }
     RC_HIP(hipEventRecord(m->ev_fork, s));
     for (int p = 1; p < parts; ++p) RC_HIP(hipStreamWaitEvent(m->sp[p], m->ev_fork, 0));
     for (int p = 0; p < parts; ++p) {
         const int i0 = (int)((int64_t)n * p / parts), i1 = (int)((int64_t)n * (p + 1) / parts);
-        encode(m, i0, i1 - i0, raw, normed, p == 0 ? s : m->sp[p]);
+        encode(m, src, i0, i1 - i0, raw, normed, p == 0 ? s : m->sp[p]);
     }
     for (int p = 1; p < parts; ++p) {
         RC_HIP(hipEventRecord(m->ev_join[p], m->sp[p]));
@@ -534,8 +560,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             const int B = cfg->max_batch, H = cfg->hidden;
             // + one tile: the second half of a split batch reads whole tiles past its last row
             m->Mp = round_up(B * m->tokens, gemm_row_pad()) + gemm_row_pad();
-            m->Pp = round_up(B * m->npatch, gemm_row_pad()) + gemm_row_pad();
-            m->patches = (uint16_t *)m->alloc((size_t)m->Pp * m->kpatch * 2);
             m->hidden = (float *)m->alloc((size_t)m->Mp * H * 4);
             m->ln_stats = (float *)m->alloc((size_t)m->Mp * 2 * LN_TILES * 4);
             RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * 2 * LN_TILES * 4));  // pad rows: finite scales
@@ -546,6 +570,8 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->resized = (uint8_t *)m->alloc((size_t)B * cfg->image_size * cfg->image_size * 3);
             const int Cp = B + gemm_row_pad();  // compact CLS streams (+ the rows a tile reads past n)
             m->cls_hidden = (float *)m->alloc((size_t)Cp * H * 4);
+            m->cls_stats = (float *)m->alloc((size_t)Cp * 2 * LN_TILES * 4);
+            RC_HIP(hipMemset(m->cls_stats, 0, (size_t)Cp * 2 * LN_TILES * 4));
             m->cls_ln = (uint16_t *)m->alloc((size_t)Cp * H * 2);
             m->cls_attn = (uint16_t *)m->alloc((size_t)Cp * H * 2);
             m->cls_mlp = (uint16_t *)m->alloc((size_t)Cp * cfg->mlp * 2);
@@ -555,7 +581,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->cls_mlp, 0, (size_t)Cp * cfg->mlp * 2));
             if (const char *fl = std::getenv("RC_EMBED_FULL_LAST")) m->cls_only_last = std::atoi(fl) == 0;
             // pad rows are read by the GEMM tiles: keep them finite (zero) forever
-            RC_HIP(hipMemset(m->patches, 0, (size_t)m->Pp * m->kpatch * 2));
             RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
             RC_HIP(hipMemset(m->ln, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->qkv, 0, (size_t)m->Mp * 3 * H * 2));
@@ -625,7 +650,17 @@ int rc_model_finalize(rc_model *m) {
         for (auto &kv : m->shapes)
             RC_REQUIRE(m->host.count(kv.first), RC_ERR_STATE, "weight not set: " + kv.first);
         auto &h = m->host;
-        m->w_patch = upload_bf16(m, {&h["embeddings.patch_embeddings.projection.weight"]});
+        {   // conv weight [H][3][P][P] → [H][(ky·P + kx)·3 + c]: the implicit GEMM's K order
+            const auto &wc = h["embeddings.patch_embeddings.projection.weight"];
+            const int P = m->cfg.patch, Hd = m->cfg.hidden;
+            std::vector<float> wp(wc.size());
+            for (int n = 0; n < Hd; ++n)
+                for (int cc = 0; cc < 3; ++cc)
+                    for (int ky = 0; ky < P; ++ky)
+                        for (int kx = 0; kx < P; ++kx)
+                            wp[((size_t)n * P * P + ky * P + kx) * 3 + cc] = wc[(((size_t)n * 3 + cc) * P + ky) * P + kx];
+            m->w_patch = upload_bf16(m, {&wp});
+        }
         m->b_patch = upload_f32(m, h["embeddings.patch_embeddings.projection.bias"]);
         m->cls = upload_f32(m, h["embeddings.cls_token"]);
         m->pos = upload_f32(m, h["embeddings.position_embeddings"]);

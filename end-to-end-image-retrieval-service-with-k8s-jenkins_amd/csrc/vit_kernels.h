@@ -2,8 +2,8 @@
 //
 // Reference arithmetic (transformers models/vit_msn/modeling_vit_msn.py, called
 // from embedding/main.py:111-113):
-//   patch embed Conv2d(3,768,16,16) (:57)  → gemm_bf16_kernel<EPI_PATCH_F32> on an
-//                                            im2col'd A built by patchify_kernel
+//   patch embed Conv2d(3,768,16,16) (:57)  → patch_gemm_kernel (gemm.h): implicit GEMM
+//                                            reading the u8 images through a bf16 LUT
 //   q/k/v/o, fc1, fc2 nn.Linear (:199-202,243-244) → gemm_bf16_kernel (bias / GELU /
 //                                            residual epilogues fused)
 //   LayerNorm eps 1e-6 (:258-259,327)      → layernorm_kernel (f32 in, bf16 out)
@@ -11,8 +11,8 @@
 //   last_hidden_state[:,0,:] (main.py:113) → cls_final_kernel (final LN on the
 //                                            CLS rows, raw + L2-normalised outputs)
 // Preprocessing (ViTImageProcessor, main.py:107): resize_{h,v}_kernel (Pillow
-// fixed-point resample), patchify_kernel (rescale+normalize via an exact f32 LUT,
-// HWC→im2col, bf16 cast).
+// fixed-point resample); rescale+normalize is an exact f32 LUT, applied inside the
+// patch GEMM's A loads (and by pixel_values_kernel for the parity hook).
 #pragma once
 
 #include "rc_common.h"
@@ -50,6 +50,11 @@ struct GemmArgs {
     float *ln_stats = nullptr;
     const float *ln_c = nullptr;
     float ln_eps = 1e-6f;
+    // implicit-GEMM patch embedding (patch_gemm_kernel): A[m][k] is read from the u8
+    // HWC images through a bf16 LUT of rescale→normalize instead of an im2col buffer
+    const uint8_t *img = nullptr;  // [images][S][S][3]
+    const uint16_t *lut = nullptr; // [3][256] bf16 bits
+    int img_size = 0;              // S
 };
 
 // ------------------------------------------------------------ LayerNorm fold
@@ -733,30 +738,6 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t *__restrict
         o[0] = clip8_fixed(a0);
         o[1] = clip8_fixed(a1);
         o[2] = clip8_fixed(a2);
-    }
-}
-
-// u8 [n, S, S, 3] → im2col'd bf16 A [n*(S/P)^2, 3*P*P], column c*P*P + kh*P + kw,
-// value = lut[c][u] (the exact f32 of rescale-then-normalize), 8 outputs per thread.
-template <int P>
-__global__ __launch_bounds__(256) void patchify_kernel(const uint8_t *__restrict__ img, const float *__restrict__ lut,
-                                                      uint16_t *__restrict__ A, int n, int S) {
-    constexpr int KC = 3 * P * P;
-    const int gp = S / P, np = gp * gp;
-    const int64_t total = (int64_t)n * np * (KC / 8);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-        const int chunk = (int)(i % (KC / 8));
-        const int64_t m = i / (KC / 8);
-        const int b = (int)(m / np), p = (int)(m % np);
-        const int py = p / gp, px = p % gp;
-        const int col0 = chunk * 8;
-        const int c = col0 / (P * P), kh = (col0 % (P * P)) / P, kw0 = col0 % P;
-        const uint8_t *src = img + (((int64_t)b * S + py * P + kh) * S + px * P + kw0) * 3 + c;
-        const float *l = lut + c * 256;
-        uint32_t w[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) w[t] = pack_bf16x2(l[src[6 * t]], l[src[6 * t + 3]]);
-        *reinterpret_cast<uint4 *>(A + m * KC + col0) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
