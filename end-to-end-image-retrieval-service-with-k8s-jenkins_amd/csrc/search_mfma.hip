@@ -44,11 +44,31 @@ template <> struct MfmaOp<f16_t> {
     static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
     }
+    // A in VGPRs, B in AGPRs, C/D in VGPRs (filter_qs_kernel at QT = 4, whose query
+    // fragments fill the AGPR file).  The builtin would copy an AGPR-resident B to
+    // VGPRs first; inline asm is invisible to the hazard recognizer, so the caller
+    // waits out the XDL-write -> VALU-read latency before touching C.
+    static __device__ __forceinline__ void mma_vav(v8 a, v8 b, f32x4_t &c) {
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    }
+    static __device__ __forceinline__ void mma_vav0(v8 a, v8 b, f32x4_t &c) {
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
+    }
 };
 template <> struct MfmaOp<bf16_t> {
     typedef __bf16 v8 __attribute__((ext_vector_type(8)));
     static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    // A in VGPRs, B in AGPRs, C/D in VGPRs (filter_qs_kernel at QT = 4, whose query
+    // fragments fill the AGPR file).  The builtin would copy an AGPR-resident B to
+    // VGPRs first; inline asm is invisible to the hazard recognizer, so the caller
+    // waits out the XDL-write -> VALU-read latency before touching C.
+    static __device__ __forceinline__ void mma_vav(v8 a, v8 b, f32x4_t &c) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    }
+    static __device__ __forceinline__ void mma_vav0(v8 a, v8 b, f32x4_t &c) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
     }
 };
 
@@ -291,18 +311,33 @@ __global__ __launch_bounds__(512, 1) void filter_gemm_kernel(FilterArgs a) {
 // MFMA roles as above (A = index rows, B = queries): lane (li, g) of acc[rf][qt]
 // holds rows 16·rf + 4g + j of query 16·qt + li.  Same thresholds, candidate
 // appends and exactness argument as filter_gemm_kernel.
-constexpr int QS_RT = 128, QS_NS = 8, QS_QT = 2, QS_WAVES = 8;
-#ifndef QS_STAGGER
-#define QS_STAGGER 0
-#endif
+// QT (queries per wave / 16) sets the LDS read rate: every row fragment read
+// feeds QT MFMAs.  QT = 2 (8 waves, 2 per SIMD) reads one ds_read_b128 per two
+// 16x16x32 MFMAs from each of 8 waves — 256 B/clk/CU, the LDS array's limit, which
+// held the round-1 kernel at mfma_busy 0.64; QT = 4 (4 waves, one per SIMD, the
+// 2·NKT query fragments of 64 queries in 256 VGPRs) halves that.
+// Row-tile height: 8 row fragments at QT = 2, 4 at QT = 4 (acc = 16·RF·QT f32 per
+// lane stays 64-128 registers next to the 64·QT·NKT/... query fragments).
+constexpr int qs_rows(int qt) { return qt == 4 ? 64 : 128; }
+// LDS ring depth in K-steps: QS_NS - 2 steps in flight (96-112 KB) cover the HBM
+// latency of a tile's first touch at either QT.
+constexpr int qs_stages(int qt) { return qt == 4 ? 16 : 8; }
 
-// ABL (A/B diagnostics, RC_FILTER_ABL; 0 in production): bit0 no DMA in the loop,
-// bit1 no MFMA, bit2 no fragment reads (MFMAs on the query registers).
-template <typename T, int NKT, int ABL = 0>
-__global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
+// ABL (A/B diagnostics, diagnostic builds only; 0 in production): bit0 no DMA in the
+// loop, bit1 no MFMA, bit2 no fragment reads (MFMAs on the query registers), bit3 no
+// epilogue.
+// (QS_WAVES is derived inside: a dependent default template argument on a __global__
+// template makes hipcc mangle the host stub differently from its launch sites.)
+template <typename T, int NKT, int QS_QT, int ABL = 0>  // 256 queries per block
+__global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a) {
+    constexpr int QS_WAVES = 16 / QS_QT;
+    constexpr int QS_RT = qs_rows(QS_QT), RF = QS_RT / 16, QS_NS = qs_stages(QS_QT);
+    // QT = 4: query fragments pinned in AGPRs, MFMAs by inline asm, row-fragment reads
+    // software-pipelined (one wave per SIMD: no partner wave hides their latency)
+    constexpr bool PIPE = QS_QT == 4;
     using Op = MfmaOp<T>;
     using v8 = typename Op::v8;
-    constexpr int STEP_BYTES = QS_RT * 128;  // 16 KB
+    constexpr int STEP_BYTES = QS_RT * 128;  // 16 KB at QT = 2
     __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -339,11 +374,15 @@ __global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
     for (int qt = 0; qt < QS_QT; ++qt) {
         asm volatile("" ::"v"(thr[qt]));
 #pragma unroll
-        for (int kk = 0; kk < 2 * NKT; ++kk) asm volatile("" ::"v"(qf[qt][kk]));
+        for (int kk = 0; kk < 2 * NKT; ++kk) {
+            if constexpr (PIPE) asm volatile("" ::"a"(qf[qt][kk]));
+            else asm volatile("" ::"v"(qf[qt][kk]));
+        }
     }
+    if constexpr (PIPE) asm volatile("s_nop 7");  // AGPR writes -> MFMA B reads (inline asm: no hazard pass)
 
-    // step t = (tile, k-step): 16 pieces of 1 KB (8 rows x 128 B); wave w issues pieces w + 8i.
-    constexpr int PPW = 16 / QS_WAVES;
+    // step t = (tile, k-step): 2·RF pieces of 1 KB (8 rows x 128 B); wave w issues pieces w + QS_WAVES·i.
+    constexpr int PPW = 2 * RF / QS_WAVES;
     uint32_t loff[PPW];  // byte offset of this lane's 16 B within the step's rows
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
@@ -357,73 +396,119 @@ __global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(Rg + (int64_t)tile * QS_RT * ld + ks * 64), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-        for (int i = 0; i < PPW; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(base + (wave + QS_WAVES * i) * 1024), 16, loff[i],
-                                                     0, 0, 0);
+        for (int i = 0; i < PPW; ++i) {
+            // (the builtin's operands kept non-dependent: a template-dependent operand defers
+            // its target check to instantiation, where the host pass drops the kernel's stub)
+            lds_void *dst = (lds_void *)(base + (wave + QS_WAVES * i) * 1024);
+            const uint32_t off = loff[i];
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, 0);
+        }
     };
-    // one barrier per PAIR of k-steps (nsteps is even): steps t, t+1 land together,
-    // steps t+6, t+7 go into the two slots freed by t-2, t-1; 6 steps in flight
-    for (int t = 0; t < min(QS_NS - 2, nsteps); ++t) issue(t);
+    // one barrier per SPS k-steps (2 at QT = 2, 4 at QT = 4; nsteps is a multiple):
+    // steps t..t+SPS-1 land together, steps t+NS-SPS..t+NS-1 go into the slots freed
+    // by t-SPS..t-1; NS - SPS steps in flight
+#ifdef RC_QS_SPS
+    constexpr int SPS = RC_QS_SPS;
+#else
+    constexpr int SPS = (PIPE && NKT % 4 == 0) ? 4 : 2;
+#endif
+    for (int t = 0; t < min(QS_NS - SPS, nsteps); ++t) issue(t);
 
-    f32x4_t acc[8][QS_QT];
+    f32x4_t acc[RF][QS_QT];
     for (int tile = 0; tile < ntiles; ++tile) {
 #pragma unroll
-        for (int rf = 0; rf < 8; ++rf)
+        for (int rf = 0; rf < RF; ++rf)
 #pragma unroll
-            for (int qt = 0; qt < QS_QT; ++qt) acc[rf][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            for (int qt = 0; qt < QS_QT; ++qt)
+                if constexpr (!PIPE) acc[rf][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};  // PIPE: first MFMA takes C = 0
 #pragma unroll
-        for (int kp = 0; kp < NKT / 2; ++kp) {
-            const int t = tile * NKT + 2 * kp;
-            // steps t, t+1 landed: the 4 younger steps t+2..t+5 (PPW = 2 DMAs each) may be in flight
-            static_assert(PPW == 2 && NKT % 2 == 0, "vmcnt below assumes 2 DMAs per wave per step, paired steps");
-            if (t + QS_NS - 3 < nsteps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int kp = 0; kp < NKT / SPS; ++kp) {
+            const int t = tile * NKT + SPS * kp;
+            // steps t..t+SPS-1 landed: the NS - 2·SPS younger steps (PPW DMAs each) may be in flight
+            static_assert(NKT % SPS == 0 && (QS_NS - 2 * SPS) * PPW < 64, "whole sync groups; vmcnt is 6 bits");
+            if (t + QS_NS - SPS - 1 < nsteps) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((QS_NS - 2 * SPS) * PPW) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             asm volatile("" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // every wave's DMA of t, t+1 landed; slots of t-2, t-1 are free
+            __builtin_amdgcn_s_barrier();  // every wave's DMA of t..t+SPS-1 landed; slots of t-SPS..t-1 are free
             asm volatile("" ::: "memory");
-            if (QS_STAGGER && wave >= 4) __builtin_amdgcn_s_sleep(QS_STAGGER);  // SIMD partners out of phase
-            if (!(ABL & 1) && t + QS_NS - 2 < nsteps) issue(t + QS_NS - 2);
-            if (!(ABL & 1) && t + QS_NS - 1 < nsteps) issue(t + QS_NS - 1);
-            // per k-step and k half: 2 groups of 4 row fragments (4 reads in flight, then
-            // their 8 MFMAs with counted lgkmcnt waits; the SIMD partner wave's MFMAs cover
-            // the rest).  Row r = 16 rf + li: its swizzle (r >> 1) & 7 = (li >> 1) & 7 does
-            // not depend on rf.
 #pragma unroll
-            for (int kl = 0; kl < 2; ++kl) {
-                const uint8_t *S = smem + ((t + kl) % QS_NS) * STEP_BYTES;
-                const int ks = 2 * kp + kl;
+            for (int j = QS_NS - SPS; j < QS_NS; ++j)
+                if (!(ABL & 1) && t + j < nsteps) issue(t + j);
+            // groups of 4 row fragments, (k half kl, k sub-chunk sh, row quarter rh): 4 reads,
+            // then their 4·QT MFMAs with counted lgkmcnt waits.  Row r = 16 rf + li: its
+            // swizzle (r >> 1) & 7 = (li >> 1) & 7 does not depend on rf.  At QT = 2 the
+            // SIMD partner wave's MFMAs cover the read latency; at QT = 4 (one wave per
+            // SIMD) the reads of group gi + 1 are issued before the MFMAs of group gi.
+            constexpr int RH = RF / 4, NG = SPS * 2 * RH;
+            auto frag_ptr = [&](int gi) {
+                const int kl = gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
+                return smem + ((t + kl) % QS_NS) * STEP_BYTES + li * 128 + (((sh * 4 + g) ^ ((li >> 1) & 7)) << 4) +
+                       rh * 4 * 2048;
+            };
+            auto load_group = [&](int gi, v8 *dst) {
+                const uint8_t *Sr = frag_ptr(gi);
+                const int ks = SPS * kp + gi / (2 * RH), sh = (gi / RH) % 2;
 #pragma unroll
-                for (int sh = 0; sh < 2; ++sh) {
-                    const uint8_t *Sr = S + li * 128 + (((sh * 4 + g) ^ ((li >> 1) & 7)) << 4);
+                for (int i = 0; i < 4; ++i)
+                    dst[i] = (ABL & 4) ? qf[i & 1][(ks * 2 + sh + i) % (2 * NKT)]
+                                       : *reinterpret_cast<const v8 *>(Sr + i * 2048);
+            };
+            v8 rfr[2][4];
+            if constexpr (PIPE) load_group(0, rfr[0]);
 #pragma unroll
-                    for (int rh = 0; rh < 2; ++rh) {
-                        v8 rfr[4];
+            for (int gi = 0; gi < NG; ++gi) {
+                const int ks = SPS * kp + gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
+                v8 *cur = rfr[PIPE ? (gi & 1) : 0];
+                if constexpr (PIPE) {
+                    if (gi + 1 < NG) load_group(gi + 1, rfr[(gi + 1) & 1]);
+                } else {
+                    load_group(gi, cur);
+                }
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            rfr[i] = (ABL & 4) ? qf[i & 1][(ks * 2 + sh + i) % (2 * NKT)]
-                                               : *reinterpret_cast<const v8 *>(Sr + (rh * 4 + i) * 2048);
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
-#pragma unroll
-                            for (int qt = 0; qt < QS_QT; ++qt)
-                                if constexpr (!(ABL & 2))
-                                    acc[rh * 4 + i][qt] = Op::mma(rfr[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
-                                else
-                                    asm volatile("" ::"v"(rfr[i]));
-                        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-                    }
+                    for (int qt = 0; qt < QS_QT; ++qt)
+                        if constexpr (ABL & 2)
+                            asm volatile("" ::"v"(cur[i]));
+                        else if constexpr (!PIPE)
+                            acc[rh * 4 + i][qt] = Op::mma(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
+                        else if (kp == 0 && gi < RH)
+                            Op::mma_vav0(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
+                        else
+                            Op::mma_vav(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
+                if constexpr (!PIPE) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
                 }
             }
         }
+        if constexpr (PIPE) {
+            // XDL write -> VALU read of acc: >= 19 wait states for a 16-pass MFMA; the
+            // empty asm per accumulator keeps every epilogue read behind the nops
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
+#pragma unroll
+            for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+                for (int qt = 0; qt < QS_QT; ++qt) asm volatile("" : "+v"(acc[rf][qt]));
+        }
         // ---- epilogue of row tile rt0 + tile: candidates s' >= thr[q]
         const int64_t rbase = a.r_begin + (rt0 + tile) * QS_RT + 4 * g;
+        if constexpr (ABL & 8) {  // diagnostics: no epilogue (accumulators kept live)
+#pragma unroll
+            for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+                for (int qt = 0; qt < QS_QT; ++qt) asm volatile("" ::"v"(acc[rf][qt]));
+            continue;
+        }
 #pragma unroll
         for (int qt = 0; qt < QS_QT; ++qt) {
             const float th = thr[qt];
             float m = -INFINITY;
 #pragma unroll
-            for (int rf = 0; rf < 8; ++rf) {
+            for (int rf = 0; rf < RF; ++rf) {
                 const f32x4_t v = acc[rf][qt];
                 m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
             }
@@ -431,7 +516,7 @@ __global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
             if (m >= th) {
                 const int q = q0 + qt * 16 + li;
 #pragma unroll
-                for (int rf = 0; rf < 8; ++rf)
+                for (int rf = 0; rf < RF; ++rf)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int64_t row = rbase + rf * 16 + j;
@@ -574,12 +659,12 @@ void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipSt
     }
 }
 
-// Filter kernel choice: 0 = auto (query-stationary for ld <= 512), 1 = the
-// two-operand-streaming kernel (RC_FILTER_VARIANT, read once; A/B runs).
-inline int filter_variant() {
+// Queries per wave of the query-stationary filter kernel (16·QT): 4 unless
+// RC_FILTER_QT=2 (read once; A/B of the LDS-read-rate trade-off above).
+inline int filter_qt() {
     static const int v = [] {
-        const char *d = std::getenv("RC_FILTER_VARIANT");
-        return d ? std::atoi(d) : 0;
+        const char *d = std::getenv("RC_FILTER_QT");
+        return d ? std::atoi(d) : 4;
     }();
     return v;
 }
@@ -610,20 +695,32 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
         FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), b0, b1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
         const int slot = timer ? timer->begin(s) : -1;
         const int nkt = (int)(p.ld / 64);
-        if (filter_variant() != 1 && (nkt == 2 || nkt == 4 || nkt == 8)) {
-            fa.tiles_per_chunk = ((b1 - b0 + QS_RT - 1) / QS_RT + nchunk - 1) / nchunk;
-            const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * QS_WAVES);
-            static const int abl = [] {
-                const char *d = std::getenv("RC_FILTER_ABL");
-                return d ? std::atoi(d) : 0;
-            }();
-            if (nkt == 8 && abl == 1) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 1>), gr, bl, 0, s, fa);
-            else if (nkt == 8 && abl == 2) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 2>), gr, bl, 0, s, fa);
-            else if (nkt == 8 && abl == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 4>), gr, bl, 0, s, fa);
-            else if (nkt == 8 && abl == 6) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 6>), gr, bl, 0, s, fa);
-            else if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8>), gr, bl, 0, s, fa);
-            else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4>), gr, bl, 0, s, fa);
-            else hipLaunchKernelGGL((filter_qs_kernel<T, 2>), gr, bl, 0, s, fa);
+        if (nkt == 2 || nkt == 4 || nkt == 8) {
+            const int qt = filter_qt();
+            const int64_t rt = qs_rows(qt);
+            fa.tiles_per_chunk = ((b1 - b0 + rt - 1) / rt + nchunk - 1) / nchunk;
+            const dim3 gr((unsigned)(nchunk * nqb));
+#if defined(RC_GEMM_ABLATION)
+            static const int abl = std::getenv("RC_FILTER_ABL") ? std::atoi(std::getenv("RC_FILTER_ABL")) : 0;
+            if (abl && nkt == 8) {
+                const dim3 bl(64 * 16 / qt);
+#define RC_ABL(Q, A) \
+    if (qt == Q && abl == A) hipLaunchKernelGGL((filter_qs_kernel<T, 8, Q, A>), gr, bl, 0, s, fa);
+                RC_ABL(4, 8) RC_ABL(4, 9) RC_ABL(4, 12) RC_ABL(4, 13) RC_ABL(2, 8) RC_ABL(2, 9) RC_ABL(2, 12) RC_ABL(2, 13)
+#undef RC_ABL
+            } else
+#endif
+            if (qt == 4) {
+                const dim3 bl(64 * 4);
+                if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 4>), gr, bl, 0, s, fa);
+                else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4, 4>), gr, bl, 0, s, fa);
+                else hipLaunchKernelGGL((filter_qs_kernel<T, 2, 4>), gr, bl, 0, s, fa);
+            } else {
+                const dim3 bl(64 * 8);
+                if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 2>), gr, bl, 0, s, fa);
+                else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4, 2>), gr, bl, 0, s, fa);
+                else hipLaunchKernelGGL((filter_qs_kernel<T, 2, 2>), gr, bl, 0, s, fa);
+            }
         } else {
             hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
         }
