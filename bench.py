@@ -466,7 +466,8 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": {
-            "kernel": "gemm_pp_kernel<EPI_GELU_BF16> (fc1: M=%d N=3072 K=768)" % (B * 197),
+            "kernel": ("gemm_pp_kernel<EPI_GELU_BF16> (fc1: M=%d N=3072 K=768)" if args.no_ln_fold else
+                       "gemm_pp_kernel<EPI_GELU_BF16_LN> (fc1 with LayerNorm 2 folded in: M=%d N=3072 K=768)") % (B * 197),
             "bound": "mfma",
             "achieved": achieved,
             "peak": PEAK_BF16_TFLOPS,
@@ -558,7 +559,7 @@ def main():
             "value": nqb * args.batch_reps / bel,
             "unit": "queries/s",
             "ms_per_batch": bel / args.batch_reps * 1e3,
-            "roofline": {"kernel": "filter_qs_kernel<f16,8> (256 queries in registers x 128-row tiles, 8-deep LDS ring, candidate epilogue)",
+            "roofline": {"kernel": "filter_qs_kernel<f16,8,4> (256 queries per block, 64 per wave in AGPRs x 64-row tiles, 16-step LDS ring, candidate epilogue)",
                          "bound": "mfma", "achieved": g_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": g_tf / PEAK_BF16_TFLOPS, "traffic": load_profile_traffic("filter_f16"),
                          "avg_launch_ms": g_ms / max(g_n, 1), "launches": g_n,

@@ -64,11 +64,17 @@ def main():
     if "--json" in sys.argv:
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
     if "--latest" in sys.argv:
-        keys = {"fc1": "gemm_pp_kernel<1, 0>", "scan_f16": "scan_topk_kernel<f16_t, 4, 1, 128>",
-                "filter_f16": "filter_qs_kernel<f16_t, 8, 0>"}
+        # fc1 is EPI_GELU_BF16_LN (5) with LayerNorm folded (default), EPI_GELU_BF16 (1) without
+        keys = {"fc1": ("gemm_pp_kernel<5, 0>", "gemm_pp_kernel<1, 0>"),
+                "scan_f16": ("scan_topk_kernel<f16_t, 4, 1, 128>",),
+                "filter_f16": ("filter_qs_kernel<f16_t, 8, 4, 0>", "filter_qs_kernel<f16_t, 8, 2, 0>")}
         latest = {}
-        for key, kname in keys.items():
+        for key, knames in keys.items():
+            kname = next((k for k in knames if any(r["kernel"] == k for r in out.values())), knames[0])
             recs = [r for r in out.values() if r["kernel"] == kname]
+            if key == "fc1" and recs:  # bench prices the unsplit batch-256 launch: the largest grid
+                gmax = max(r["grid"] for r in recs)
+                recs = [r for r in recs if r["grid"] == gmax]
             if not recs or not all("hbm_read_bytes" in r and "hbm_write_bytes" in r for r in recs):
                 continue
             n = sum(r["dispatches"] for r in recs)
