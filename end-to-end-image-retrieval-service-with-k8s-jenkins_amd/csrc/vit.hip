@@ -144,9 +144,7 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
-    int attn_variant = 3;          // RC_ATTN_VARIANT=1 / 2 select the v1 / v2 kernels
-    int n_cu = 256;                // persistent grids (attention_v3_kernel)
-    int active_parts = 1;          // concurrent batch parts in flight (forward): they share the CUs
+    int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
     int split = 2;                 // batch parts encoded concurrently (RC_EMBED_SPLIT / rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -478,12 +476,6 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
         const int ta = m->timers[T_ATTN].begin(s);
         if (m->attn_variant == 1 || T > ATT2_ROWS)
             hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads, scale);
-        else if (m->attn_variant == 3 && T == 197)  // ViT-B/16 at 224x224: the token count as a constant
-            hipLaunchKernelGGL(attention_v3_kernel<197>, dim3(std::min(n * c.heads, std::max(1, m->n_cu / m->active_parts))), dim3(512), 0, s, qkv,
-                               attn, T, c.heads, n * c.heads, scale * 1.4426950408889634f);
-        else if (m->attn_variant == 3)
-            hipLaunchKernelGGL(attention_v3_kernel<0>, dim3(std::min(n * c.heads, std::max(1, m->n_cu / m->active_parts))), dim3(512), 0, s, qkv,
-                               attn, T, c.heads, n * c.heads, scale * 1.4426950408889634f);
         else if (T == 197)
             hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
@@ -528,7 +520,6 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
     // bursts overlap another part's MFMA main loops
     int parts = std::max(1, std::min(m->split, kMaxParts));
     while (parts > 1 && n < parts * m->split_min) --parts;
-    m->active_parts = parts;
     if (parts == 1) {
         encode(m, src, 0, n, raw, normed, s);
         return;
@@ -598,7 +589,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             build_lut(m);
             if (const char *gv = std::getenv("RC_GEMM_VARIANT")) m->gemm_variant = std::atoi(gv);
             if (const char *av = std::getenv("RC_ATTN_VARIANT")) m->attn_variant = std::atoi(av);
-            RC_HIP(hipDeviceGetAttribute(&m->n_cu, hipDeviceAttributeMultiprocessorCount, device));
             if (const char *sp = std::getenv("RC_EMBED_SPLIT")) m->split = std::atoi(sp);
             RC_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
             for (int p = 1; p < kMaxParts; ++p) {

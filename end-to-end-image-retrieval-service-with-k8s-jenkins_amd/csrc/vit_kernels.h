@@ -472,208 +472,6 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     }
 }
 
-// Self-attention v3: the arithmetic of attention_v2_kernel (same fragments, same
-// f32 softmax, same bf16 P, bit-identical outputs), restructured for HBM.  v2
-// runs one (image, head) per block in two phases — DMA everything, then compute
-// — and since every block is identical, the whole chip moves in lockstep: all
-// CUs load, then all compute with nothing in flight (3.9 TB/s, 49 % of HBM).
-// v3 is persistent: one 512-thread block per CU (2 waves per SIMD) walks pairs
-// p = blockIdx.x, + gridDim.x, ...; the LDS holds two pair buffers of K and V
-// (2 x 208 x 128 B each, 104 KB in all) and pair p + gridDim.x streams into the
-// idle buffer — its K/V by LDS-DMA, its query fragments into registers — while
-// pair p computes, so HBM always has the next pair's ~78 KB per CU in flight.
-// One barrier per pair: after it every wave's loads of pair p have landed and
-// every wave is done with pair p - gridDim.x, whose buffer the next DMA
-// overwrites.  Wave w takes query tiles w and w + 8 (13 tiles of 16).
-constexpr int ATT3_PIECES = 2 * ATT2_TILES * 2;  // 1-KB pieces per pair: K, V
-constexpr int ATT3_BUF = 2 * ATT2_ROWS * 128;
-
-template <int TOK>
-__global__ __launch_bounds__(512, 1) void attention_v3_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                          int tokens_rt, int heads, int npairs, float scale_log2e) {
-    constexpr int HD = 64;
-    const int tokens = TOK > 0 ? TOK : tokens_rt;
-    // two distinct LDS objects: the compiler can then prove that a DMA into one buffer
-    // does not alias the reads of the other (else it waits vmcnt(0) before every read)
-    __shared__ __attribute__((aligned(16))) uint8_t lds0[ATT3_BUF];
-    __shared__ __attribute__((aligned(16))) uint8_t lds1[ATT3_BUF];
-    const int H = heads * HD, H3 = 3 * H;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, li = lane & 15;
-    const int qq = li >> 2, pp = li & 3;
-    const int nqt = (tokens + 15) / 16;
-
-    auto pair_base = [&](int p) {
-        const int img = p / heads, h = p - img * heads;
-        return qkv + (int64_t)img * tokens * H3 + h * HD;
-    };
-    // pieces 0-25 K, 26-51 V of pair p into buffer b; wave w issues w, w+8, ...
-    auto issue = [&](int p, uint8_t *dst) {
-        const uint16_t *base = pair_base(p);
-        for (int piece = wave; piece < ATT3_PIECES; piece += 8) {
-            const bool isv = piece >= ATT2_TILES * 2;
-            const int r = (isv ? piece - ATT2_TILES * 2 : piece) * 8 + (lane >> 3);
-            const int pc = lane & 7;
-            const int c = isv ? (pc ^ (((r >> 1) & 3) << 1)) : (pc ^ ((r >> 1) & 7));
-            const int rr = r < tokens ? r : tokens - 1;
-            const uint16_t *src = base + (int64_t)rr * H3 + (isv ? 2 * H : H) + c * 8;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(dst + piece * 1024), 16, 0, 0);
-        }
-    };
-    // this wave's query fragments of pair p: tiles wave, wave + 8
-    auto load_q = [&](int p, bf16x8 (&qf)[2][2]) {
-        const uint16_t *base = pair_base(p);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = (wave + 8 * i) * 16 + li;
-            const int qc = q < tokens ? q : tokens - 1;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-                qf[i][s2] = *reinterpret_cast<const bf16x8 *>(base + (int64_t)qc * H3 + s2 * 32 + g * 8);
-        }
-    };
-
-    auto compute = [&](int p, const uint8_t *Ks, const bf16x8 (&qfa)[2][2]) {
-        const uint8_t *Vs = Ks + ATT2_ROWS * 128;
-        const int img = p / heads, h = p - img * heads;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int qt = wave + 8 * i;
-            if (qt >= nqt) break;  // wave-uniform
-            const bf16x8 *qf = qfa[i];
-            f32x4 st[ATT2_TILES];
-#pragma unroll
-            for (int t = 0; t < ATT2_TILES; ++t) {
-                st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-                const int r = t * 16 + li;
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    const int c = s2 * 4 + g;
-                    const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                    st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s2], st[t], 0, 0, 0);
-                }
-                if (t & 1) asm volatile("" ::: "memory");
-            }
-#pragma unroll
-            for (int t = 0; t < ATT2_TILES; ++t)
-                if ((t + 1) * 16 > tokens) {
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj)
-                        if (t * 16 + g * 4 + jj >= tokens) st[t][jj] = -INFINITY;
-                }
-            float mx = -INFINITY;
-#pragma unroll
-            for (int t = 0; t < ATT2_TILES; ++t)
-                mx = fmaxf(mx, fmaxf(fmaxf(st[t][0], st[t][1]), fmaxf(st[t][2], st[t][3])));
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float nmc = -mx * scale_log2e;
-            float sum = 0.f;
-#pragma unroll
-            for (int t = 0; t < ATT2_TILES; ++t)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const float pr = __builtin_amdgcn_exp2f(fmaf(st[t][jj], scale_log2e, nmc));
-                    st[t][jj] = pr;
-                    sum += pr;
-                }
-            sum += __shfl_xor(sum, 16);
-            sum += __shfl_xor(sum, 32);
-
-            f32x4 o[4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-            auto vrow_addr = [&](int row, int d) {
-                const int chunk = (2 * d + (pp >> 1)) ^ (((row >> 1) & 3) << 1);
-                return (lds_s16x4_t *)(Vs + row * 128 + chunk * 16 + (pp & 1) * 8);
-            };
-            // transposed V reads by inline asm: the builtin carries no alias information, so
-            // the compiler would wait for the next pair's in-flight LDS-DMA (vmcnt(0)) before
-            // the first of them; the asm reads' results are fenced by an explicit lgkmcnt(0)
-            // whose asm takes them as operands, so no MFMA can be scheduled above it
-            auto tr_read = [&](int row, int d) {
-                s16x4 v;
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)vrow_addr(row, d)));
-                return v;
-            };
-#pragma unroll
-            for (int tp = 0; tp < ATT2_TILES / 2; ++tp) {
-                const int t = tp * 2;
-                bf16x8 pf;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    pf[jj] = (__bf16)st[t][jj];
-                    pf[jj + 4] = (__bf16)st[t + 1][jj];
-                }
-                s16x4 lo[4], hi[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    lo[d] = tr_read(t * 16 + g * 4 + qq, d);
-                    hi[d] = tr_read(t * 16 + 16 + g * 4 + qq, d);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)"
-                             : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]),
-                               "+v"(hi[3]));
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const s16x8 vv = {lo[d][0], lo[d][1], lo[d][2], lo[d][3], hi[d][0], hi[d][1], hi[d][2], hi[d][3]};
-                    o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
-                }
-            }
-            {
-                constexpr int t = ATT2_TILES - 1;
-                s16x4 pf4;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) pf4[jj] = __builtin_bit_cast(short, (__bf16)st[t][jj]);
-                s16x4 v4[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) v4[d] = tr_read(t * 16 + g * 4 + qq, d);
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v4[0]), "+v"(v4[1]), "+v"(v4[2]), "+v"(v4[3]));
-#pragma unroll
-                for (int d = 0; d < 4; ++d) o[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(v4[d], pf4, o[d], 0, 0, 0);
-            }
-            const int q = qt * 16 + li;
-            if (q < tokens) {
-                const float inv = 1.0f / sum;
-                uint16_t *orow = out + ((int64_t)img * tokens + q) * H + h * HD;
-#pragma unroll
-                for (int d = 0; d < 4; ++d)
-                    *reinterpret_cast<uint2 *>(orow + d * 16 + g * 4) =
-                        make_uint2(pack_bf16x2(o[d][0] * inv, o[d][1] * inv), pack_bf16x2(o[d][2] * inv, o[d][3] * inv));
-            }
-        }
-    };
-
-    int p = blockIdx.x;
-    if (p >= npairs) return;  // block-uniform
-    const int step = gridDim.x;
-    bf16x8 qa[2][2], qb[2][2];  // query fragments of the even / odd pairs of this block
-    issue(p, lds0);
-    load_q(p, qa);
-    // two pairs per trip, so the register sets and LDS buffers alternate statically
-    while (true) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pair p landed (and the previous pair's stores)
-        __syncthreads();
-        if (p + step < npairs) {
-            issue(p + step, lds1);
-            load_q(p + step, qb);
-        }
-        compute(p, lds0, qa);
-        p += step;
-        if (p >= npairs) break;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (p + step < npairs) {
-            issue(p + step, lds0);
-            load_q(p + step, qa);
-        }
-        compute(p, lds1, qb);
-        p += step;
-        if (p >= npairs) break;
-    }
-}
-
 // Self-attention for one (image, head): S = 197 tokens, head dim 64.
 // K (XOR-swizzled 128-B rows) and V (160-B rows, conflict-free for the
 // transposed reads) of the head live in LDS; each wave takes 16-query tiles.

@@ -225,29 +225,3 @@ def test_ln_fold_matches_unfused_and_oracle(vitmod, weights12, cuda):
         assert 1.0 - cosine(fold[i], ref[j]) <= 2e-3
     m.close()
 
-
-@pytest.mark.parametrize("n,size", [(256, 224), (5, 224), (3, 160)])
-def test_persistent_attention_bitwise_equals_v2(vitmod, cuda, n, size, monkeypatch):
-    """attention_v3_kernel (persistent, double-buffered Q/K/V in LDS; default) performs the
-    arithmetic of attention_v2_kernel in the same order: identical embeddings bit for bit, at
-    the bench batch (more pairs than CUs: several pairs per block), at a batch with fewer pairs
-    than CUs, and at a runtime token count (160x160 → 101 tokens)."""
-    import torch
-
-    from oracle.weights import seeded_vit_msn_weights
-
-    sd = seeded_vit_msn_weights(1907, num_layers=2)
-    tokens = (size // 16) ** 2 + 1
-    sd["embeddings.position_embeddings"] = sd["embeddings.position_embeddings"][:, :tokens].copy()
-    rng = np.random.default_rng(n)
-    imgs = torch.from_numpy(rng.integers(0, 256, (n, size, size, 3), dtype=np.uint8))
-    out = {}
-    for v in ("2", "3"):
-        monkeypatch.setenv("RC_ATTN_VARIANT", v)
-        m = vitmod.VitMsnEmbedder(sd, device=0, max_batch=n, model_config={"image_size": size, "num_hidden_layers": 2})
-        m.set_last_layer(False)  # both layers through the full attention kernel
-        out[v] = m.embed(imgs)
-        torch.cuda.synchronize()
-        m.close()
-    assert torch.equal(out["2"][0], out["3"][0]) and torch.equal(out["2"][1], out["3"][1])
-    assert torch.isfinite(out["3"][0]).all()
