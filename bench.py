@@ -441,6 +441,31 @@ def main():
                                  "pipeline": "embed_jpeg_stream: host Huffman of batch i+1 (worker thread, side stream) under the GPU embed of batch i"}}
         if rank == 0 and world == 1 and not args.no_cpu:
             jpeg["cpu_baseline"] = cpu_jpeg_baseline(datas)
+        # the batched ingest core behind POST /push_images (ingesting/core.py: the reference's
+        # push_image steps per image, one decode / embed / upsert pass per batch)
+        core = importlib.import_module(f"{PKG}.ingesting.core")
+        importlib.import_module(f"{PKG}.config").Config.EMBED_MAX_BATCH = B  # the service embedder's batch
+        files = [(f"img{i}.jpg", d, "image/jpeg") for i, d in enumerate(datas[:B])]
+        ireps = 4
+        ix = importlib.import_module(f"{PKG}.index").Index("bench-ingest", dimension=768, dtype="float16",
+                                                           capacity=len(files) * (ireps + 1), device=local)
+        core.ingest_many(files, ix)  # warm: creates the service embedder
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(ireps):
+            resp = core.ingest_many(files, ix)
+        torch.cuda.synchronize()
+        barrier()
+        eli = max_over_ranks(time.perf_counter() - t0)
+        jpeg["ingest_core"] = {
+            "value": world * len(files) * ireps / eli,
+            "unit": "images/s (JPEG bytes -> validated, GPU-decoded, embedded, upserted, per-image responses)",
+            "what": f"ingesting.core.ingest_many over {len(files)} JPEG uploads per call, {ireps} calls, uuid ids, "
+                    f"string-id fp16 Index (host id map + metadata); GCS is a no-op hook",
+            "responses_ok": len(resp) == len(files) and all(r["message"] == "Successfully!" for r in resp),
+        }
+        ix.close()
 
     model.close()
     del images, raw, nrm

@@ -72,8 +72,8 @@ def main():
         for key, knames in keys.items():
             kname = next((k for k in knames if any(r["kernel"] == k for r in out.values())), knames[0])
             recs = [r for r in out.values() if r["kernel"] == kname]
-            if key == "fc1" and recs:  # bench prices the unsplit batch-256 launch: the largest grid
-                gmax = max(r["grid"] for r in recs)
+            if recs:  # bench prices the full-size launches (unsplit fc1, 125M-row scan / filter): the longest grid
+                gmax = max(recs, key=lambda r: r["dur_us"])["grid"]
                 recs = [r for r in recs if r["grid"] == gmax]
             if not recs or not all("hbm_read_bytes" in r and "hbm_write_bytes" in r for r in recs):
                 continue
