@@ -687,18 +687,27 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
 
     const int g = batch_stage_ratio(p.k, ws.cap);
     int64_t b0 = 0, b1 = std::min<int64_t>(p.n_rows, ws.cap);  // stage 1: every row is a candidate
+    // With nq > 256 the nqb query blocks that read one row chunk run side by side on one
+    // XCD so that its L2 serves the second to last reader; over a long chunk their
+    // progress drifts apart by more than the L2 holds (memory-side reads 2.8x the rows
+    // at 125M rows).  Sub-launches of <= 2 GB of rows realign them: reads fall to 1.05x
+    // and the filter runs 3-5 % faster (profiles/r02/r02_ab_results.txt).
+    const int64_t split = nqb > 1 ? std::max<int64_t>(SB_TILE, ((int64_t)1 << 31) / (p.ld * (int64_t)sizeof(T)) / SB_TILE * SB_TILE)
+                                  : (int64_t)0;
     while (b0 < p.n_rows) {
-        const int64_t rt_total = (b1 - b0 + SB_TILE - 1) / SB_TILE;
+      const int slot = timer ? timer->begin(s) : -1;
+      for (int64_t c0 = b0; c0 < b1;) {
+        const int64_t c1 = split > 0 ? std::min(b1, c0 + split) : b1;
+        const int64_t rt_total = (c1 - c0 + SB_TILE - 1) / SB_TILE;
         int64_t nchunk = std::min<int64_t>(rt_total, std::max<int64_t>(1, (256 + nqb - 1) / nqb));
         nchunk = (nchunk + 7) / 8 * 8;
         const int64_t tpc = (rt_total + nchunk - 1) / nchunk;
-        FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), b0, b1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
-        const int slot = timer ? timer->begin(s) : -1;
+        FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), c0, c1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
         const int nkt = (int)(p.ld / 64);
         if (nkt == 2 || nkt == 4 || nkt == 8) {
             const int qt = filter_qt();
             const int64_t rt = qs_rows(qt);
-            fa.tiles_per_chunk = ((b1 - b0 + rt - 1) / rt + nchunk - 1) / nchunk;
+            fa.tiles_per_chunk = ((c1 - c0 + rt - 1) / rt + nchunk - 1) / nchunk;
             const dim3 gr((unsigned)(nchunk * nqb));
 #if defined(RC_GEMM_ABLATION)
             static const int abl = std::getenv("RC_FILTER_ABL") ? std::atoi(std::getenv("RC_FILTER_ABL")) : 0;
@@ -725,6 +734,8 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
             hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
         }
         RC_LAUNCH_CHECK();
+        c0 = c1;
+      }
         if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(b1 - b0) * (double)p.ld);
         launch_rescore<T>(p, ws, b1 == p.n_rows ? 1 : 0, s);
         b0 = b1;
