@@ -112,6 +112,7 @@ class DeviceIndex:
         return vecs.to(device=self.device, dtype=torch.float32).contiguous()
 
     def upsert_rows(self, vecs: torch.Tensor, rows: torch.Tensor, stream=None) -> None:
+        """rows must be distinct (rc_index_upsert); callers with repeated ids dedupe first."""
         vecs = self._vecs(vecs)
         rows = rows.to(device=self.device, dtype=torch.int64).contiguous()
         if rows.numel() != vecs.shape[0]:

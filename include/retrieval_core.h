@@ -94,7 +94,10 @@ int rc_index_reserve(rc_index *h, int max_nq, int max_k);
  * vecs: device f32 [n, dim]; rows: device i64 [n] local row slots (host-assigned:
  * an existing id keeps its row, so upsert overwrites).  Each row is L2-normalised
  * in f32, cast to the storage dtype and scattered; its norm is kept so fetch can
- * return the original values.  An all-zero vector is rejected by the host layer. */
+ * return the original values.  An all-zero vector is rejected by the host layer.
+ * Rows must be distinct within one call (one wave per vector writes its row: a
+ * repeated row would interleave two vectors); Index.upsert keeps the last
+ * occurrence of a repeated id before calling. */
 int rc_index_upsert(rc_index *h, const float *vecs, int64_t n, const int64_t *rows, void *stream);
 
 /* replaces index.fetch(ids)["vectors"][id]["values"] — retriever/main.py:142.
