@@ -636,8 +636,8 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
 // to bf16 — a [3][256] LUT in LDS, the values the im2col kernel wrote before.
 // 128 x 256 tile, 4 waves (as gemm_w2_kernel, whose fragment layout and epilogue it
 // shares), two workgroups per CU; both operands register-staged (one 16-B A load
-// and four 16-B W loads per lane per 32-deep K-step, issued before the step's
-// MFMAs and written to the other LDS slot after them).
+// and four 16-B W loads per lane per 32-deep K-step, issued two steps ahead and
+// written to the other LDS slot after the MFMAs of the step before their own).
 template <int P>
 __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     constexpr int BM = 128, BN = 256, BK = 32, KC = 3 * P * P;
@@ -673,19 +673,23 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     const uint16_t *wrow = a.W + (int64_t)(n0 + tid) * KC;
     const int asw = ((ar >> 3) & 1) << 1, wsw = ((tid >> 3) & 1) << 1;  // chunk XOR of the fragment layout
 
-    uint4 av, wv[4];
-    auto load = [&](int kt) {
+    // register staging two K-steps ahead: set R holds step kt + 2 while step kt + 1's
+    // set is written to LDS, so each global load has two steps of MFMAs to land
+    struct Regs {
+        uint4 av, wv[4];
+    };
+    auto load = [&](int kt, Regs &r) {
         const int k0 = kt * BK + 16 * ah;
         const int ky = k0 / (3 * P), off = k0 - ky * (3 * P);
-        av = *reinterpret_cast<const uint4 *>(abase + ky * arow_stride + off);
+        r.av = *reinterpret_cast<const uint4 *>(abase + ky * arow_stride + off);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) wv[c] = *reinterpret_cast<const uint4 *>(wrow + kt * BK + 8 * c);
+        for (int c = 0; c < 4; ++c) r.wv[c] = *reinterpret_cast<const uint4 *>(wrow + kt * BK + 8 * c);
     };
-    auto store = [&](int slot, int kt) {
+    auto store = [&](int slot, int kt, const Regs &r) {
         uint8_t *As = smem + slot * SLOT;
         uint8_t *Ws = As + A_BYTES;
         const int c0 = (kt * BK + 16 * ah) % 3;  // channel of the first byte (k = ky·3P + kx·3 + c)
-        const uint32_t w4[4] = {av.x, av.y, av.z, av.w};
+        const uint32_t w4[4] = {r.av.x, r.av.y, r.av.z, r.av.w};
         uint32_t o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -696,7 +700,7 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
         *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah) ^ asw) << 4)) = make_uint4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah + 1) ^ asw) << 4)) = make_uint4(o[4], o[5], o[6], o[7]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4 *>(Ws + tid * 64 + ((c ^ wsw) << 4)) = wv[c];
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4 *>(Ws + tid * 64 + ((c ^ wsw) << 4)) = r.wv[c];
     };
     const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
 
@@ -707,12 +711,17 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     constexpr int nk = KC / BK;
-    load(0);
+    static_assert(nk % 2 == 0 && nk >= 2, "K steps are taken in pairs");
+    Regs r0, r1;
+    load(0, r0);
+    load(1, r1);
     __syncthreads();  // the LUT
-    store(0, 0);
+    store(0, 0, r0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) load(kt + 1);  // in flight under this step's MFMAs
+    // one K-step: the MFMAs on slot kt & 1, with `nxt` (step kt + 1) written to the
+    // other slot afterwards and `fre` (step kt's set, already in LDS) reloaded with kt + 2
+    auto step = [&](int kt, Regs &fre, const Regs &nxt) {
+        if (kt + 2 < nk) load(kt + 2, fre);
         const uint8_t *As = smem + (kt & 1) * SLOT;
         const uint8_t *Ws = As + A_BYTES;
         bf16x8 wf[4], af[8];
@@ -726,8 +735,12 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
-        if (kt + 1 < nk) store((kt + 1) & 1, kt + 1);  // the slot step kt - 1 read (closed by the last barrier)
+        if (kt + 1 < nk) store((kt + 1) & 1, kt + 1, nxt);  // the slot step kt - 1 read (closed by the last barrier)
         __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, r0, r1);
+        step(kt + 1, r1, r0);
     }
     w2_epilogue<EPI_PATCH_F32>(a, acc, smem, m0, n0);
 }
