@@ -584,7 +584,9 @@ def main():
             "value": nqb * args.batch_reps / bel,
             "unit": "queries/s",
             "ms_per_batch": bel / args.batch_reps * 1e3,
-            "roofline": {"kernel": "filter_qs_kernel<f16,8,4> (256 queries per block, 64 per wave in AGPRs x 64-row tiles, 16-step LDS ring, candidate epilogue)",
+            "roofline": {"kernel": ("filter_qs_kernel<f16,8,4> (256 queries per block, 64 per wave in AGPRs x 64-row tiles, 16-step LDS ring, candidate epilogue)"
+                                    if os.environ.get("RC_FILTER_QT") == "4" else
+                                    "filter_qs_kernel<f16,8,2> (256 queries per block, 32 per wave in registers x 128-row tiles, 8-step LDS ring, candidate epilogue)"),
                          "bound": "mfma", "achieved": g_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": g_tf / PEAK_BF16_TFLOPS, "traffic": load_profile_traffic("filter_f16"),
                          "avg_launch_ms": g_ms / max(g_n, 1), "launches": g_n,

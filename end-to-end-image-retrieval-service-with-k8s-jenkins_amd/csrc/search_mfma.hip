@@ -659,12 +659,14 @@ void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipSt
     }
 }
 
-// Queries per wave of the query-stationary filter kernel (16·QT): 4 unless
-// RC_FILTER_QT=2 (read once; A/B of the LDS-read-rate trade-off above).
+// Queries per wave of the query-stationary filter kernel (16·QT): 2 unless
+// RC_FILTER_QT=4 (read once).  With the 2-GB sub-launches the two forms are within
+// 1 % at config 4 (QT = 2 ahead, profiles/r02/r02_ab_results.txt), so the default is
+// the form whose MFMAs the compiler schedules (no inline asm, no manual hazard nops).
 inline int filter_qt() {
     static const int v = [] {
         const char *d = std::getenv("RC_FILTER_QT");
-        return d ? std::atoi(d) : 4;
+        return d && std::atoi(d) == 4 ? 4 : 2;
     }();
     return v;
 }

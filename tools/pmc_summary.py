@@ -67,7 +67,7 @@ def main():
         # fc1 is EPI_GELU_BF16_LN (5) with LayerNorm folded (default), EPI_GELU_BF16 (1) without
         keys = {"fc1": ("gemm_pp_kernel<5, 0>", "gemm_pp_kernel<1, 0>"),
                 "scan_f16": ("scan_topk_kernel<f16_t, 4, 1, 128>",),
-                "filter_f16": ("filter_qs_kernel<f16_t, 8, 4, 0>", "filter_qs_kernel<f16_t, 8, 2, 0>")}
+                "filter_f16": ("filter_qs_kernel<f16_t, 8, 2, 0>", "filter_qs_kernel<f16_t, 8, 4, 0>")}
         latest = {}
         for key, knames in keys.items():
             kname = next((k for k in knames if any(r["kernel"] == k for r in out.values())), knames[0])
