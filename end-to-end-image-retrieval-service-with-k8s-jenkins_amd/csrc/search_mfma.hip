@@ -697,9 +697,9 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
     const int64_t split = nqb > 1 ? std::max<int64_t>(SB_TILE, ((int64_t)1 << 31) / (p.ld * (int64_t)sizeof(T)) / SB_TILE * SB_TILE)
                                   : (int64_t)0;
     while (b0 < p.n_rows) {
-      const int slot = timer ? timer->begin(s) : -1;
       for (int64_t c0 = b0; c0 < b1;) {
         const int64_t c1 = split > 0 ? std::min(b1, c0 + split) : b1;
+        const int slot = timer ? timer->begin(s) : -1;  // per dispatch, as rocprofv3 counts them
         const int64_t rt_total = (c1 - c0 + SB_TILE - 1) / SB_TILE;
         int64_t nchunk = std::min<int64_t>(rt_total, std::max<int64_t>(1, (256 + nqb - 1) / nqb));
         nchunk = (nchunk + 7) / 8 * 8;
@@ -736,9 +736,9 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
             hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
         }
         RC_LAUNCH_CHECK();
+        if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(c1 - c0) * (double)p.ld);
         c0 = c1;
       }
-        if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(b1 - b0) * (double)p.ld);
         launch_rescore<T>(p, ws, b1 == p.n_rows ? 1 : 0, s);
         b0 = b1;
         b1 = std::min<int64_t>(p.n_rows, b1 * g);
