@@ -370,40 +370,57 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                 }
         }
         __syncthreads();
-        float4 add[16];
+        // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
+        // may still be live): 8 residual loads back to back, then the adds, the LN statistics
+        // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 512 + tid;
-            const int rl = id >> 6, ch = id & 63;
-            const int row = m0 + h * 128 + rl;
-            const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
-            if constexpr (EPI == EPI_RESID_F32) {
-                add[it] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
-            } else {
-                const int np = a.tokens - 1;
-                const int p = rr % np;
-                add[it] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
-            }
-        }
+        for (int p8 = 0; p8 < 16; p8 += 8) {
+            float4 add[8];
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 512 + tid;
-            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
-            const int row = m0 + h * 128 + rl;
-            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
-            const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
-            if (row < a.M) {
-                int64_t orow = row;
-                if constexpr (EPI == EPI_PATCH_F32) {
+            for (int j = 0; j < 8; ++j) {
+                const int it = p8 + j;
+                const int id = it * 512 + tid;
+                const int rl = id >> 6, ch = id & 63;
+                const int row = m0 + h * 128 + rl;
+                const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
+                if constexpr (EPI == EPI_RESID_F32) {
+                    add[j] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
+                } else {
                     const int np = a.tokens - 1;
-                    const int img = row / np, p = row - img * np;
-                    orow = (int64_t)img * a.tokens + 1 + p;
+                    const int p = rr % np;
+                    add[j] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
                 }
-                float4 *dst = reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4);
-                if constexpr ((ABL & 32) != 0) nt_store16(dst, o);  // diagnostic: streaming store
-                else *dst = o;
-                if (a.ln_x != nullptr)  // LayerNorm fold producer
-                    ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
+            }
+            float4 o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int rl = ((p8 + j) * 512 + tid) >> 6, ch = tid & 63;
+                const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
+                o[j] = make_float4(v.x + add[j].x, v.y + add[j].y, v.z + add[j].z, v.w + add[j].w);
+            }
+            float2 st[8];
+            if (a.ln_x != nullptr) {  // LayerNorm fold producer
+#pragma unroll
+                for (int j = 0; j < 8; ++j) st[j] = ln_row_stats(o[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int id = (p8 + j) * 512 + tid;
+                const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
+                const int row = m0 + h * 128 + rl;
+                if (row < a.M) {
+                    int64_t orow = row;
+                    if constexpr (EPI == EPI_PATCH_F32) {
+                        const int np = a.tokens - 1;
+                        const int img = row / np, p = row - img * np;
+                        orow = (int64_t)img * a.tokens + 1 + p;
+                    }
+                    float4 *dst = reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4);
+                    if constexpr ((ABL & 32) != 0) nt_store16(dst, o[j]);  // diagnostic: streaming store
+                    else *dst = o[j];
+                    if (a.ln_x != nullptr)
+                        ln_row_store(o[j], st[j], a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane);
+                }
             }
         }
         if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
@@ -472,37 +489,54 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
             }
         }
         __syncthreads();
-        float4 add[16];
+        // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
+        // may still be live): 8 residual loads back to back, then the adds, the LN statistics
+        // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 256 + tid;
-            const int rl = id >> 6, ch = id & 63;
-            const int row = m0 + h * 64 + rl;
-            const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
-            if constexpr (EPI == EPI_RESID_F32) {
-                add[it] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
-            } else {
-                const int p = rr % (a.tokens - 1);
-                add[it] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
-            }
-        }
+        for (int p8 = 0; p8 < 16; p8 += 8) {
+            float4 add[8];
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 256 + tid;
-            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
-            const int row = m0 + h * 64 + rl;
-            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
-            const float4 o = make_float4(v.x + add[it].x, v.y + add[it].y, v.z + add[it].z, v.w + add[it].w);
-            if (row < a.M) {
-                int64_t orow = row;
-                if constexpr (EPI == EPI_PATCH_F32) {
-                    const int np = a.tokens - 1;
-                    const int img = row / np, p = row - img * np;
-                    orow = (int64_t)img * a.tokens + 1 + p;
+            for (int j = 0; j < 8; ++j) {
+                const int it = p8 + j;
+                const int id = it * 256 + tid;
+                const int rl = id >> 6, ch = id & 63;
+                const int row = m0 + h * 64 + rl;
+                const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
+                if constexpr (EPI == EPI_RESID_F32) {
+                    add[j] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
+                } else {
+                    const int p = rr % (a.tokens - 1);
+                    add[j] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
                 }
-                *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o;
-                if (a.ln_x != nullptr)  // LayerNorm fold producer
-                    ln_emit_row(o, a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane, true);
+            }
+            float4 o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int rl = ((p8 + j) * 256 + tid) >> 6, ch = tid & 63;
+                const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
+                o[j] = make_float4(v.x + add[j].x, v.y + add[j].y, v.z + add[j].z, v.w + add[j].w);
+            }
+            float2 st[8];
+            if (a.ln_x != nullptr) {  // LayerNorm fold producer
+#pragma unroll
+                for (int j = 0; j < 8; ++j) st[j] = ln_row_stats(o[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int id = (p8 + j) * 256 + tid;
+                const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
+                const int row = m0 + h * 64 + rl;
+                if (row < a.M) {
+                    int64_t orow = row;
+                    if constexpr (EPI == EPI_PATCH_F32) {
+                        const int np = a.tokens - 1;
+                        const int img = row / np, p = row - img * np;
+                        orow = (int64_t)img * a.tokens + 1 + p;
+                    }
+                    *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o[j];
+                    if (a.ln_x != nullptr)
+                        ln_row_store(o[j], st[j], a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane);
+                }
             }
         }
         if (h == 0) __syncthreads();  // the second half overwrites the staging rows

@@ -88,17 +88,24 @@ __device__ __forceinline__ float2 ln_row_scale(const float *__restrict__ st, flo
 }
 
 // Producer side, one wave holding one row's 256-column segment as float4 v per
-// lane: write bf16(v) and the tile's (mean, M2).  Wave-collective.
-__device__ __forceinline__ void ln_emit_row(const float4 v, uint16_t *__restrict__ xrow, float *__restrict__ strow,
-                                            int lane, bool store) {
+// lane: the tile's (mean, M2) (wave-collective) and the stores of bf16(v) and
+// the statistics.  The tiled epilogues compute the statistics of all their rows
+// first, branch-free, so the wave reductions of different rows interleave.
+__device__ __forceinline__ float2 ln_row_stats(const float4 v) {
     const float s = wave_sum((v.x + v.y) + (v.z + v.w));
     const float mt = s * (1.0f / 256);
     const float d0 = v.x - mt, d1 = v.y - mt, d2 = v.z - mt, d3 = v.w - mt;
-    const float M2 = wave_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
-    if (store) {
-        reinterpret_cast<uint2 *>(xrow)[lane] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
-        if (lane == 0) *reinterpret_cast<float2 *>(strow) = make_float2(mt, M2);
-    }
+    return make_float2(mt, wave_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3)));
+}
+__device__ __forceinline__ void ln_row_store(const float4 v, float2 st, uint16_t *__restrict__ xrow,
+                                             float *__restrict__ strow, int lane) {
+    reinterpret_cast<uint2 *>(xrow)[lane] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+    if (lane == 0) *reinterpret_cast<float2 *>(strow) = st;
+}
+__device__ __forceinline__ void ln_emit_row(const float4 v, uint16_t *__restrict__ xrow, float *__restrict__ strow,
+                                            int lane, bool store) {
+    const float2 st = ln_row_stats(v);
+    if (store) ln_row_store(v, st, xrow, strow, lane);
 }
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;
