@@ -72,6 +72,29 @@ def seeded_vit_msn_weights(seed: int = 1907, num_layers: int = LAYERS) -> dict[s
     return out
 
 
+def with_massive_activations(sd: dict[str, np.ndarray], channels=(17, 401), patch_bias: float = 40.0,
+                             fc2_bias: float = 20.0, ln_gamma: float = 0.05) -> dict[str, np.ndarray]:
+    """A copy of ``sd`` whose residual stream carries trained-ViT-like outlier channels.
+
+    Trained ViTs keep a few hidden channels at ~100x the magnitude of the rest on every
+    token ("massive activations"), and their LayerNorm gammas damp those channels.  The
+    seeded weights above have no such channels, so they do not stress the bf16 residual
+    copy or the LayerNorm fold (rstd·(x·W′ − μ·c), where μ and rstd are then set by the
+    outliers).  Here the patch-embedding bias and every layer's fc2 bias push ``channels``
+    up (≈ patch_bias + layer·fc2_bias: 280 after 12 layers, against |x| ≈ 1 elsewhere)
+    and every LayerNorm gamma of those channels is ``ln_gamma``.
+    """
+    out = {k: v.copy() for k, v in sd.items()}
+    ch = np.asarray(channels)
+    out["embeddings.patch_embeddings.projection.bias"][ch] += np.float32(patch_bias)
+    for k in out:
+        if k.endswith("output.dense.bias") and "attention" not in k:
+            out[k][ch] += np.float32(fc2_bias)
+        if k.endswith(("layernorm_before.weight", "layernorm_after.weight")) or k == "layernorm.weight":
+            out[k][ch] = np.float32(ln_gamma)
+    return out
+
+
 def to_hf_v5(sd: dict[str, np.ndarray]) -> dict[str, np.ndarray]:
     """Legacy checkpoint keys → transformers 5.x ``ViTMSNModel`` module names."""
     ren = {

@@ -23,6 +23,10 @@ from oracle.weights import seeded_vit_msn_weights
 pytestmark = pytest.mark.gpu
 
 BF16_COS_TOL = 1e-2  # north-star bound for the bf16 path: 1 - cos(got, ref) <= 1e-2
+# north-star bound of the fp32 tier.  The bf16 path meets it as well on the 12-layer
+# seeded model (measured max 1.1e-4 over the test image + random images,
+# tools/precision_probe.py), so it is asserted as this build's regression guard.
+FP32_TIER_COS_TOL = 1e-3
 
 
 @pytest.fixture(scope="module")
@@ -81,7 +85,7 @@ def test_embed_test_image_matches_reference(model12):
     raw = raw.cpu().numpy()[0]
     assert np.isfinite(raw).all()
     assert 1.0 - cosine(raw, ref) <= BF16_COS_TOL
-    assert 1.0 - cosine(raw, ref) <= 2e-3  # what this build actually achieves (regression guard)
+    assert 1.0 - cosine(raw, ref) <= FP32_TIER_COS_TOL
     nrm = nrm.cpu().numpy()[0]
     assert np.allclose(nrm, raw / np.linalg.norm(raw), atol=1e-6)
 
@@ -124,6 +128,7 @@ def test_embed_matches_numpy_oracle_random(model12, weights12):
     raw = raw.cpu().numpy()
     for i in range(2):
         assert 1.0 - cosine(raw[i], ref[i]) <= BF16_COS_TOL
+        assert 1.0 - cosine(raw[i], ref[i]) <= FP32_TIER_COS_TOL
 
 
 def test_embed_full_batch_256_properties(vitmod, weights12, cuda):
@@ -143,6 +148,7 @@ def test_embed_full_batch_256_properties(vitmod, weights12, cuda):
     got = raw.cpu().numpy()[pick]
     for j in range(len(pick)):
         assert 1.0 - cosine(got[j], ref[j]) <= BF16_COS_TOL
+        assert 1.0 - cosine(got[j], ref[j]) <= FP32_TIER_COS_TOL
     m.close()
 
 
@@ -222,6 +228,39 @@ def test_ln_fold_matches_unfused_and_oracle(vitmod, weights12, cuda):
     ref = embed_cls(np.stack([preprocess(imgs[i]) for i in pick]), weights12)
     for j, i in enumerate(pick):
         assert 1.0 - cosine(fold[i], ref[j]) <= BF16_COS_TOL
-        assert 1.0 - cosine(fold[i], ref[j]) <= 2e-3
+        assert 1.0 - cosine(fold[i], ref[j]) <= FP32_TIER_COS_TOL
+    m.close()
+
+
+def test_embed_massive_activation_channels(vitmod, weights12, cuda):
+    """Trained ViTs carry a few residual channels at ~100x the rest (massive activations);
+    the seeded weights do not.  With oracle.weights.with_massive_activations the residual
+    stream spans 280 vs ~0.5 (560x): the bf16 residual copy and the LayerNorm fold (whose
+    mean and rstd the outliers then set) must still match the fp32 oracle — on every
+    channel and on the ordinary channels alone (the outliers would dominate the cosine)."""
+    import torch
+
+    from oracle.weights import with_massive_activations
+
+    outl = (17, 401)
+    sd = with_massive_activations(weights12, channels=outl)
+    rng = np.random.default_rng(21)
+    imgs = rng.integers(0, 256, (3, 224, 224, 3), dtype=np.uint8)
+    imgs[0] = np.array(Image.fromarray(_test_image()).resize((224, 224)))
+    ref = embed_cls(np.stack([preprocess(x) for x in imgs]), sd)
+    keep = np.ones(768, bool)
+    keep[list(outl)] = False
+    m = vitmod.VitMsnEmbedder(sd, device=0, max_batch=3)
+    outs = {}
+    for fold in (True, False):
+        m.set_ln_fold(fold)
+        raw, _ = m.embed(torch.from_numpy(imgs))
+        outs[fold] = raw.cpu().numpy()
+        assert np.isfinite(outs[fold]).all()
+        for i in range(3):
+            assert 1.0 - cosine(outs[fold][i], ref[i]) <= FP32_TIER_COS_TOL
+            assert 1.0 - cosine(outs[fold][i][keep], ref[i][keep]) <= FP32_TIER_COS_TOL
+    for i in range(3):  # fold vs standalone LayerNorm: measured ~1e-6
+        assert 1.0 - cosine(outs[True][i][keep], outs[False][i][keep]) <= 1e-4
     m.close()
 

@@ -107,3 +107,31 @@ def test_tie_rule_row_ascending():
     X = np.ones((10, 4), dtype=np.float32)
     r, s = cosine_topk(X, np.ones(4), 3)
     assert r[0].tolist() == [0, 1, 2]
+
+
+def test_massive_activation_weights_shape_the_residual_stream():
+    """oracle.weights.with_massive_activations: only the named channels of the patch bias,
+    fc2 biases and LayerNorm gammas change, and the residual stream then carries them at
+    ~100x the other channels on the patch tokens (40 after the embedding, +20 per layer, vs ~0.5)."""
+    import oracle.vit as V
+    from oracle.weights import with_massive_activations
+
+    sd = seeded_vit_msn_weights(1907, num_layers=2)
+    mv = with_massive_activations(sd, channels=(3, 700))
+    changed = sorted(k for k in sd if not np.array_equal(sd[k], mv[k]))
+    assert changed == sorted(["embeddings.patch_embeddings.projection.bias", "layernorm.weight"] +
+                             [f"encoder.layer.{i}.{n}" for i in range(2)
+                              for n in ("output.dense.bias", "layernorm_before.weight", "layernorm_after.weight")])
+    for k in changed:
+        d = np.nonzero(sd[k] != mv[k])[0]
+        assert set(d.tolist()) <= {3, 700}
+    seen = []
+    orig = V._ln
+    try:
+        V._ln = lambda x, w, b: (seen.append(np.abs(x[:, 1:, [3, 700]]).min() / np.median(np.abs(x))), orig(x, w, b))[1]
+        rng = np.random.default_rng(0)
+        out = embed_cls(preprocess(rng.integers(0, 256, (224, 224, 3), dtype=np.uint8))[None], mv)
+    finally:
+        V._ln = orig
+    assert np.isfinite(out).all()
+    assert min(seen) > 50  # the outlier channels stay far above the rest on every patch token
