@@ -71,6 +71,80 @@ __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
     __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4 *>(dst));
 }
 
+// Copy-out of the f32 epilogues (residual add / patch scatter + position): the
+// block's NT threads move ROWS staged f32 rows (1-KB rows of 256 columns, 16-B chunk
+// XOR (row & 63) in `smem`; tile rows r0 .. r0 + ROWS of the output, columns n0 ..
+// n0 + 256), one row per wave per step, in passes of 8 rows: 8 residual / position
+// loads back to back, then the adds, the LN statistics of the 8 rows (branch-free,
+// so their wave reductions interleave) and the stores.  HL: the residual stream is
+// the bf16 pair (a.ln_x, a.res_lo) (vit_kernels.h, "Residual stream as bf16 pairs");
+// otherwise f32 a.out_f32, plus the bf16 copy and statistics when a.ln_x is set.
+template <int EPI, int NT, int ROWS_PER_WAVE, int PASS = 8>
+__device__ __forceinline__ void resid_copy_out(const GemmArgs &a, const uint8_t *smem, int tid, int r0, int n0) {
+    constexpr bool HL = epi_hl(EPI);
+    const int lane = tid & 63;
+    const bool stats = HL ? a.ln_stats != nullptr : a.ln_x != nullptr;
+#pragma unroll
+    for (int p8 = 0; p8 < ROWS_PER_WAVE; p8 += PASS) {
+        float4 add[PASS];
+        uint4 addp[PASS];
+#pragma unroll
+        for (int j = 0; j < PASS; ++j) {
+            const int id = (p8 + j) * NT + tid;
+            const int rl = id >> 6, ch = id & 63;
+            const int row = r0 + rl;
+            const int rr = row < a.M ? row : (r0 < a.M ? r0 : 0);  // clamp: keep the load in bounds, result unused
+            if constexpr (epi_resid(EPI)) {
+                const int64_t off = (int64_t)rr * a.N + n0 + ch * 4;
+                if constexpr (HL) addp[j] = hl_load(a.ln_x + off, a.res_lo + off);
+                else add[j] = *reinterpret_cast<const float4 *>(a.out_f32 + off);
+            } else {
+                const int p = rr % (a.tokens - 1);
+                add[j] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
+            }
+        }
+        float4 o[PASS];
+        uint4 op[PASS];
+#pragma unroll
+        for (int j = 0; j < PASS; ++j) {
+            const int rl = ((p8 + j) * NT + tid) >> 6, ch = tid & 63;
+            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
+            float4 r;
+            if constexpr (EPI == EPI_RESID_HL) r = hl_value(addp[j]);
+            else r = add[j];
+            o[j] = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+            if constexpr (HL) op[j] = hl_split(o[j]);
+        }
+        float2 st[PASS];
+        if (stats) {  // LayerNorm fold producer
+#pragma unroll
+            for (int j = 0; j < PASS; ++j) st[j] = ln_row_stats(HL ? hl_value(op[j]) : o[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < PASS; ++j) {
+            const int id = (p8 + j) * NT + tid;
+            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
+            const int row = r0 + rl;
+            if (row < a.M) {
+                int64_t orow = row;
+                if constexpr (epi_patch(EPI)) {
+                    const int np = a.tokens - 1;
+                    const int img = row / np, p = row - img * np;
+                    orow = (int64_t)img * a.tokens + 1 + p;
+                }
+                float *srow = a.ln_stats + (orow * LN_TILES + n0 / 256) * 2;
+                if constexpr (HL) {
+                    hl_store(op[j], a.ln_x + orow * a.N + n0 + ch * 4, a.res_lo + orow * a.N + n0 + ch * 4);
+                    if (stats && lane == 0) *reinterpret_cast<float2 *>(srow) = st[j];
+                } else {
+                    *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o[j];
+                    if (stats) ln_row_store(o[j], st[j], a.ln_x + orow * a.N + n0, srow, lane);
+                }
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------- ping-pong GEMM --
 // 256x256x64 tile, 8 waves in two groups: G0 = waves 0-3 (output rows 0-127),
 // G1 = waves 4-7 (rows 128-255); wave w and w+4 share a SIMD.  Each wave owns
@@ -373,56 +447,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
         // may still be live): 8 residual loads back to back, then the adds, the LN statistics
         // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
-#pragma unroll
-        for (int p8 = 0; p8 < 16; p8 += 8) {
-            float4 add[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int it = p8 + j;
-                const int id = it * 512 + tid;
-                const int rl = id >> 6, ch = id & 63;
-                const int row = m0 + h * 128 + rl;
-                const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
-                if constexpr (EPI == EPI_RESID_F32) {
-                    add[j] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
-                } else {
-                    const int np = a.tokens - 1;
-                    const int p = rr % np;
-                    add[j] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
-                }
-            }
-            float4 o[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int rl = ((p8 + j) * 512 + tid) >> 6, ch = tid & 63;
-                const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
-                o[j] = make_float4(v.x + add[j].x, v.y + add[j].y, v.z + add[j].z, v.w + add[j].w);
-            }
-            float2 st[8];
-            if (a.ln_x != nullptr) {  // LayerNorm fold producer
-#pragma unroll
-                for (int j = 0; j < 8; ++j) st[j] = ln_row_stats(o[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int id = (p8 + j) * 512 + tid;
-                const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
-                const int row = m0 + h * 128 + rl;
-                if (row < a.M) {
-                    int64_t orow = row;
-                    if constexpr (EPI == EPI_PATCH_F32) {
-                        const int np = a.tokens - 1;
-                        const int img = row / np, p = row - img * np;
-                        orow = (int64_t)img * a.tokens + 1 + p;
-                    }
-                    float4 *dst = reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4);
-                    if constexpr ((ABL & 32) != 0) nt_store16(dst, o[j]);  // diagnostic: streaming store
-                    else *dst = o[j];
-                    if (a.ln_x != nullptr)
-                        ln_row_store(o[j], st[j], a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane);
-                }
-            }
-        }
+        // (bf16 pairs: passes of 4 rows; 8 would spill beside the other group's accumulators)
+        resid_copy_out<EPI, 512, 16, epi_hl(EPI) ? 4 : 8>(a, smem, tid, m0 + h * 128, n0);
         if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
     }
 }
@@ -489,56 +515,10 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
             }
         }
         __syncthreads();
-        // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
-        // may still be live): 8 residual loads back to back, then the adds, the LN statistics
-        // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
-#pragma unroll
-        for (int p8 = 0; p8 < 16; p8 += 8) {
-            float4 add[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int it = p8 + j;
-                const int id = it * 256 + tid;
-                const int rl = id >> 6, ch = id & 63;
-                const int row = m0 + h * 64 + rl;
-                const int rr = row < a.M ? row : m0;  // clamp: keep the load in bounds, result unused
-                if constexpr (EPI == EPI_RESID_F32) {
-                    add[j] = *reinterpret_cast<const float4 *>(a.out_f32 + (int64_t)rr * a.N + n0 + ch * 4);
-                } else {
-                    const int p = rr % (a.tokens - 1);
-                    add[j] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
-                }
-            }
-            float4 o[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int rl = ((p8 + j) * 256 + tid) >> 6, ch = tid & 63;
-                const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
-                o[j] = make_float4(v.x + add[j].x, v.y + add[j].y, v.z + add[j].z, v.w + add[j].w);
-            }
-            float2 st[8];
-            if (a.ln_x != nullptr) {  // LayerNorm fold producer
-#pragma unroll
-                for (int j = 0; j < 8; ++j) st[j] = ln_row_stats(o[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int id = (p8 + j) * 256 + tid;
-                const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
-                const int row = m0 + h * 64 + rl;
-                if (row < a.M) {
-                    int64_t orow = row;
-                    if constexpr (EPI == EPI_PATCH_F32) {
-                        const int np = a.tokens - 1;
-                        const int img = row / np, p = row - img * np;
-                        orow = (int64_t)img * a.tokens + 1 + p;
-                    }
-                    *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o[j];
-                    if (a.ln_x != nullptr)
-                        ln_row_store(o[j], st[j], a.ln_x + orow * a.N + n0, a.ln_stats + (orow * LN_TILES + n0 / 256) * 2, lane);
-                }
-            }
-        }
+        // 16 rows per wave in two passes of 8: 8 residual loads back to back, then the adds,
+        // the LN statistics of the 8 rows (branch-free, so their wave reductions interleave),
+        // and the stores
+        resid_copy_out<EPI, 256, 16>(a, smem, tid, m0 + h * 64, n0);
         if (h == 0) __syncthreads();  // the second half overwrites the staging rows
     }
 }
@@ -672,7 +652,8 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
 // shares), two workgroups per CU; both operands register-staged (one 16-B A load
 // and four 16-B W loads per lane per 32-deep K-step, issued two steps ahead and
 // written to the other LDS slot after the MFMAs of the step before their own).
-template <int P>
+// EPI: EPI_PATCH_F32 or EPI_PATCH_HL (the residual stream as bf16 pairs).
+template <int P, int EPI>
 __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     constexpr int BM = 128, BN = 256, BK = 32, KC = 3 * P * P;
     constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 KB + 16 KB
@@ -776,7 +757,7 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
         step(kt, r0, r1);
         step(kt + 1, r1, r0);
     }
-    w2_epilogue<EPI_PATCH_F32>(a, acc, smem, m0, n0);
+    w2_epilogue<EPI>(a, acc, smem, m0, n0);
 }
 
 // Skinny GEMM for M <= 256 (the last layer's CLS rows: O-proj, fc1, fc2 with
@@ -826,7 +807,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
         } else {
             v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
         }
-        if constexpr (EPI == EPI_RESID_F32) {
+        if constexpr (EPI == EPI_RESID_HL) {  // residual stream as bf16 pairs (ln_emit_kernel adds the statistics)
+            const int64_t off = (int64_t)row * a.N + c;
+            const float4 r = hl_value(hl_load(a.ln_x + off, a.res_lo + off));
+            hl_store(hl_split(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w)), a.ln_x + off, a.res_lo + off);
+        } else if constexpr (EPI == EPI_RESID_F32) {
             float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + c);
             const float4 r = *o;
             *o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
@@ -847,14 +832,22 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
 // LayerNorm-fold producer pass for rows a skinny GEMM wrote (M <= 256): one wave per
 // (row, 256-column tile), the same lane -> column map and reductions as the tiled
 // kernels' epilogues (ln_emit_row), so the partials are bit-identical for any M.
+// lo != null: the rows are the bf16 pairs (ln_x, lo); only the statistics are written.
 __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ x, uint16_t *__restrict__ ln_x,
-                                                     float *__restrict__ ln_stats, int M) {
+                                                     const uint16_t *__restrict__ lo, float *__restrict__ ln_stats, int M) {
     const int lane = threadIdx.x & 63;
     const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (item >= M * LN_TILES) return;  // wave-uniform
     const int row = item / LN_TILES, t = item - row * LN_TILES;
-    const float4 v = reinterpret_cast<const float4 *>(x + (int64_t)row * 256 * LN_TILES + t * 256)[lane];
-    ln_emit_row(v, ln_x + (int64_t)row * 256 * LN_TILES + t * 256, ln_stats + ((int64_t)row * LN_TILES + t) * 2, lane, true);
+    const int64_t off = (int64_t)row * 256 * LN_TILES + t * 256;
+    float *srow = ln_stats + ((int64_t)row * LN_TILES + t) * 2;
+    if (lo != nullptr) {
+        const float2 st = ln_row_stats(hl_value(hl_load(ln_x + off + 4 * lane, lo + off + 4 * lane)));
+        if (lane == 0) *reinterpret_cast<float2 *>(srow) = st;
+        return;
+    }
+    const float4 v = reinterpret_cast<const float4 *>(x + off)[lane];
+    ln_emit_row(v, ln_x + off, srow, lane, true);
 }
 
 // Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel, any N % 128 == 0),
@@ -889,7 +882,12 @@ inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
     RC_REQUIRE(a.img && a.lut && a.img_size % 16 == 0 && a.N % 256 == 0 && a.K == 3 * 16 * 16 && a.M >= 1,
                RC_ERR_UNSUPPORTED, "patch GEMM: 16x16 patches, N % 256 == 0");
     const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
-    hipLaunchKernelGGL(patch_gemm_kernel<16>, dim3(ntm * ntn), dim3(256), 0, s, a);
+    if (a.res_lo != nullptr) {
+        RC_REQUIRE(a.ln_x != nullptr, RC_ERR_INVALID, "bf16-pair residual stream needs ln_x");
+        hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_HL>), dim3(ntm * ntn), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_F32>), dim3(ntm * ntn), dim3(256), 0, s, a);
+    }
     RC_LAUNCH_CHECK();
 }
 
@@ -900,14 +898,18 @@ template <int EPI>
 void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
-    const int pick = gemm_pick(a, variant, EPI == EPI_PATCH_F32);
+    const int pick = gemm_pick(a, variant, epi_patch(EPI));
+    if constexpr (epi_hl(EPI)) {
+        RC_REQUIRE(a.ln_x && a.res_lo && pick != GEMM_V1, RC_ERR_UNSUPPORTED,
+                   "bf16-pair residual epilogues: ln_x + res_lo, ping-pong / two-workgroup / skinny kernels");
+    }
     if constexpr (epi_ln(EPI)) {
         RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_SKINNY) && a.ln_c && a.ln_stats, RC_ERR_UNSUPPORTED,
                    "LayerNorm-fold consumers run on the ping-pong or skinny kernel");
     }
     switch (pick) {
         case GEMM_V1: {
-            if constexpr (!epi_ln(EPI)) {
+            if constexpr (!epi_ln(EPI) && !epi_hl(EPI)) {
                 RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
                 const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
                 hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
@@ -924,15 +926,15 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case GEMM_SKINNY: {
-            RC_REQUIRE(EPI != EPI_PATCH_F32 && a.N % 32 == 0 && a.M >= 1, RC_ERR_UNSUPPORTED,
+            RC_REQUIRE(!epi_patch(EPI) && a.N % 32 == 0 && a.M >= 1, RC_ERR_UNSUPPORTED,
                        "skinny GEMM: bf16 / GELU / residual epilogues, N a multiple of 32");
             const int waves = ((a.M + 15) / 16) * (a.N / 32);
             hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
-            if (a.ln_x != nullptr) {  // LayerNorm-fold producer: the partials in a second pass
+            if (a.ln_x != nullptr && a.ln_stats != nullptr) {  // LayerNorm-fold producer: the partials in a second pass
                 RC_LAUNCH_CHECK();
                 RC_REQUIRE(a.N == 256 * LN_TILES, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
                 hipLaunchKernelGGL(ln_emit_kernel, dim3((a.M * LN_TILES + 3) / 4), dim3(256), 0, s, a.out_f32, a.ln_x,
-                                   a.ln_stats, a.M);
+                                   a.res_lo, a.ln_stats, a.M);
             }
             break;
         }

@@ -8,9 +8,10 @@
 //             K ordered (ky, kx, c) for the implicit-GEMM patch embedding;
 //             biases / LayerNorm params / cls / pos — f32
 //   workspace (sized for max_batch images, rows padded to the GEMM tile):
-//             hidden f32 [Mp][H], ln bf16 [Mp][H] (LayerNorm output, or bf16(x) under
-//             the LayerNorm fold, with ln_stats f32 [Mp][3][2]), qkv bf16 [Mp][3H],
-//             attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
+//             residual stream: under the LayerNorm fold the bf16 pair ln = RNE(x),
+//             res_lo = RNE(x − ln) [Mp][H] with ln_stats f32 [Mp][3][2]; without it
+//             hidden f32 [Mp][H] and ln bf16 [Mp][H] = LayerNorm output; qkv bf16
+//             [Mp][3H], attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -134,6 +135,7 @@ struct rc_model {
     int Mp = 0;
     uint16_t *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
+    uint16_t *res_lo = nullptr;  // LayerNorm fold: low halves of the residual stream's bf16 pairs
     float *ln_stats = nullptr;     // [Mp][3][2] LayerNorm-fold partials (per 256-column tile: mean, M2)
     bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
@@ -368,6 +370,12 @@ void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, bool fc1 = false) {
     m->timers[T_GEMM].end(t0, s, flops);
 }
 
+// residual-stream producer GEMM (O-proj, fc2): f32 stream, or bf16 pairs under the fold
+void resid_gemm(rc_model *m, const GemmArgs &a, hipStream_t s) {
+    if (a.res_lo != nullptr) gemm<EPI_RESID_HL>(m, a, s);
+    else gemm<EPI_RESID_F32>(m, a, s);
+}
+
 void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint16_t *y, int M, hipStream_t s) {
     const int t = m->timers[T_LN].begin(s);
     hipLaunchKernelGGL(layernorm_kernel<3>, dim3((M + 3) / 4), dim3(256), 0, s, x, g, b, y, M, m->cfg.ln_eps);
@@ -381,14 +389,14 @@ void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint
 // and fc2 (+residual) as M = n GEMMs on the compact rows.  The kernels are the
 // full-batch ones (a GEMM row's result does not depend on M), so a CLS row gets
 // the same arithmetic as in the full layer except attention's summation order.
-void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *qkv, const float *hidden, float scale,
-                    hipStream_t s) {
+void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *qkv, const float *hidden,
+                    const uint16_t *hi, const uint16_t *lo, float scale, hipStream_t s) {
     const auto &c = m->cfg;
     const int H = c.hidden, T = m->tokens;
     float *hc = m->cls_hidden + (int64_t)i0 * H;
     uint16_t *ac = m->cls_attn + (int64_t)i0 * H, *lc = m->cls_ln + (int64_t)i0 * H;
     uint16_t *mc = m->cls_mlp + (int64_t)i0 * c.mlp;
-    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, T, hc);
+    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, hi, lo, T, hc);
     RC_LAUNCH_CHECK();
     const int ta = m->timers[T_ATTN].begin(s);
     const int items = n * c.heads;
@@ -434,16 +442,18 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
     // M <= 256 included), so an image's embedding does not depend on its batch.
     const bool fold = m->ln_fold;
     float *st = m->ln_stats + r0 * 2 * LN_TILES;
+    uint16_t *lo = fold ? m->res_lo + r0 * H : nullptr;  // the residual stream is the pair (ln, lo)
     auto produce = [&](GemmArgs a, bool emit) {
-        if (fold && emit) {
+        if (fold) {
             a.ln_x = ln;
-            a.ln_stats = st;
+            a.res_lo = lo;
+            a.ln_stats = emit ? st : nullptr;
         }
         return a;
     };
     // 2. embeddings: CLS + pos, patch GEMM (+bias +pos) into the residual stream
     hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, hidden, T, H, m->cls, m->pos, fold ? ln : nullptr,
-                       fold ? st : nullptr);
+                       fold ? st : nullptr, lo);
     RC_LAUNCH_CHECK();
     {
         GemmArgs a = produce(GemmArgs{nullptr, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden, m->pos,
@@ -470,7 +480,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
         }
         if (m->cls_only_last && l == c.layers - 1) {
-            last_layer_cls(m, L, i0, n, qkv, hidden, scale, s);
+            last_layer_cls(m, L, i0, n, qkv, hidden, fold ? ln : nullptr, lo, scale, s);
             break;
         }
         const int ta = m->timers[T_ATTN].begin(s);
@@ -484,7 +494,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
                                scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
-        gemm<EPI_RESID_F32>(m, produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true), s);
+        resid_gemm(m, produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true), s);
         if (fold) {
             GemmArgs a{ln, L.w_fc1_f, L.b_fc1_f, M, c.mlp, H, mlp, nullptr, nullptr, T};
             a.ln_c = L.c_fc1;
@@ -496,12 +506,14 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, true);
         }
         // the last layer's fc2 feeds only the final LN of the CLS rows (cls_final_kernel)
-        gemm<EPI_RESID_F32>(m, produce(GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T},
-                                       l + 1 < c.layers), s);
+        resid_gemm(m, produce(GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T},
+                              l + 1 < c.layers), s);
     }
     // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
     const float *fin = m->cls_only_last ? m->cls_hidden + (int64_t)i0 * H : hidden;
-    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, fin, m->cls_only_last ? 1 : T, m->lnf_w, m->lnf_b,
+    const bool pair = fold && !m->cls_only_last;
+    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, fin, pair ? ln : nullptr, pair ? lo : nullptr,
+                       m->cls_only_last ? 1 : T, m->lnf_w, m->lnf_b,
                        c.ln_eps,
                        raw + (int64_t)i0 * H, normed ? normed + (int64_t)i0 * H : nullptr);
     RC_LAUNCH_CHECK();
@@ -564,6 +576,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->ln_stats = (float *)m->alloc((size_t)m->Mp * 2 * LN_TILES * 4);
             RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * 2 * LN_TILES * 4));  // pad rows: finite scales
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
+            m->res_lo = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->qkv = (uint16_t *)m->alloc((size_t)m->Mp * 3 * H * 2);
             m->attn = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->mlp = (uint16_t *)m->alloc((size_t)m->Mp * cfg->mlp * 2);
@@ -583,6 +596,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             // pad rows are read by the GEMM tiles: keep them finite (zero) forever
             RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
             RC_HIP(hipMemset(m->ln, 0, (size_t)m->Mp * H * 2));
+            RC_HIP(hipMemset(m->res_lo, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->qkv, 0, (size_t)m->Mp * 3 * H * 2));
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));

@@ -26,8 +26,14 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
 
 // EPI_BF16_LN / EPI_GELU_BF16_LN: the bf16 epilogues as consumers of the LayerNorm fold
-enum GemmEpi { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_PATCH_F32 = 3, EPI_BF16_LN = 4, EPI_GELU_BF16_LN = 5 };
+// EPI_RESID_HL / EPI_PATCH_HL: the residual-stream producers with the stream kept as bf16
+// pairs (see "Residual stream as bf16 pairs"; GemmArgs::res_lo)
+enum GemmEpi { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_PATCH_F32 = 3, EPI_BF16_LN = 4, EPI_GELU_BF16_LN = 5,
+               EPI_RESID_HL = 6, EPI_PATCH_HL = 7 };
 constexpr bool epi_bf16_out(int e) { return e == EPI_BF16 || e == EPI_GELU_BF16 || e == EPI_BF16_LN || e == EPI_GELU_BF16_LN; }
+constexpr bool epi_resid(int e) { return e == EPI_RESID_F32 || e == EPI_RESID_HL; }
+constexpr bool epi_patch(int e) { return e == EPI_PATCH_F32 || e == EPI_PATCH_HL; }
+constexpr bool epi_hl(int e) { return e == EPI_RESID_HL || e == EPI_PATCH_HL; }
 constexpr bool epi_gelu(int e) { return e == EPI_GELU_BF16 || e == EPI_GELU_BF16_LN; }
 constexpr bool epi_ln(int e) { return e == EPI_BF16_LN || e == EPI_GELU_BF16_LN; }
 
@@ -48,6 +54,10 @@ struct GemmArgs {
     //     epilogue applies rstd·(acc − μ·c) + bias with μ, rstd from ln_stats[row][3][2]
     uint16_t *ln_x = nullptr;
     float *ln_stats = nullptr;
+    //   EPI_RESID_HL / EPI_PATCH_HL: the residual stream is the bf16 pair (ln_x, res_lo) instead
+    //     of out_f32 (see "Residual stream as bf16 pairs"): the residual is read from and the
+    //     result written to the pair; the statistics only when ln_stats != null
+    uint16_t *res_lo = nullptr;
     const float *ln_c = nullptr;
     float ln_eps = 1e-6f;
     // implicit-GEMM patch embedding (patch_gemm_kernel): A[m][k] is read from the u8
@@ -70,6 +80,40 @@ struct GemmArgs {
 // bf16(LN(x)) while |μ| ≲ σ per token; c is summed from the bf16 W′ the MFMAs
 // use, so the μ·c term cancels exactly what the MFMAs add for the mean.
 constexpr int LN_TILES = 3;  // 768 columns / 256
+
+// ------------------------------------------- Residual stream as bf16 pairs
+// Under the LayerNorm fold the residual stream x is kept as two bf16 arrays, hi =
+// RNE(x) — exactly the bf16(x) the QKV / fc1 GEMMs read as A — and lo = RNE(x − hi),
+// instead of an f32 array plus that bf16 copy: the producers (patch GEMM, O-proj,
+// fc2, cls_init) write 4 B per element instead of 6 and the residual epilogues read
+// the same 4 B.  The value is x′ = f32(hi) + f32(lo), ~17 significant bits (|x − x′|
+// ≤ 2⁻¹⁸|x|, against the 2⁻⁹ of the bf16 GEMM operands); every reader forms x′ with
+// hl_value's arithmetic, and the producers compute the LN statistics from that same
+// x′, so the skinny (ln_emit_kernel) and tiled paths stay bit-identical.
+__device__ __forceinline__ float4 bf16x4_f32(uint2 u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ uint2 pack_bf16x4(float4 v) { return make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)); }
+// (hi.x, hi.y, lo.x, lo.y) of four consecutive elements
+__device__ __forceinline__ uint4 hl_split(float4 x) {
+    const uint2 h = pack_bf16x4(x);
+    const float4 hf = bf16x4_f32(h);
+    const uint2 l = pack_bf16x4(make_float4(x.x - hf.x, x.y - hf.y, x.z - hf.z, x.w - hf.w));
+    return make_uint4(h.x, h.y, l.x, l.y);
+}
+__device__ __forceinline__ float4 hl_value(uint4 p) {
+    const float4 h = bf16x4_f32(make_uint2(p.x, p.y)), l = bf16x4_f32(make_uint2(p.z, p.w));
+    return make_float4(h.x + l.x, h.y + l.y, h.z + l.z, h.w + l.w);
+}
+__device__ __forceinline__ uint4 hl_load(const uint16_t *hi, const uint16_t *lo) {
+    const uint2 h = *reinterpret_cast<const uint2 *>(hi), l = *reinterpret_cast<const uint2 *>(lo);
+    return make_uint4(h.x, h.y, l.x, l.y);
+}
+__device__ __forceinline__ void hl_store(uint4 p, uint16_t *hi, uint16_t *lo) {
+    *reinterpret_cast<uint2 *>(hi) = make_uint2(p.x, p.y);
+    *reinterpret_cast<uint2 *>(lo) = make_uint2(p.z, p.w);
+}
 
 // Chan combination of the LN_TILES partials of one row → (rstd, −rstd·μ)
 __device__ __forceinline__ float2 ln_row_scale(const float *__restrict__ st, float eps) {
@@ -264,18 +308,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
 
 // Final LayerNorm of the CLS row of each image + the two /embed outputs.
 template <int NV>
-__global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__ hidden, int tokens,
+// hi != null: the rows are the bf16 pairs (hi, lo) instead of `hidden`.
+__global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
+                                                      const uint16_t *__restrict__ lo, int tokens,
                                                       const float *__restrict__ g, const float *__restrict__ b,
                                                       float eps, float *__restrict__ raw, float *__restrict__ normed) {
     constexpr int H = 256 * NV;
     const int lane = threadIdx.x;
     const int img = blockIdx.x;
-    const float4 *xr = reinterpret_cast<const float4 *>(hidden + (int64_t)img * tokens * H);
+    const int64_t r0 = (int64_t)img * tokens * H;
+    const float4 *xr = reinterpret_cast<const float4 *>(hidden + r0);
     float4 v[NV];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-        v[i] = xr[lane + 64 * i];
+        v[i] = hi ? hl_value(hl_load(hi + r0 + 4 * (lane + 64 * i), lo + r0 + 4 * (lane + 64 * i))) : xr[lane + 64 * i];
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
     const float mean = wave_sum(s) * (1.0f / H);
@@ -311,12 +358,26 @@ __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__
 }
 
 // hidden[img*tokens + 0] = cls + pos[0]; with ln_x: also its bf16 copy and LN partials
-// (the LayerNorm fold's producer for the CLS rows; H = 768, one wave per 256 columns)
+// (the LayerNorm fold's producer for the CLS rows; H = 768, one wave per 256 columns);
+// with lo: the row as the bf16 pair (ln_x, lo) and no f32 row
 __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidden, int tokens, int H,
                                                       const float *__restrict__ cls, const float *__restrict__ pos,
-                                                      uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats) {
+                                                      uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats,
+                                                      uint16_t *__restrict__ lo) {
     const int img = blockIdx.x;
     const int64_t row = (int64_t)img * tokens;
+    if (lo != nullptr) {
+        if (threadIdx.x < 64 * LN_TILES) {
+            const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const int c = t * 256 + lane * 4;
+            const uint4 p = hl_split(make_float4(cls[c] + pos[c], cls[c + 1] + pos[c + 1], cls[c + 2] + pos[c + 2],
+                                                 cls[c + 3] + pos[c + 3]));
+            hl_store(p, ln_x + row * H + c, lo + row * H + c);
+            const float2 st = ln_row_stats(hl_value(p));
+            if (lane == 0) *reinterpret_cast<float2 *>(ln_stats + (row * LN_TILES + t) * 2) = st;
+        }
+        return;
+    }
     for (int c = threadIdx.x; c < H; c += 256) hidden[row * H + c] = cls[c] + pos[c];
     if (ln_x != nullptr && threadIdx.x < 64 * LN_TILES) {
         const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -603,12 +664,14 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const uint16_t *__res
 // LN2 / MLP on the n CLS rows gathered into a compact [n][768] stream.
 
 // hc[i][:] = hidden[i * tokens][:]   (one block of 192 lanes per image, float4)
-__global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict__ hidden, int tokens,
-                                                        float *__restrict__ hc) {
+__global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
+                                                        const uint16_t *__restrict__ lo, int tokens, float *__restrict__ hc) {
     constexpr int H = 768;
     const int img = blockIdx.x;
+    const int64_t r0 = (int64_t)img * tokens * H;
     reinterpret_cast<float4 *>(hc + (int64_t)img * H)[threadIdx.x] =
-        reinterpret_cast<const float4 *>(hidden + (int64_t)img * tokens * H)[threadIdx.x];
+        hi ? hl_value(hl_load(hi + r0 + 4 * threadIdx.x, lo + r0 + 4 * threadIdx.x))
+           : reinterpret_cast<const float4 *>(hidden + r0)[threadIdx.x];
 }
 
 // CLS-query attention, one wave per (image, head), tokens <= 256, head dim 64.
