@@ -2,7 +2,7 @@
 # Interleaved A/B of embed throughput under different settings.
 # usage: tools/ab_env.sh ROUNDS "VAR=a --flag" "VAR=b" ... [-- extra bench args]
 # A setting's VAR=value words go to the environment, its --words to bench.py.
-# Prints one line per run: setting, parts, images/s, ms/step.
+# Prints one line per run: setting, parts, images/s, ms/step.  AB_PARTS="2" limits the parts settings.
 set -u
 ROUNDS=$1; shift
 SETS=()
@@ -11,7 +11,7 @@ while [ $# -gt 0 ] && [ "$1" != "--" ]; do SETS+=("$1"); shift; done
 mkdir -p gpurun_out
 for r in $(seq "$ROUNDS"); do
   for s in "${SETS[@]}"; do
-    for parts in 1 2; do
+    for parts in ${AB_PARTS:-1 2}; do
       ev=(); fl=()
       for w in $s; do case $w in --*) fl+=("$w");; *) ev+=("$w");; esac; done
       out=$(env "${ev[@]}" timeout -k 10 300 python -u bench.py --no-cpu --no-search --ingest-images 0 --jpeg-images 0 \
