@@ -466,6 +466,30 @@ def main():
             "responses_ok": len(resp) == len(files) and all(r["message"] == "Successfully!" for r in resp),
         }
         ix.close()
+        # bulk ingest: the same batches through ingest_stream (decode of batch i+1 under the
+        # embed + upsert of batch i)
+        sreps = 8
+        ix = importlib.import_module(f"{PKG}.index").Index("bench-ingest-stream", dimension=768, dtype="float16",
+                                                           capacity=len(files) * (sreps + 1), device=local)
+        for _ in core.ingest_stream([files], ix):  # warm
+            pass
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        nresp = 0
+        for resp in core.ingest_stream([files] * sreps, ix):
+            nresp += len(resp)
+        torch.cuda.synchronize()
+        barrier()
+        els = max_over_ranks(time.perf_counter() - t0)
+        jpeg["ingest_core"]["stream"] = {
+            "value": world * len(files) * sreps / els,
+            "unit": "images/s (JPEG bytes -> responses, pipelined)",
+            "what": f"ingesting.core.ingest_stream over {sreps} batches of {len(files)} JPEG uploads: validation + "
+                    f"decode of batch i+1 (worker thread, side stream) under the embed + upsert of batch i",
+            "responses_ok": nresp == len(files) * sreps,
+        }
+        ix.close()
 
     model.close()
     del images, raw, nrm

@@ -463,9 +463,10 @@ class Index:
         keep = list(last.values())
         if len(keep) != len(ids):
             vecs = vecs[torch.tensor(keep, dtype=torch.int64, device=vecs.device)]
-        if not bool((vecs != 0).any(dim=1).all()):
-            raise ValueError("Dense vectors must contain at least one non-zero value for the cosine metric")
+        nonzero = (vecs != 0).any(dim=1).all()  # queued behind the producer of vecs; read below
         items = [(ids[i], None, dict(metadata[i] or {})) for i in keep]
+        if not bool(nonzero):
+            raise ValueError("Dense vectors must contain at least one non-zero value for the cosine metric")
         with self._mu:
             self._upsert_locked(items, vecs)
         return {"upserted_count": len(items)}

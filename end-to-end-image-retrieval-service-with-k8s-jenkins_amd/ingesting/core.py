@@ -19,8 +19,9 @@ deployment passes an object that uploads and signs.
 """
 from __future__ import annotations
 
+import sys
 import uuid
-from typing import Callable, Sequence
+from typing import Callable, Iterable, Iterator, Sequence
 
 from fastapi import HTTPException
 
@@ -54,17 +55,11 @@ def validate_extension(filename: str | None) -> str:
     return ext
 
 
-def ingest_many(files: Sequence[tuple], index, storage: StorageHook | None = None,
-                id_factory: Callable[[], str] | None = None) -> list[dict]:
-    """files: ``(filename, bytes[, content_type])`` per image → one response dict per image.
-
-    Every image is validated before anything is embedded or stored (a bad file
-    fails the whole call with the reference's 400, and nothing is ingested).
-    ``index`` may be a zero-argument callable (opened only once the batch is valid)."""
+def _prepare(files: Sequence[tuple]):
+    """Extension checks, then the validation decode (ingesting/main.py:111-119) of every file:
+    (names, blobs, content types, extensions, decoded images).  Raises the reference's 400s."""
     from ..embedding import main as emb
 
-    storage = storage or StorageHook()
-    id_factory = id_factory or (lambda: str(uuid.uuid4()))
     names, blobs, ctypes_, exts = [], [], [], []
     for f in files:
         filename, data = f[0], f[1]
@@ -73,13 +68,23 @@ def ingest_many(files: Sequence[tuple], index, storage: StorageHook | None = Non
         blobs.append(data)
         ctypes_.append(f[2] if len(f) > 2 else None)
     if not blobs:
-        return []
+        return names, blobs, ctypes_, exts, []
     try:  # validation decode (ingesting/main.py:116-119), on the GPU for baseline JPEGs
         images = emb.decode_many(blobs)
     except HTTPException as e:
         if e.status_code == 400:
             raise HTTPException(status_code=400, detail="Invalid image file")
         raise
+    return names, blobs, ctypes_, exts, images
+
+
+def _finish(prep, index, storage: StorageHook, id_factory: Callable[[], str]) -> list[dict]:
+    """Embed the decoded batch, then ids, storage hook and ONE upsert (ingesting/main.py:124-168)."""
+    from ..embedding import main as emb
+
+    names, blobs, ctypes_, exts, images = prep
+    if not blobs:
+        return []
     raw, _ = emb.get_embedder().embed_images(images)
     ids = [id_factory() for _ in blobs]
     paths = [f"images/{fid}.{ext}" for fid, ext in zip(ids, exts)]
@@ -91,6 +96,76 @@ def ingest_many(files: Sequence[tuple], index, storage: StorageHook | None = Non
     index.upsert_tensor(ids, raw, [{"gcs_path": p, "filename": n} for p, n in zip(paths, names)])
     return [{"message": "Successfully!", "file_id": fid, "gcs_path": p, "signed_url": u}
             for fid, p, u in zip(ids, paths, urls)]
+
+
+def ingest_many(files: Sequence[tuple], index, storage: StorageHook | None = None,
+                id_factory: Callable[[], str] | None = None) -> list[dict]:
+    """files: ``(filename, bytes[, content_type])`` per image → one response dict per image.
+
+    Every image is validated before anything is embedded or stored (a bad file
+    fails the whole call with the reference's 400, and nothing is ingested).
+    ``index`` may be a zero-argument callable (opened only once the batch is valid)."""
+    return _finish(_prepare(files), index, storage or StorageHook(), id_factory or (lambda: str(uuid.uuid4())))
+
+
+def ingest_stream(batches: Iterable[Sequence[tuple]], index, storage: StorageHook | None = None,
+                  id_factory: Callable[[], str] | None = None) -> Iterator[list[dict]]:
+    """Bulk ingest: ``ingest_many`` over a stream of upload batches, pipelined.  Batch i+1 is
+    validated and decoded (host Huffman on a worker thread, GPU reconstruction on a side
+    stream) while the GPU embeds batch i and the host upserts it; yields each batch's
+    responses in order, exactly what ``ingest_many`` returns for it.  A batch that fails
+    validation raises its 400 when it is reached (the batches before it are ingested, the
+    ones after it are not)."""
+    import torch
+
+    from ..embedding import main as emb
+
+    storage = storage or StorageHook()
+    id_factory = id_factory or (lambda: str(uuid.uuid4()))
+    dev = emb.get_embedder().device
+    side = torch.cuda.Stream(device=dev)
+    main = torch.cuda.current_stream(dev)
+
+    def prepare(files):
+        with torch.cuda.device(dev), torch.cuda.stream(side):
+            prep = _prepare(files)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return prep, ev
+
+    it = iter(batches)
+    # both threads hold the GIL for short Python stretches between ctypes calls (which release
+    # it); at the default 5 ms switch interval each hand-off can stall the other thread for
+    # that long (tools/ingest_probe.py: 17.1k images/s at 5 ms, 18.4k at 1 ms)
+    old_switch = sys.getswitchinterval()
+    sys.setswitchinterval(min(old_switch, 1e-3))
+    try:
+        yield from _pipeline(it, prepare, main, index, storage, id_factory)
+    finally:
+        sys.setswitchinterval(old_switch)
+
+
+def _pipeline(it, prepare, main, index, storage, id_factory):
+    """ingest_stream's loop: the worker prepares batch i+1 while this thread finishes batch i."""
+    import concurrent.futures as cf
+
+    import torch
+
+    opened = None
+    with cf.ThreadPoolExecutor(1) as ex:
+        first = next(it, None)
+        fut = ex.submit(prepare, first) if first is not None else None
+        while fut is not None:
+            prep, ev = fut.result()
+            nxt = next(it, None)
+            fut = ex.submit(prepare, nxt) if nxt is not None else None
+            main.wait_event(ev)
+            for im in prep[4]:
+                if isinstance(im, torch.Tensor) and im.is_cuda:
+                    im.record_stream(main)
+            if opened is None:
+                opened = index() if callable(index) else index
+            yield _finish(prep, opened, storage, id_factory)
 
 
 def push_one(filename: str, data: bytes, index, content_type: str | None = None, storage: StorageHook | None = None,

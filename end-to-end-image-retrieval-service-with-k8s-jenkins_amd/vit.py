@@ -69,6 +69,23 @@ def load_checkpoint_dir(path: str) -> tuple[dict, dict, dict]:
     return dict(sd), cfg, pre
 
 
+def _packed_view(ims: Sequence, device) -> "torch.Tensor | None":
+    """[n, H, W, 3] view when ``ims`` are equal-size contiguous u8 device tensors lying back to
+    back in one buffer (what JpegDecoder.decode returns for a chunk), else None."""
+    first = ims[0]
+    if not (isinstance(first, torch.Tensor) and first.is_cuda and first.device == torch.device(device)
+            and first.dtype == torch.uint8 and first.is_contiguous()):
+        return None
+    n, z = len(ims), first.numel()
+    base = first.data_ptr()
+    for k, im in enumerate(ims):
+        if not (isinstance(im, torch.Tensor) and im.shape == first.shape and im.is_cuda
+                and im.data_ptr() == base + k * z and im.is_contiguous()
+                and im.untyped_storage().data_ptr() == first.untyped_storage().data_ptr()):
+            return None
+    return first.as_strided((n,) + tuple(first.shape), (z,) + tuple(first.stride()))
+
+
 class VitMsnEmbedder:
     """One ``rc_model`` on one GPU: fixed weights, workspace for ``max_batch`` images."""
 
@@ -169,7 +186,10 @@ class VitMsnEmbedder:
         for idx in groups.values():
             for s0 in range(0, len(idx), self.max_batch):
                 chunk = idx[s0:s0 + self.max_batch]
-                if all(isinstance(images[i], torch.Tensor) for i in chunk):
+                x = _packed_view([images[i] for i in chunk], self.device)
+                if x is not None:  # consecutive views of one decode buffer: no stack copy
+                    pass
+                elif all(isinstance(images[i], torch.Tensor) for i in chunk):
                     x = torch.stack([images[i].to(self.device) for i in chunk])
                 elif not any(isinstance(images[i], torch.Tensor) for i in chunk):
                     x = torch.from_numpy(np.stack([np.asarray(images[i], dtype=np.uint8) for i in chunk]))
@@ -178,7 +198,13 @@ class VitMsnEmbedder:
                                      if not isinstance(images[i], torch.Tensor) else images[i].to(self.device)
                                      for i in chunk])
                 r, m = self.embed(x, normalized=normalized)
-                sel = torch.tensor(chunk, dtype=torch.int64, device=self.device)
+                c0 = chunk[0]
+                if chunk == list(range(c0, c0 + len(chunk))):  # in input order: a slice copy, no host sync
+                    raw[c0:c0 + len(chunk)].copy_(r)
+                    if normalized:
+                        nrm[c0:c0 + len(chunk)].copy_(m)
+                    continue
+                sel = torch.tensor(chunk, dtype=torch.int64).pin_memory().to(self.device, non_blocking=True)
                 raw.index_copy_(0, sel, r)
                 if normalized:
                     nrm.index_copy_(0, sel, m)

@@ -4,6 +4,8 @@
   returns, per image, what a loop of single ``/push_image`` calls returns
   (reference ``ingesting/main.py:101-168``), and the index it fills answers
   ``search`` (``retriever/utils.py:59-66``) like the single-push index.
+* ``ingest_stream`` (bulk ingest: decode of batch i+1 under the embed of batch i)
+  returns per batch what ``ingest_many`` returns and stores the same bits.
 * The ``/push_image`` → ``/search_image`` services (reference
   ``tests/test_ingesting.py:47-50``, ``tests/test_retriever.py:46-54``).
 * BASELINE config 5, single-GPU shape: 65,536 synthetic images embedded on the
@@ -70,6 +72,46 @@ def test_ingest_many_equals_single_pushes(cuda):
     assert ret.search(batch_ix, q, top_k=5)[0] == "id-5"
     batch_ix.close()
     single_ix.close()
+
+
+def test_ingest_stream_equals_ingest_many_per_batch(cuda):
+    """The pipelined bulk ingest (decode of batch i+1 under the embed of batch i) returns, batch
+    by batch, what ingest_many returns, and stores the same vectors bit for bit."""
+    core = import_pkg("ingesting.core")
+    index = import_pkg("index")
+    files = _jpegs(48, 5)  # JPEG + PNG, three sizes
+    batches = [files[:16], files[16:40], files[40:]]
+    ids_a = (f"s-{i}" for i in itertools.count())
+    ids_b = (f"s-{i}" for i in itertools.count())
+    ix_s = index.Index("stream", dimension=768, capacity=64, device=cuda, shards=2)
+    ix_m = index.Index("many", dimension=768, capacity=64, device=cuda)
+    got = list(core.ingest_stream(iter(batches), ix_s, id_factory=lambda: next(ids_a)))
+    want = [core.ingest_many(b, ix_m, id_factory=lambda: next(ids_b)) for b in batches]
+    assert got == want and [len(r) for r in got] == [16, 24, 8]
+    ids = [r["file_id"] for rs in got for r in rs]
+    fa, fb = ix_s.fetch(ids), ix_m.fetch(ids)
+    for i in ids:
+        assert np.array_equal(fa["vectors"][i]["values"], fb["vectors"][i]["values"])
+        assert fa["vectors"][i]["metadata"] == fb["vectors"][i]["metadata"]
+    ix_s.close()
+    ix_m.close()
+
+
+def test_ingest_stream_stops_at_an_invalid_batch(cuda):
+    from fastapi import HTTPException
+
+    core = import_pkg("ingesting.core")
+    index = import_pkg("index")
+    ix = index.Index("stream-rej", dimension=768, capacity=32, device=cuda)
+    good = _jpegs(6, 7)
+    bad = _jpegs(2, 8) + [("bad.jpg", b"This is not an image.", "image/jpeg")]
+    gen = core.ingest_stream(iter([good, bad, _jpegs(4, 9)]), ix)
+    assert len(next(gen)) == 6
+    with pytest.raises(HTTPException) as e:
+        next(gen)
+    assert e.value.status_code == 400 and e.value.detail == "Invalid image file"
+    assert len(ix) == 6  # the invalid batch and the ones after it are not ingested
+    ix.close()
 
 
 def test_ingest_many_rejects_before_ingesting(cuda):
