@@ -311,23 +311,51 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 
     // epilogue: acc[mq][nq][mi][ni][j] = C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
-    if constexpr (epi_bf16_out(EPI) && (ABL & 64) != 0 && !epi_ln(EPI)) {
-        // diagnostic: no LDS staging — bf16 pairs of 16-lane rows swapped with
-        // v_permlane16_swap so each lane stores 16 B (8 consecutive columns)
+    // fc1 (GELU + LayerNorm-fold consumer): no LDS staging — bf16 pairs of 16-lane rows
+    // swapped with v_permlane16_swap so each lane stores 16 B (8 consecutive columns);
+    // lane (g, li) of rows 16-block holds columns 4g..4g+3 of both 16-column halves ni, the
+    // swap of rows 1<->0 and 3<->2 between the ni halves makes them 8 contiguous columns.
+    // (Also ABL 64 for the other bf16 epilogues in diagnostic builds.)
+    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN || (epi_bf16_out(EPI) && (ABL & 64) != 0 && !epi_ln(EPI));
+    if constexpr (DIRECT) {
+        float4 bq[2][2], cq[2][2];
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                if constexpr (epi_ln(EPI)) {
+                    bq[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+                    cq[nq][ni] = *reinterpret_cast<const float4 *>(a.ln_c + n0 + cl);
+                } else {
+                    bq[nq][ni] = biasr[nq][ni];
+                }
+            }
 #pragma unroll
         for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
-                const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                const int rl = grp * 128 + mq * 64 + mi * 16 + li;
+                const int row = m0 + rl;
+                float2 r = make_float2(1.f, 0.f);
+                if constexpr (epi_ln(EPI)) r = *reinterpret_cast<const float2 *>(smem + 2 * STAGE + rl * 8);
 #pragma unroll
                 for (int nq = 0; nq < 2; ++nq) {
                     uint32_t u[2][2];
 #pragma unroll
                     for (int ni = 0; ni < 2; ++ni) {
                         const f32x4 v4 = acc[mq][nq][mi][ni];
-                        const float4 b4 = biasr[nq][ni];
-                        f32x2 lo = f32x2{v4[0] + b4.x, v4[1] + b4.y}, hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
-                        if constexpr (epi_gelu(EPI)) {
+                        const float4 b4 = bq[nq][ni];
+                        f32x2 lo, hi;
+                        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′, as the staged epilogue
+                            const float4 c4 = cq[nq][ni];
+                            lo = f32x2{fmaf(r.x, v4[0], fmaf(r.y, c4.x, b4.x)), fmaf(r.x, v4[1], fmaf(r.y, c4.y, b4.y))};
+                            hi = f32x2{fmaf(r.x, v4[2], fmaf(r.y, c4.z, b4.z)), fmaf(r.x, v4[3], fmaf(r.y, c4.w, b4.w))};
+                        } else {
+                            lo = f32x2{v4[0] + b4.x, v4[1] + b4.y};
+                            hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
+                        }
+                        if constexpr (epi_gelu(EPI) && !(ABL & 16)) {
                             lo = gelu_fast2(lo);
                             hi = gelu_fast2(hi);
                         }
