@@ -468,17 +468,24 @@ def main():
         ix.close()
         # bulk ingest: the same batches through ingest_stream (decode of batch i+1 under the
         # embed + upsert of batch i)
-        sreps = 8
+        sreps = 16
         ix = importlib.import_module(f"{PKG}.index").Index("bench-ingest-stream", dimension=768, dtype="float16",
-                                                           capacity=len(files) * (sreps + 1), device=local)
-        for _ in core.ingest_stream([files], ix):  # warm
+                                                           capacity=len(files) * (sreps + 2), device=local)
+        for _ in core.ingest_stream([files] * 2, ix):  # warm
             pass
         torch.cuda.synchronize()
+        import gc
+
+        gc.collect()  # a full collection of this large process inside the timed loop costs ~60 ms
         barrier()
         t0 = time.perf_counter()
         nresp = 0
+        tb = time.perf_counter()
         for resp in core.ingest_stream([files] * sreps, ix):
             nresp += len(resp)
+            if os.environ.get("BENCH_DEBUG"):
+                log(f"ingest_stream batch {nresp // len(files)}: {(time.perf_counter() - tb) * 1e3:.1f} ms")
+                tb = time.perf_counter()
         torch.cuda.synchronize()
         barrier()
         els = max_over_ranks(time.perf_counter() - t0)

@@ -25,6 +25,12 @@ def main():
     datas = synthetic_jpegs(256, 11)
     files = [(f"img{i}.jpg", d, "image/jpeg") for i, d in enumerate(datas)]
     ix = index.Index("probe", dimension=768, dtype="float16", capacity=256 * 40, device=0)
+    if os.environ.get("PROBE_BENCH_MODEL"):  # the bench's own model + a JPEG stream first, as bench.py does
+        vit = import_pkg("vit")
+        bm = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=0, max_batch=256)
+        for _ in bm.embed_jpeg_stream([datas] * 4):
+            pass
+        torch.cuda.synchronize()
     core.ingest_many(files, ix)
     torch.cuda.synchronize()
     t = {"prepare": 0.0, "embed": 0.0, "finish_host": 0.0}
