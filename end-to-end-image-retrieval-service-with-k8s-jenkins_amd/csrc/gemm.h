@@ -857,6 +857,76 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
     }
 }
 
+// Split-K skinny GEMM with an f32 residual epilogue, for the last layer's fc2 on the
+// CLS rows (M = images, N = 768, K = 3072; every batch size, so the CLS rows of an image
+// get the same bits in any batch): the skinny kernel's one wave per 16
+// rows x 32 columns walks all of K as a chain of dependent 16x16x32 MFMAs and global
+// loads (54 us at M = 128); here KS waves split K, write f32 partials [KS][M][N], and
+// skinny_reduce_kernel adds them in ks order + bias + the residual (deterministic).
+// Used only on the CLS rows, so batch invariance is unaffected (the full-layer GEMMs of
+// a small batch keep the skinny kernel, bit-identical to the tiled ones).
+template <int NI, int KS>
+__global__ __launch_bounds__(256) void gemm_skinny_splitk_kernel(GemmArgs a, float *__restrict__ part) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nct * nrt * KS) return;
+    const int ks = w % KS, tile = w / KS;
+    const int ct = tile % nct, rt = tile / nct;
+    const int KL = a.K / KS, k0 = ks * KL;
+    const int n0 = ct * 16 * NI, row = rt * 16 + li;
+    const uint16_t *Ar = a.A + (int64_t)row * a.K + k0 + 8 * g;
+    const uint16_t *Wr = a.W + (int64_t)(n0 + li) * a.K + k0 + 8 * g;
+    f32x4 acc[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int k = 0; k < KL; k += 32) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8 *>(Ar + k);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+            const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(Wr + (int64_t)ni * 16 * a.K + k);
+            acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af, acc[ni], 0, 0, 0);
+        }
+    }
+    if (row >= a.M) return;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+        *reinterpret_cast<f32x4 *>(part + ((int64_t)ks * a.M + row) * a.N + n0 + ni * 16 + 4 * g) = acc[ni];
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmArgs a, const float *__restrict__ part) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of outputs
+    if (i >= (int64_t)a.M * a.N / 4) return;
+    const int64_t e = i * 4;
+    const int c = (int)(e % a.N);
+    float4 s = *reinterpret_cast<const float4 *>(part + e);
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks) {
+        const float4 p = *reinterpret_cast<const float4 *>(part + (int64_t)ks * a.M * a.N + e);
+        s = make_float4(s.x + p.x, s.y + p.y, s.z + p.z, s.w + p.w);
+    }
+    const float4 b = *reinterpret_cast<const float4 *>(a.bias + c);
+    float4 *o = reinterpret_cast<float4 *>(a.out_f32 + e);
+    const float4 r = *o;
+    *o = make_float4(r.x + (s.x + b.x), r.y + (s.y + b.y), r.z + (s.z + b.z), r.w + (s.w + b.w));
+}
+
+constexpr int SKINNY_KS = 4;
+
+// out_f32 [M][N] += A·Wᵀ + bias on the split-K skinny path (part: >= SKINNY_KS·M·N floats)
+inline void launch_skinny_splitk_resid(const GemmArgs &a, float *part, hipStream_t s) {
+    RC_REQUIRE(a.M >= 1 && a.N % 32 == 0 && a.K % (32 * SKINNY_KS) == 0 && a.out_f32 && !a.ln_x, RC_ERR_UNSUPPORTED,
+               "split-K skinny GEMM: N % 32 == 0, K % 128 == 0, f32 residual");
+    const int waves = ((a.M + 15) / 16) * (a.N / 32) * SKINNY_KS;
+    hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS>), dim3((waves + 3) / 4), dim3(256), 0, s, a, part);
+    RC_LAUNCH_CHECK();
+    const int64_t n4 = (int64_t)a.M * a.N / 4;
+    hipLaunchKernelGGL(skinny_reduce_kernel<SKINNY_KS>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, a, part);
+    RC_LAUNCH_CHECK();
+}
+
 // LayerNorm-fold producer pass for rows a skinny GEMM wrote (M <= 256): one wave per
 // (row, 256-column tile), the same lane -> column map and reductions as the tiled
 // kernels' epilogues (ln_emit_row), so the partials are bit-identical for any M.

@@ -141,6 +141,7 @@ struct rc_model {
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
     bool cls_only_last = true;     // rc_model_set_last_layer / RC_EMBED_FULL_LAST=1
     float *cls_hidden = nullptr, *cls_stats = nullptr;
+    float *cls_part = nullptr;     // split-K partials of the CLS-row fc2 [SKINNY_KS][Cp][H]
     uint16_t *cls_ln = nullptr, *cls_attn = nullptr, *cls_mlp = nullptr;
     uint8_t *resized = nullptr, *resize_tmp = nullptr;
     size_t resize_tmp_bytes = 0;
@@ -420,7 +421,13 @@ void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *
         layernorm(m, hc, L.ln2_w, L.ln2_b, lc, n, s);
         gemm<EPI_GELU_BF16>(m, GemmArgs{lc, L.w_fc1, L.b_fc1, n, c.mlp, H, mc, nullptr, nullptr, 1}, s);
     }
-    gemm<EPI_RESID_F32>(m, GemmArgs{mc, L.w_fc2, L.b_fc2, n, H, c.mlp, nullptr, hc, nullptr, 1}, s);
+    {  // fc2 (K = 3072) split over K: the plain skinny kernel's K chain is latency-bound
+        const GemmArgs f2{mc, L.w_fc2, L.b_fc2, n, H, c.mlp, nullptr, hc, nullptr, 1};
+        const double flops = 2.0 * f2.M * f2.N * f2.K;
+        const int t0 = m->timers[T_GEMM].begin(s);
+        launch_skinny_splitk_resid(f2, m->cls_part + (int64_t)i0 * SKINNY_KS * H, s);  // per part: disjoint
+        m->timers[T_GEMM].end(t0, s, flops);
+    }
 }
 
 // Encoder for images [i0, i0 + n) of the batch (u8 S x S x 3 images at `images`,
@@ -584,6 +591,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             const int Cp = B + gemm_row_pad();  // compact CLS streams (+ the rows a tile reads past n)
             m->cls_hidden = (float *)m->alloc((size_t)Cp * H * 4);
             m->cls_stats = (float *)m->alloc((size_t)Cp * 2 * LN_TILES * 4);
+            m->cls_part = (float *)m->alloc((size_t)SKINNY_KS * Cp * H * 4);
             RC_HIP(hipMemset(m->cls_stats, 0, (size_t)Cp * 2 * LN_TILES * 4));
             m->cls_ln = (uint16_t *)m->alloc((size_t)Cp * H * 2);
             m->cls_attn = (uint16_t *)m->alloc((size_t)Cp * H * 2);
