@@ -956,7 +956,7 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 // deferred-store persistent kernel: each lost on every shape and was removed.)
 enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9 };
 
-inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
+inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
     if (a.N % 256 != 0) return GEMM_V1;
@@ -965,7 +965,10 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
     // position read + write): the two-workgroup kernel overlaps that epilogue
     // with the co-resident workgroup's MFMAs (O-proj 96 -> 89 us at batch 256,
     // tools/gemm_calib.py).  Everything else streams K at 128 flop/B: ping-pong.
-    if (a.N <= 768 && a.K <= 768) return GEMM_W2;
+    // With the residual stream as bf16 pairs the O-proj epilogue moves 8 B per element
+    // instead of 10 and the ping-pong kernel wins there too (+0.5-1.1 % images/s at
+    // parts = 2, profiles/r02/r02_ab_results.txt).
+    if (a.N <= 768 && a.K <= 768 && !pair_epilogue) return GEMM_W2;
     return GEMM_PINGPONG;
 }
 
@@ -996,7 +999,7 @@ template <int EPI>
 void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
-    const int pick = gemm_pick(a, variant, epi_patch(EPI));
+    const int pick = gemm_pick(a, variant, epi_patch(EPI), epi_hl(EPI));
     if constexpr (epi_hl(EPI)) {
         RC_REQUIRE(a.ln_x && a.res_lo && pick != GEMM_V1, RC_ERR_UNSUPPORTED,
                    "bf16-pair residual epilogues: ln_x + res_lo, ping-pong / two-workgroup / skinny kernels");
