@@ -370,7 +370,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                     }
                     const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
                     if (row < a.M) {
-                        uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * a.N + col);
+                        uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + col);
                         const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
                         if constexpr ((ABL & 32) != 0) nt_store16(dst, val);
                         else *dst = val;
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
             if constexpr ((ABL & 8) != 0) {
                 asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
             } else if (m0 + rl < a.M) {
-                uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8);
+                uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8);
                 if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
                 else *dst = v;
             }
@@ -522,7 +522,8 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
             const int id = it * 256 + tid;
             const int rl = id >> 5, ch = id & 31;
             const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
-            if (m0 + rl < a.M) *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+            if (m0 + rl < a.M)
+                *reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8) = v;
         }
         return;
     }
@@ -851,7 +852,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
                 v2 = hi.x;
                 v3 = hi.y;
             }
-            *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * a.N + c) =
+            *reinterpret_cast<uint2 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + c) =
                 make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
         }
     }
@@ -1000,6 +1001,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
     const int pick = gemm_pick(a, variant, epi_patch(EPI), epi_hl(EPI));
+    RC_REQUIRE(a.ldc == 0 || (a.ldc >= a.N && pick != GEMM_V1 && epi_bf16_out(EPI)), RC_ERR_UNSUPPORTED,
+               "an output row stride (ldc) needs a bf16 epilogue on the ping-pong / two-workgroup / skinny kernels");
     if constexpr (epi_hl(EPI)) {
         RC_REQUIRE(a.ln_x && a.res_lo && pick != GEMM_V1, RC_ERR_UNSUPPORTED,
                    "bf16-pair residual epilogues: ln_x + res_lo, ping-pong / two-workgroup / skinny kernels");

@@ -391,18 +391,32 @@ void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint
 // full-batch ones (a GEMM row's result does not depend on M), so a CLS row gets
 // the same arithmetic as in the full layer except attention's summation order.
 void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *qkv, const float *hidden,
-                    const uint16_t *hi, const uint16_t *lo, float scale, hipStream_t s) {
+                    const uint16_t *hi, const uint16_t *lo, const float *st_rows, float scale, hipStream_t s) {
     const auto &c = m->cfg;
     const int H = c.hidden, T = m->tokens;
     float *hc = m->cls_hidden + (int64_t)i0 * H;
     uint16_t *ac = m->cls_attn + (int64_t)i0 * H, *lc = m->cls_ln + (int64_t)i0 * H;
     uint16_t *mc = m->cls_mlp + (int64_t)i0 * c.mlp;
-    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, hi, lo, T, hc);
+    // LayerNorm fold: the QKV GEMM before this produced K and V only; Q is needed for the
+    // CLS rows alone, from their bf16 rows and statistics gathered compact (same arithmetic
+    // as the full QKV GEMM: the skinny / tiled kernels give a row the same bits at any M)
+    const bool q_cls = m->ln_fold && hi != nullptr;
+    float *cst = m->cls_stats + (int64_t)i0 * 2 * LN_TILES;
+    uint16_t *qc = m->cls_mlp + (int64_t)i0 * c.mlp;  // [n][H] compact queries (fc1 overwrites it later)
+    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, hi, lo, T, hc, q_cls ? lc : nullptr,
+                       st_rows, cst);
     RC_LAUNCH_CHECK();
+    if (q_cls) {
+        GemmArgs q{lc, L.w_qkv_f, L.b_qkv_f, n, H, H, qc, nullptr, nullptr, 1};
+        q.ln_c = L.c_qkv;
+        q.ln_stats = cst;
+        q.ln_eps = c.ln_eps;
+        gemm<EPI_BF16_LN>(m, q, s);
+    }
     const int ta = m->timers[T_ATTN].begin(s);
     const int items = n * c.heads;
     hipLaunchKernelGGL(attention_cls_kernel, dim3((items + 3) / 4), dim3(256), 0, s, qkv, ac, T, c.heads, items,
-                       scale * 1.4426950408889634f);
+                       scale * 1.4426950408889634f, q_cls ? qc : nullptr);
     RC_LAUNCH_CHECK();
     m->timers[T_ATTN].end(ta, s, 4.0 * items * (double)T * (H / c.heads));
     GemmArgs o{ac, L.w_o, L.b_o, n, H, H, nullptr, hc, nullptr, 1};
@@ -477,8 +491,13 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
     for (int l = 0; l < c.layers; ++l) {
         const Layer &L = m->layers[l];
         if (fold) {
-            GemmArgs a{ln, L.w_qkv_f, L.b_qkv_f, M, 3 * H, H, qkv, nullptr, nullptr, T};
-            a.ln_c = L.c_qkv;
+            // the CLS-only last layer needs Q on the CLS rows alone (last_layer_cls): K and V
+            // here, into their columns of the qkv rows
+            const bool kv_only = m->cls_only_last && l == c.layers - 1;
+            const int64_t q0 = kv_only ? H : 0;
+            GemmArgs a{ln, L.w_qkv_f + q0 * H, L.b_qkv_f + q0, M, 3 * H - (int)q0, H, qkv + q0, nullptr, nullptr, T};
+            a.ldc = 3 * H;
+            a.ln_c = L.c_qkv + q0;
             a.ln_stats = st;
             a.ln_eps = c.ln_eps;
             gemm<EPI_BF16_LN>(m, a, s);
@@ -487,7 +506,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
         }
         if (m->cls_only_last && l == c.layers - 1) {
-            last_layer_cls(m, L, i0, n, qkv, hidden, fold ? ln : nullptr, lo, scale, s);
+            last_layer_cls(m, L, i0, n, qkv, hidden, fold ? ln : nullptr, lo, st, scale, s);
             break;
         }
         const int ta = m->timers[T_ATTN].begin(s);

@@ -47,6 +47,7 @@ struct GemmArgs {
     const float *pos;   // EPI_PATCH_F32: position embeddings [tokens][N]
     int tokens;         // EPI_PATCH_F32: tokens per image (patches + 1)
     int group_m = 0;                 // ping-pong tile order: 0 = row-major, G = groups of G row tiles
+    int ldc = 0;                     // bf16 outputs: row stride in elements (0 = N)
     // LayerNorm folded across a GEMM pair (see "LayerNorm fold" below):
     //   producer (f32 epilogues): ln_x != null → also write bf16(x) rows and per-(row, 256-column
     //     tile) partial statistics (mean, M2) into ln_stats[row][N / 256][2]
@@ -664,11 +665,20 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const uint16_t *__res
 // LN2 / MLP on the n CLS rows gathered into a compact [n][768] stream.
 
 // hc[i][:] = hidden[i * tokens][:]   (one block of 192 lanes per image, float4)
+// With hc_ln: also the CLS rows' bf16 hi and LN statistics, compact (the A operand and
+// row scales of the last layer's CLS-only Q GEMM).
 __global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
-                                                        const uint16_t *__restrict__ lo, int tokens, float *__restrict__ hc) {
+                                                        const uint16_t *__restrict__ lo, int tokens, float *__restrict__ hc,
+                                                        uint16_t *__restrict__ hc_ln, const float *__restrict__ st,
+                                                        float *__restrict__ hc_st) {
     constexpr int H = 768;
     const int img = blockIdx.x;
     const int64_t r0 = (int64_t)img * tokens * H;
+    if (hc_ln != nullptr) {
+        reinterpret_cast<uint2 *>(hc_ln + (int64_t)img * H)[threadIdx.x] = reinterpret_cast<const uint2 *>(hi + r0)[threadIdx.x];
+        if (threadIdx.x < 2 * LN_TILES)
+            hc_st[img * 2 * LN_TILES + threadIdx.x] = st[(int64_t)img * tokens * 2 * LN_TILES + threadIdx.x];
+    }
     reinterpret_cast<float4 *>(hc + (int64_t)img * H)[threadIdx.x] =
         hi ? hl_value(hl_load(hi + r0 + 4 * threadIdx.x, lo + r0 + 4 * threadIdx.x))
            : reinterpret_cast<const float4 *>(hidden + r0)[threadIdx.x];
@@ -680,8 +690,11 @@ __global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict
 // of the unrounded p, out = (P·V)·(1/sum) rounded to bf16.
 // Scores: lane j owns keys j, j+64, j+128, j+192 (16-B loads of its key row);
 // P·V: 8 lanes per V row, 8 rows per load instruction (see below).
+// q != null: the CLS query rows come compact ([images][H], the last layer's Q computed
+// for the CLS rows only) instead of from qkv.
 __global__ __launch_bounds__(256) void attention_cls_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                           int tokens, int heads, int items, float scale_log2e) {
+                                                           int tokens, int heads, int items, float scale_log2e,
+                                                           const uint16_t *__restrict__ qc) {
     constexpr int HD = 64, MAXT = 256;
     __shared__ float ps[4][MAXT];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -693,7 +706,7 @@ __global__ __launch_bounds__(256) void attention_cls_kernel(const uint16_t *__re
     float sum = 0.f;
     if (live) {
         float q[HD];
-        const uint4 *q4 = reinterpret_cast<const uint4 *>(base);
+        const uint4 *q4 = reinterpret_cast<const uint4 *>(qc ? qc + (int64_t)img * H + h * HD : base);
 #pragma unroll
         for (int i = 0; i < HD / 8; ++i) {
             const uint4 u = q4[i];

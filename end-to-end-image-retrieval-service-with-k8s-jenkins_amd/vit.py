@@ -303,7 +303,7 @@ def gflop_per_image(cfg: dict = VIT_MSN_BASE, cls_only_last: bool = False) -> fl
 
     ``cls_only_last``: the FLOPs ``rc_embed`` executes when the last layer runs
     attention / O-proj / MLP for the CLS row only (rc_model_set_last_layer):
-    LN1 + QKV stay on all T rows, the rest shrinks to one row (32.93 GFLOP).
+    LN1 + K/V stay on all T rows, Q and the rest shrink to one row (32.70 GFLOP).
     """
     H, F, L = cfg["hidden_size"], cfg["intermediate_size"], cfg["num_hidden_layers"]
     P = cfg["patch_size"]
@@ -313,7 +313,7 @@ def gflop_per_image(cfg: dict = VIT_MSN_BASE, cls_only_last: bool = False) -> fl
     per_layer = T * (3 * H * H + H * H + 2 * H * F) + 2 * T * T * H
     if not cls_only_last:
         return 2.0 * (patch + L * per_layer) / 1e9
-    last = T * 3 * H * H + (H * H + 2 * H * F) + 2 * T * H
+    last = T * 2 * H * H + H * H + (H * H + 2 * H * F) + 2 * T * H
     return 2.0 * (patch + (L - 1) * per_layer + last) / 1e9
 
 
