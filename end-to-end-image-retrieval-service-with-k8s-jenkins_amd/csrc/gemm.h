@@ -72,13 +72,14 @@ __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
 }
 
 // Copy-out of the f32 epilogues (residual add / patch scatter + position): the
-// block's NT threads move ROWS staged f32 rows (1-KB rows of 256 columns, 16-B chunk
-// XOR (row & 63) in `smem`; tile rows r0 .. r0 + ROWS of the output, columns n0 ..
-// n0 + 256), one row per wave per step, in passes of 8 rows: 8 residual / position
-// loads back to back, then the adds, the LN statistics of the 8 rows (branch-free,
-// so their wave reductions interleave) and the stores.  HL: the residual stream is
-// the bf16 pair (a.ln_x, a.res_lo) (vit_kernels.h, "Residual stream as bf16 pairs");
-// otherwise f32 a.out_f32, plus the bf16 copy and statistics when a.ln_x is set.
+// block's NT threads move NT / 64 · ROWS_PER_WAVE staged f32 rows (1-KB rows of 256
+// columns, 16-B chunk XOR (row & 63) in `smem`; output rows r0 .., columns n0 ..
+// n0 + 256), one row per wave per step, in passes of PASS rows: PASS residual /
+// position loads back to back, then the adds, the LN statistics of those rows
+// (branch-free, so their wave reductions interleave) and the stores.  HL: the
+// residual stream is the bf16 pair (a.ln_x, a.res_lo) (vit_kernels.h, "Residual
+// stream as bf16 pairs"); otherwise f32 a.out_f32, plus the bf16 copy and statistics
+// when a.ln_x is set.
 template <int EPI, int NT, int ROWS_PER_WAVE, int PASS = 8>
 __device__ __forceinline__ void resid_copy_out(const GemmArgs &a, const uint8_t *smem, int tid, int r0, int n0) {
     constexpr bool HL = epi_hl(EPI);
