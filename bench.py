@@ -28,6 +28,7 @@ before anything touches the GPU; ``--dry-run`` checks that rank plumbing on CPU
 from __future__ import annotations
 
 import argparse
+import io
 import json
 import os
 import sys
@@ -80,10 +81,7 @@ def torch_vit_forward(sd):
     mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
     std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
 
-    def forward(u8):  # u8 [B,224,224,3]
-        x = u8.permute(0, 3, 1, 2).to(torch.float64) * (1 / 255.0)
-        x = ((x.to(torch.float32) - mean) / std).contiguous()
-        e = F.conv2d(x, sd["embeddings.patch_embeddings.projection.weight"], sd["embeddings.patch_embeddings.projection.bias"], stride=16)
+    def encoder(e):  # patch-conv output [B,768,14,14] -> raw CLS
         e = e.flatten(2).transpose(1, 2)
         B = e.shape[0]
         h = torch.cat([sd["embeddings.cls_token"].expand(B, -1, -1), e], 1) + sd["embeddings.position_embeddings"]
@@ -99,19 +97,41 @@ def torch_vit_forward(sd):
             h = h + F.linear(y, sd[p + "output.dense.weight"], sd[p + "output.dense.bias"])
         return F.layer_norm(h, (768,), sd["layernorm.weight"], sd["layernorm.bias"], 1e-6)[:, 0]
 
+    def forward(u8):  # u8 [B,224,224,3]
+        x = u8.permute(0, 3, 1, 2).to(torch.float64) * (1 / 255.0)
+        x = ((x.to(torch.float32) - mean) / std).contiguous()
+        return encoder(F.conv2d(x, sd["embeddings.patch_embeddings.projection.weight"],
+                                sd["embeddings.patch_embeddings.projection.bias"], stride=16))
+
+    forward.encoder = encoder
     return forward
+
+
+def host_cores() -> dict:
+    """The cores this process may run on (affinity / cgroup cpuset), which is what the CPU
+    baselines use: torch's intra-op pool is set to that count explicitly."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"affinity": aff, "os_cpu_count": os.cpu_count()}
+
+
+def _torch_threads():
+    import torch
+
+    torch.set_num_threads(host_cores()["affinity"])
+    return torch.get_num_threads()
 
 
 def cpu_embed_baseline(budget_s: float = 15.0, batch: int = 16):
     """The reference's CPU path for config 2: ViTImageProcessor's rescale/normalize (224x224
     input: the resize is an identity) and ViTMSNModel's fp32 forward, restated with the same
     torch.nn.functional ops transformers calls (modeling_vit_msn.py: conv patch embed, pre-LN
-    layers, SDPA attention with scale 1/8, exact-erf GELU, final LN), seeded weights, all host
-    threads torch is given, bounded by time."""
+    layers, SDPA attention with scale 1/8, exact-erf GELU, final LN), seeded weights, on every
+    core this process may use (torch threads set to the affinity count), bounded by time."""
     import torch
 
     from oracle.weights import seeded_vit_msn_weights
 
+    threads = _torch_threads()
     sd = {k: torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32)) for k, v in seeded_vit_msn_weights(0).items()}
     forward = torch_vit_forward(sd)
 
@@ -124,24 +144,26 @@ def cpu_embed_baseline(budget_s: float = 15.0, batch: int = 16):
             forward(imgs)
             done += batch
     el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "reference-lib",
-            "cpu": cpu_model_name(),
+    return {"value": done / el, "unit": "images/s", "cores": threads, "kind": "reference-lib",
+            "cpu": cpu_model_name(), "host_cores": host_cores(),
+            "cores_note": "torch intra-op threads = the process's CPU affinity (os.sched_getaffinity): the cores "
+                          "this job may use on the box (its cgroup cpuset), not the machine's total",
             "sample": f"{done} synthetic 224x224 images (batches of {batch}) through rescale/normalize + a torch fp32 "
                       f"ViT-MSN-base forward (torch.nn.functional, the library the reference's transformers path "
                       f"runs on), {el:.1f}s"}
 
 
-def synthetic_jpegs(n: int, seed: int, size: int = 224) -> list[bytes]:
-    """Baseline 4:2:0 q90 JPEGs of smooth random content plus noise (PIL encoder)."""
-    import io
-
+def synthetic_jpegs(n: int, seed: int, size=224) -> list[bytes]:
+    """Baseline 4:2:0 q90 JPEGs of smooth random content plus noise (PIL encoder); size = side
+    or (width, height)."""
     from PIL import Image
 
+    w, h = (size, size) if isinstance(size, int) else size
     rng = np.random.default_rng(seed)
     out = []
     for _ in range(n):
-        base = rng.integers(0, 256, (size // 8 + 1, size // 8 + 1, 3), dtype=np.uint8)
-        arr = np.asarray(Image.fromarray(base).resize((size, size), Image.BILINEAR)).astype(np.int16)
+        base = rng.integers(0, 256, (h // 8 + 1, w // 8 + 1, 3), dtype=np.uint8)
+        arr = np.asarray(Image.fromarray(base).resize((w, h), Image.BILINEAR)).astype(np.int16)
         arr = np.clip(arr + rng.integers(-12, 13, arr.shape), 0, 255).astype(np.uint8)
         b = io.BytesIO()
         Image.fromarray(arr).save(b, format="JPEG", quality=90, subsampling=2)
@@ -151,8 +173,6 @@ def synthetic_jpegs(n: int, seed: int, size: int = 224) -> list[bytes]:
 
 def cpu_jpeg_baseline(datas: list[bytes], budget_s: float = 4.0):
     """The reference decode (embedding/main.py:97: PIL open + convert RGB), one host thread."""
-    import io
-
     from PIL import Image
 
     done, t0 = 0, time.perf_counter()
@@ -213,6 +233,163 @@ def cpu_batch_search_baseline(n_rows=1_000_000, dim=512, nq=256, k=100, index_ro
                       f"= {el:.2f}s each, extrapolated linearly to {index_rows:,} rows"}
 
 
+def _pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(q / 100.0 * (len(xs) - 1))))]
+
+
+def _lat(fn, reps: int, warm: int = 3):
+    """fn() timed reps times after warm calls (host wall clock, each call synchronous): p50/p99 ms."""
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return {"p50_ms": _pct(ts, 50), "p99_ms": _pct(ts, 99), "mean_ms": sum(ts) / len(ts), "reps": reps}
+
+
+def planted_index_rows(n=10_000, dim=768, seed=0, query=None, planted=5):
+    """Config 1's synthetic index: n x dim N(0,1) rows (seed 0) with `planted` near-duplicates of
+    the query (query + small noise) at known rows, so the exact top-5 is known."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    rows = []
+    if query is not None:
+        q = np.asarray(query, np.float32)
+        rows = list(range(17, 17 + 97 * planted, 97))
+        for j, r in enumerate(rows):
+            X[r] = q + (0.02 * (j + 1)) * np.linalg.norm(q) / np.sqrt(dim) * rng.standard_normal(dim).astype(np.float32)
+    return X, rows
+
+
+def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
+    """Batch-1 request latency, the reference's own request shape: /embed of the reference's
+    test image (embedding/main.py:88-124), search top-5 over config 1's 10k x 768 index
+    (retriever/main.py:127-130 times exactly this call) and /search_image end to end through
+    the FastAPI app (TestClient, in process).  CPU reference beside each: PIL decode +
+    ViTImageProcessor arithmetic + a torch fp32 forward at batch 1, numpy exact top-5."""
+    import importlib
+
+    import torch
+
+    emb = importlib.import_module(f"{pkg}.embedding.main")
+    ing = importlib.import_module(f"{pkg}.ingesting.utils")
+    ret = importlib.import_module(f"{pkg}.retriever.utils")
+    retmain = importlib.import_module(f"{pkg}.retriever.main")
+    img_path = os.path.join(REPO, "tests", "golden", "test_image.jpeg")  # the reference's fixture
+    data = open(img_path, "rb").read()
+    out = {}
+    out["embed"] = dict(_lat(lambda: emb.embed_bytes(data), reps), what="embed_bytes (the /embed core): 300x168 "
+                        "baseline JPEG -> GPU decode -> device resize -> ViT-MSN-base -> 768 floats on the host")
+    vec = emb.embed_bytes(data)
+    X, planted = planted_index_rows(query=vec)
+    ix = ing.get_index("bench-latency-10k", dimension=768, dtype="float32", capacity=len(X))
+    ix.upsert_tensor([f"r{i}" for i in range(len(X))], torch.from_numpy(X).to(torch.cuda.current_device()),
+                     [{"gcs_path": f"images/r{i}.jpg"} for i in range(len(X))])
+    got = ret.search(ix, vec, top_k=5)
+    out["search_top5"] = dict(_lat(lambda: ret.search(ix, vec, top_k=5), reps * 5),
+                              what="retriever.utils.search(index, emb, top_k=5) over 10,000 x 768 f32 rows "
+                                   "(index.query with include_values=True, as the reference calls it)",
+                              planted_found=sorted(got) == sorted(f"r{r}" for r in planted))
+    from fastapi.testclient import TestClient
+
+    client = TestClient(retmain.app)
+    old_index = retmain.index
+    retmain.index = lambda: ix
+    try:
+        def post():
+            r = client.post("/search_image", files={"file": ("test_image.jpeg", data, "image/jpeg")})
+            assert r.status_code == 200 and len(r.json()) == 5
+        out["search_image"] = dict(_lat(post, reps), what="POST /search_image through the FastAPI app (TestClient): "
+                                   "validation decode, GPU embed, exact top-5, fetch, 5 URLs")
+    finally:
+        retmain.index = old_index
+    if cpu:
+        from PIL import Image
+
+        from oracle.cosine_topk import cosine_topk_f32
+        from oracle.preprocess import preprocess
+        from oracle.weights import seeded_vit_msn_weights
+
+        threads = _torch_threads()
+        sd = {k: torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32)) for k, v in seeded_vit_msn_weights(0).items()}
+        fwd = torch_vit_forward_pixels(sd)
+
+        def cpu_embed():
+            im = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+            with torch.inference_mode():
+                return fwd(torch.from_numpy(preprocess(im)[None]))
+
+        out["embed"]["cpu_baseline"] = dict(_lat(cpu_embed, 10, warm=2), cores=threads, kind="reference-lib",
+                                            what="PIL decode + ViTImageProcessor arithmetic (resize, rescale, "
+                                                 "normalize) + torch fp32 ViT-MSN-base forward, batch 1")
+        Xn = X / np.linalg.norm(X, axis=1, keepdims=True)
+        q = np.asarray(vec, np.float32)
+        out["search_top5"]["cpu_baseline"] = dict(_lat(lambda: cosine_topk_f32(Xn, q, 5), reps * 5), kind="port",
+                                                  what="numpy exact cosine top-5 over the same 10k x 768 rows")
+    ix.close()
+    return out
+
+
+def torch_vit_forward_pixels(sd):
+    """pixel_values [B,3,224,224] f32 -> raw CLS: torch_vit_forward without the u8 rescale."""
+    import torch.nn.functional as F
+
+    fwd_u8 = torch_vit_forward(sd)
+
+    def forward(x):
+        e = F.conv2d(x, sd["embeddings.patch_embeddings.projection.weight"], sd["embeddings.patch_embeddings.projection.bias"], stride=16)
+        return fwd_u8.encoder(e)
+
+    return forward
+
+
+def jpeg_300x168_line(model, B: int, world: int, rank: int, barrier, max_over_ranks, reps: int = 8, cpu: bool = True):
+    """Batches of the reference fixture's shape (300 x 168 baseline JPEGs, tests/test_embedding.py:17;
+    resize at embedding/main.py:107) through the bulk path: host Huffman of batch i+1 under GPU
+    IDCT / colour / resize / embed of batch i.  CPU beside: Pillow decode + the processor's
+    resize/rescale/normalize + torch fp32 forward, bounded."""
+    import torch
+
+    datas = synthetic_jpegs(B, 7100 + rank, size=(168, 300))  # W x H of tests/data/test_image.jpeg
+    for _ in model.embed_jpeg_stream([datas] * 2):
+        pass
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in model.embed_jpeg_stream([datas] * reps):
+        pass
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    out = {"workload": f"{B} synthetic 168x300 (WxH, the reference fixture's shape) q90 4:2:0 baseline JPEGs per "
+                       f"batch per GPU, {reps} batches: GPU JPEG "
+                       f"decode (bit-exact with PIL) -> Pillow-exact bicubic resize to 224 -> ViT-MSN-base",
+           "value": world * B * reps / el, "unit": "images/s (JPEG bytes -> embedding)"}
+    if cpu:
+        from PIL import Image
+
+        from oracle.preprocess import preprocess
+        from oracle.weights import seeded_vit_msn_weights
+
+        threads = _torch_threads()
+        sd = {k: torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32)) for k, v in seeded_vit_msn_weights(0).items()}
+        fwd = torch_vit_forward_pixels(sd)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 10.0 or done == 0:
+            batch = [np.asarray(Image.open(io.BytesIO(datas[(done + j) % len(datas)])).convert("RGB")) for j in range(16)]
+            with torch.inference_mode():
+                fwd(torch.from_numpy(np.stack([preprocess(im) for im in batch])))
+            done += 16
+        cel = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": done / cel, "unit": "images/s", "cores": threads, "kind": "reference-lib",
+                               "sample": f"{done} of the same JPEGs: PIL decode + ViTImageProcessor arithmetic (numpy "
+                                         f"restatement, bit-exact) + torch fp32 forward in batches of 16, {cel:.1f}s"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -229,7 +406,9 @@ def main():
                     help="run the last encoder layer on every row (default: CLS rows only, rc_model_set_last_layer)")
     ap.add_argument("--no-ln-fold", action="store_true",
                     help="run the standalone LayerNorm kernel instead of folding LN into QKV / fc1 (A/B)")
-    ap.add_argument("--ingest-images", type=int, default=16384, help="config 5 sample per GPU (0 = skip)")
+    ap.add_argument("--ingest-images", type=int, default=1_250_000,
+                    help="config 5: images embedded + upserted per GPU (10M / 8 GPUs; 0 = skip)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency lines")
     ap.add_argument("--jpeg-images", type=int, default=256, help="JPEG decode sample per GPU (0 = skip)")
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -304,8 +483,6 @@ def main():
     for _ in range(args.warmup):
         model.embed(images, out=(raw, nrm))
     torch.cuda.synchronize()
-    model.timing(["fc1"])
-    model.timing_reset()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -314,27 +491,40 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = max_over_ranks(time.perf_counter() - t0)
-    fc1c_ms, fc1c_n, _ = model.timing_read("fc1")
-    model.timing(False)
     assert torch.isfinite(raw).all()
     imgs_per_s = world * B * args.steps / el
-    # Roofline of the dominant kernel: the timed steps above run the batch as
-    # --parts concurrent slices, so an fc1 launch there shares the GPU; its own
-    # efficiency is timed on the unsplit batch (the GEMM alone on the chip).
+    # Roofline of the projection GEMMs: the timed steps above run the batch as --parts
+    # concurrent slices, so a GEMM launch there shares the GPU; each GEMM's own efficiency is
+    # timed on the unsplit batch (the GEMM alone on the chip), with HIP events on the launch
+    # stream around every full-batch launch of that projection.  `roofline` prices the one that
+    # takes the most time per step; `gemms` lists all four.
+    M = B * 197
+    shapes = {"qkv": (M, 2304, 768, "gemm_pp_kernel<4,0,12> (QKV, LayerNorm 1 folded in)"),
+              "oproj": (M, 768, 768, "gemm_pp_kernel<6,0,12> (O-proj + residual + LN-2 statistics)"),
+              "fc1": (M, 3072, 768, "gemm_pp_kernel<5,0,12> (fc1 + GELU, LayerNorm 2 folded in)"),
+              "fc2": (M, 768, 3072, "gemm_pp_kernel<6,0,48> (fc2 + residual + LN-1 statistics)")}
     model.set_parts(1)
     model.embed(images, out=(raw, nrm))
     torch.cuda.synchronize()
-    model.timing(["fc1"])
+    model.timing(list(shapes) + ["attention"])
     model.timing_reset()
     for _ in range(args.roofline_steps):
         model.embed(images, out=(raw, nrm))
     torch.cuda.synchronize()
-    fc1_ms, fc1_n, fc1_flops = model.timing_read("fc1")
+    gemms = {}
+    for role, (gm, gn, gk, kname) in shapes.items():
+        ms, n, fl = model.timing_read(role)
+        avg = ms / max(n, 1)
+        tf = (fl / max(n, 1)) / (avg / 1e3) / 1e12 if avg > 0 else 0.0
+        gemms[role] = {"kernel": f"{kname}: M={gm} N={gn} K={gk}", "avg_launch_ms": avg, "launches": n,
+                       "flops_per_launch": fl / max(n, 1), "achieved_tflops": tf, "frac": tf / PEAK_BF16_TFLOPS,
+                       "ms_per_step": ms / args.roofline_steps, "traffic": load_profile_traffic(role)}
+    att_ms, att_n, _ = model.timing_read("attention")
     model.timing(False)
     model.set_parts(args.parts)
-    fc1_avg_ms = fc1_ms / max(fc1_n, 1)
-    fc1_flops_launch = fc1_flops / max(fc1_n, 1)
-    achieved = fc1_flops_launch / (fc1_avg_ms / 1e3) / 1e12
+    dominant = max(gemms, key=lambda r: gemms[r]["ms_per_step"])
+    dom = gemms[dominant]
+    gemm_step_ms = sum(g["ms_per_step"] for g in gemms.values())
     # FLOPs rc_embed executes per image (the CLS-only last layer skips the rows
     # /embed never returns); the full-model figure is reported beside it
     gflop = vit.gflop_per_image(cls_only_last=not args.full_last_layer)
@@ -353,20 +543,26 @@ def main():
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        tlog = t0
         for b0 in range(0, n_img, B):
             batch = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g5)
             model.embed(batch, out=(raw, nrm))
             sidx5.upsert_local(nrm, local_rows + b0)  # each rank fills its own shard: no collective
+            if rank == 0 and time.perf_counter() - tlog > 15:
+                tlog = time.perf_counter()
+                log(f"bench: config 5 ingest {b0 + B:,}/{n_img:,} images ({(b0 + B) / (tlog - t0):,.0f}/s)")
         torch.cuda.synchronize()
         barrier()
         el5 = max_over_ranks(time.perf_counter() - t0)
-        sidx5.set_rows(world * n_img)  # local row j of rank r is global row j * world + r
+        n_rows5 = sidx5.publish_rows()  # local row j of rank r is global row j * world + r
         # retrieve: queries = rank 0's first ingested images, regenerated and embedded on every rank
+        nq5 = args.batch_queries
         gq5 = torch.Generator(device=dev).manual_seed(6000)
-        qimgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=gq5)
-        model.embed(qimgs, out=(raw, nrm))
-        nq5 = min(args.batch_queries, B)
-        q5 = nrm[:nq5].clone()
+        q5 = torch.empty((nq5, 768), dtype=torch.float32, device=dev)
+        for q0 in range(0, nq5, B):
+            qimgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=gq5)
+            model.embed(qimgs, out=(raw, nrm))
+            q5[q0:q0 + B] = nrm[:min(B, nq5 - q0)]
         sidx5.search(q5, 100, mode="mfma")
         torch.cuda.synchronize()
         barrier()
@@ -377,13 +573,14 @@ def main():
         el5q = max_over_ranks(time.perf_counter() - t0)
         recall1 = float((r5[:, 0].cpu() == torch.arange(nq5) * world).float().mean())  # rank 0's rows j*world
         ingest = {
-            "workload": f"BASELINE config 5 (bounded sample): {n_img:,} synthetic 224x224 images per GPU generated on "
-                        f"device, embedded (ViT-MSN-base) and upserted into a row-sharded 768-d fp16 index, then "
-                        f"{nq5} queries top-100",
-            "value": world * n_img / el5, "unit": "images/s (embed + upsert)",
-            "extrapolated_10M_images_s": 1e7 / (world * n_img / el5),
+            "workload": f"BASELINE config 5 at its per-GPU size: {n_img:,} synthetic 224x224 images per GPU "
+                        f"({world * n_img:,} in all) generated on device, embedded (ViT-MSN-base, batches of {B}) "
+                        f"and upserted rank-locally into a row-sharded 768-d fp16 index, then {nq5} queries top-100 "
+                        f"(batched MFMA search + RCCL all-gather merge)",
+            "value": world * n_img / el5, "unit": "images/s (embed + upsert)", "seconds": el5,
+            "index_rows": n_rows5,
             "retrieve": {"value": nq5 / el5q, "unit": "queries/s", "ms_per_batch": el5q * 1e3,
-                         "index_rows": world * n_img, "top1_self_recall": recall1},
+                         "queries": nq5, "k": 100, "index_rows": n_rows5, "top1_self_recall": recall1},
         }
         sidx5.close()
         del sidx5
@@ -498,6 +695,13 @@ def main():
         }
         ix.close()
 
+    if jpeg is not None:
+        jpeg["fixture_shape"] = jpeg_300x168_line(model, B, world, rank, barrier, max_over_ranks,
+                                                  cpu=rank == 0 and world == 1 and not args.no_cpu)
+    latency = None
+    if not args.no_latency:
+        latency = latency_lines(PKG, cpu=rank == 0 and world == 1 and not args.no_cpu)
+
     model.close()
     del images, raw, nrm
     torch.cuda.empty_cache()
@@ -522,20 +726,22 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": {
-            "kernel": ("gemm_pp_kernel<EPI_GELU_BF16> (fc1: M=%d N=3072 K=768)" if args.no_ln_fold else
-                       "gemm_pp_kernel<EPI_GELU_BF16_LN> (fc1 with LayerNorm 2 folded in: M=%d N=3072 K=768)") % (B * 197),
+            "kernel": dom["kernel"] + " — the projection GEMM with the most time per step",
             "bound": "mfma",
-            "achieved": achieved,
+            "achieved": dom["achieved_tflops"],
             "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": achieved / PEAK_BF16_TFLOPS,
-            "traffic": load_profile_traffic("fc1"),
-            "avg_launch_ms": fc1_avg_ms,
-            "launches": fc1_n,
-            "flops_per_launch": fc1_flops_launch,
-            "measured_on": "unsplit batch (parts=1), the GEMM alone on the GPU",
-            "concurrent_avg_launch_ms": fc1c_ms / max(fc1c_n, 1),
+            "frac": dom["achieved_tflops"] / PEAK_BF16_TFLOPS,
+            "traffic": dom["traffic"],
+            "avg_launch_ms": dom["avg_launch_ms"],
+            "launches": dom["launches"],
+            "flops_per_launch": dom["flops_per_launch"],
+            "measured_on": "unsplit batch (parts=1), HIP events on the launch stream around each full-batch launch",
         },
+        "gemms": gemms,
+        "gemm_ms_per_step": gemm_step_ms,
+        "attention_ms_per_step": att_ms / args.roofline_steps,
+        "attention_avg_launch_ms": att_ms / max(att_n, 1),
         "embed_parts": args.parts,
         "layernorm": "standalone kernel" if args.no_ln_fold else
         "folded into QKV / fc1 epilogues (producers emit bf16(x) + per-tile mean/M2)",
@@ -550,6 +756,8 @@ def main():
         result["ingest"] = ingest
     if jpeg is not None:
         result["jpeg"] = jpeg
+    if latency is not None:
+        result["latency"] = latency
 
     # ------------------------------------------------- search (secondary) --
     if not args.no_search:

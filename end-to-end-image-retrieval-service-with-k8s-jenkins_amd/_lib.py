@@ -86,6 +86,7 @@ _pf = C.POINTER(C.c_float)
 SIGNATURES = {
     "rc_last_error": (C.c_char_p, []),
     "rc_abi_version": (C.c_int, []),
+    "rc_alloc_count": (C.c_int64, []),
     "rc_index_create": (C.c_int, [_i32, _i32, _i32, _i64, _i64, C.POINTER(_vp)]),
     "rc_index_destroy": (C.c_int, [_vp]),
     "rc_index_info": (C.c_int, [_vp, _pi32, _pi32, _pi64, _pi64]),

@@ -42,11 +42,30 @@ def _headers():
     return hs
 
 
+def _deps(src: str) -> list[str]:
+    """src plus every in-tree header it includes, transitively (#include "...")."""
+    import re
+
+    seen, todo = [], [src]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.append(f)
+        for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', open(f).read(), flags=re.M):
+            for d in (os.path.dirname(f), CSRC, os.path.join(REPO, "include")):
+                cand = os.path.join(d, inc)
+                if os.path.exists(cand):
+                    todo.append(cand)
+                    break
+    return seen
+
+
 def _compile(src: str, extra: list[str]) -> str:
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
     stamp = obj + ".flags"
     flags = " ".join(CFLAGS + extra)
-    newest_dep = max(os.path.getmtime(p) for p in [src, __file__] + _headers())
+    newest_dep = max(os.path.getmtime(p) for p in [__file__] + _deps(src))
     same_flags = os.path.exists(stamp) and open(stamp).read() == flags
     if same_flags and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj

@@ -30,6 +30,9 @@ class Config:
     INDEX_DEVICES = os.getenv("RC_INDEX_DEVICES", "")
     INDEX_SHARDS = int(os.getenv("RC_INDEX_SHARDS", "1"))
     EMBED_MAX_BATCH = int(os.getenv("RC_EMBED_MAX_BATCH", "32"))
+    # embedding GPUs (data parallel, one model per entry; entries may repeat): "" = the
+    # distinct GPUs of the index shards (RC_INDEX_DEVICES), "all", or a comma list
+    EMBED_DEVICES = os.getenv("RC_EMBED_DEVICES", "")
     MODEL_PATH = os.getenv("RC_MODEL_PATH", "")  # local checkpoint dir (config.json + weights)
     WEIGHT_SEED = int(os.getenv("RC_WEIGHT_SEED", "1907"))
     GPU_JPEG = os.getenv("RC_GPU_JPEG", "1") != "0"  # decode baseline JPEGs on the GPU (bit-exact with PIL)

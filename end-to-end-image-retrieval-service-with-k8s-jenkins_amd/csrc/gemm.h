@@ -163,7 +163,10 @@ __device__ __forceinline__ void resid_copy_out(const GemmArgs &a, const uint8_t 
 // ABL (diagnostic builds only): bit0 = no DMA in the K loop, bit1 = no MFMA,
 // bit2 = no epilogue (accumulators kept live), bit3 = no global stores in the
 // bf16 epilogue (LDS staging kept), bit4 = no GELU.  ABL = 0 is the product kernel.
-template <int EPI, int ABL = 0>
+// NKT: K / 64 fixed at compile time for the model's shapes (12: QKV / O-proj / fc1,
+// 48: fc2), 0 = from a.K.  It also names the launch: O-proj (EPI 6, NKT 12) and fc2
+// (EPI 6, NKT 48) share an epilogue but are separate rows in a kernel trace.
+template <int EPI, int ABL = 0, int NKT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     constexpr int BM = 256, BN = 256, BK = 64;
     constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;  // A tile then W tile, 32 KB each
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                 biasr[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
     }
 
-    const int nk = K / BK;
+    const int nk = NKT > 0 ? NKT : K / BK;
     auto kofs = [](int kt) { return kt * BK; };
     stage4(0, kofs(0), 0);
     stage4(0, kofs(0), 4);
@@ -249,6 +252,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     if (grp == 1) bar();  // stagger: G1 one segment behind
 
     bf16x8 af[4][2], wf[2][2];  // [mi][s], [ni][s]
+#pragma nounroll
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         const uint8_t *As = smem + cur * STAGE;
@@ -950,18 +954,17 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
     ln_emit_row(v, ln_x + off, srow, lane, true);
 }
 
-// Kernel choice: 1 = 128x128 4-wave kernel (gemm_bf16_kernel, any N % 128 == 0),
-// 4 = ping-pong 256x256, 8 = two-workgroup 128x256, 9 = skinny (M <= 256), 0 = auto.
-// Auto follows interleaved A/B timings on the batch-256 shapes (tools/gemm_calib.py):
-// ping-pong everywhere except the short square projections.  (Round 1 also measured
-// a 256x256 / 128x256 single-barrier kernel, a persistent kernel, Stream-K and a
-// deferred-store persistent kernel: each lost on every shape and was removed.)
-enum GemmVariant { GEMM_AUTO = 0, GEMM_V1 = 1, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9 };
+// Kernel choice: 4 = ping-pong 256x256, 8 = two-workgroup 128x256, 9 = skinny
+// (M <= 256), 0 = auto.  Auto follows interleaved A/B timings on the batch-256 shapes
+// (tools/gemm_calib.py): ping-pong everywhere except the short square projections.
+// (Rounds 1-2 also measured a 128x128 4-wave kernel, a 256x256 / 128x256 single-
+// barrier kernel, a persistent kernel, Stream-K and a deferred-store persistent
+// kernel: each lost on every shape and was removed.)
+enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9 };
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
-    if (a.N % 256 != 0) return GEMM_V1;
     // Short square projections (O-proj, patch embed: N = K = 768) finish in
     // ~2.3 rounds of 256x256 tiles and carry a heavy f32 epilogue (residual /
     // position read + write): the two-workgroup kernel overlaps that epilogue
@@ -1002,25 +1005,16 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
     const int pick = gemm_pick(a, variant, epi_patch(EPI), epi_hl(EPI));
-    RC_REQUIRE(a.ldc == 0 || (a.ldc >= a.N && pick != GEMM_V1 && epi_bf16_out(EPI)), RC_ERR_UNSUPPORTED,
-               "an output row stride (ldc) needs a bf16 epilogue on the ping-pong / two-workgroup / skinny kernels");
+    RC_REQUIRE(a.ldc == 0 || (a.ldc >= a.N && epi_bf16_out(EPI)), RC_ERR_UNSUPPORTED,
+               "an output row stride (ldc) needs a bf16 epilogue");
     if constexpr (epi_hl(EPI)) {
-        RC_REQUIRE(a.ln_x && a.res_lo && pick != GEMM_V1, RC_ERR_UNSUPPORTED,
-                   "bf16-pair residual epilogues: ln_x + res_lo, ping-pong / two-workgroup / skinny kernels");
+        RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
         RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_SKINNY) && a.ln_c && a.ln_stats, RC_ERR_UNSUPPORTED,
                    "LayerNorm-fold consumers run on the ping-pong or skinny kernel");
     }
     switch (pick) {
-        case GEMM_V1: {
-            if constexpr (!epi_ln(EPI) && !epi_hl(EPI)) {
-                RC_REQUIRE(a.N % GEMM_BN == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 128");
-                const int ntm = (a.M + GEMM_BM - 1) / GEMM_BM, ntn = a.N / GEMM_BN;
-                hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(ntm * ntn), dim3(256), 0, s, a);
-            }
-            break;
-        }
         case GEMM_W2: {
             if constexpr (!epi_ln(EPI)) {
                 RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
@@ -1047,7 +1041,10 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             a.group_m = gemm_group_m(a);
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
-            hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(ntm * ntn), dim3(512), 0, s, a);
+            const dim3 gr(ntm * ntn), bl(512);
+            if (a.K == 768) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 12>), gr, bl, 0, s, a);
+            else if (a.K == 3072) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 48>), gr, bl, 0, s, a);
+            else hipLaunchKernelGGL((gemm_pp_kernel<EPI>), gr, bl, 0, s, a);
             break;
         }
 #if defined(RC_GEMM_ABLATION)

@@ -28,17 +28,18 @@ void set_last_error(const std::string &m) { g_last_error = m; }
 template <typename T>
 __global__ __launch_bounds__(256) void upsert_kernel(T *__restrict__ rows, float *__restrict__ norms, int64_t ld, int dim,
                                                     const float *__restrict__ vecs, const int64_t *__restrict__ src_idx,
-                                                    const int64_t *__restrict__ slot, int64_t n) {
+                                                    const int64_t *__restrict__ slot, int64_t n, int64_t cap) {
     const int lane = threadIdx.x & 63;
     const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (v >= n) return;
+    const int64_t r = slot[v];
+    if (r < 0 || r >= cap) return;  // device-side guard: never write outside the row slots (hosts validate first)
     const float *src = vecs + (src_idx ? src_idx[v] : v) * dim;
     float ss = 0.f;
     for (int c = lane; c < dim; c += 64) ss = fmaf(src[c], src[c], ss);
     ss = wave_sum(ss);
     const float nrm = sqrtf(ss);
     const float inv = nrm > 0.f ? 1.0f / nrm : 0.f;
-    const int64_t r = slot[v];
     T *dst = rows + r * ld;
     for (int c = lane; c < ld; c += 64) dst[c] = Elem<T>::cast(c < dim ? src[c] * inv : 0.f);
     if (lane == 0) norms[r] = nrm;
@@ -47,11 +48,15 @@ __global__ __launch_bounds__(256) void upsert_kernel(T *__restrict__ rows, float
 template <typename T>
 __global__ __launch_bounds__(256) void fetch_kernel(const T *__restrict__ rows, const float *__restrict__ norms, int64_t ld,
                                                    int dim, const int64_t *__restrict__ slot, int64_t n,
-                                                   float *__restrict__ out) {
+                                                   float *__restrict__ out, int64_t cap) {
     const int lane = threadIdx.x & 63;
     const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (v >= n) return;
     const int64_t r = slot[v];
+    if (r < 0 || r >= cap) {  // out of range: NaN values, never a read outside the rows
+        for (int c = lane; c < dim; c += 64) out[v * dim + c] = __builtin_nanf("");
+        return;
+    }
     const float nrm = norms ? norms[r] : 1.0f;
     for (int c = lane; c < dim; c += 64) out[v * dim + c] = Elem<T>::load(rows, r * ld + c) * nrm;
 }
@@ -247,6 +252,12 @@ constexpr int kMaxBlocks = 2048;
 constexpr int kBatchMinQueries = 8;      // below this the HBM-bound scan wins (1-4 queries per pass)
 constexpr int64_t kBatchMinRows = 65536;  // tiny shards: the staged path's fixed cost dominates
 
+// Every global row a shard can report must fit the 32-bit row word of the top-k
+// keys (merge_lists_kernel) below the all-ones value: row_base + (cap - 1) * stride < 2^32 - 1.
+bool row_map_fits(int64_t row_base, int64_t row_stride, int64_t cap) {
+    return (double)row_base + (double)(cap - 1) * (double)row_stride < 4294967295.0;
+}
+
 int pick_nch(int dim) {
     const int need = (dim + 127) / 128;
     for (int n : kNchSet)
@@ -271,7 +282,7 @@ template <typename T>
 void launch_upsert(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *slots, hipStream_t s) {
     const unsigned grid = (unsigned)((n + 3) / 4);
     hipLaunchKernelGGL(upsert_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, vecs, src_idx,
-                       slots, n);
+                       slots, n, h->capacity);
     RC_LAUNCH_CHECK();
 }
 
@@ -279,7 +290,7 @@ template <typename T>
 void launch_fetch(rc_index *h, const int64_t *slots, int64_t n, float *out, bool stored, hipStream_t s) {
     const unsigned grid = (unsigned)((n + 3) / 4);
     hipLaunchKernelGGL(fetch_kernel<T>, dim3(grid), dim3(256), 0, s, (const T *)h->rows, stored ? nullptr : h->norms, h->ld,
-                       h->dim, slots, n, out);
+                       h->dim, slots, n, out, h->capacity);
     RC_LAUNCH_CHECK();
 }
 
@@ -364,7 +375,7 @@ void batched_search_exact(rc_index *h, const float *queries, int nq, int64_t n_r
     BatchPlan p{h->rows, h->dtype, h->dim, h->nch, h->ld, n_rows, h->row_base, h->row_stride, queries, nq, k, scores, out_rows};
     if (h->gtimer.enabled) h->gtimer.create();
     batched_search(p, h->bws, s, h->gtimer.enabled ? &h->gtimer : nullptr);
-    int nblk = (int)std::min<int64_t>(FB_BLOCKS, std::max<int64_t>(1, (n_rows + 511) / 512));
+    int nblk = (int)std::min<int64_t>(h->bws.fb_blocks, std::max<int64_t>(1, (n_rows + 511) / 512));
     int64_t rpb = (n_rows + nblk - 1) / nblk;
     rpb = std::max<int64_t>(32, (rpb + 31) / 32 * 32);
     nblk = (int)std::max<int64_t>(1, (n_rows + rpb - 1) / rpb);
@@ -402,6 +413,7 @@ extern "C" {
 
 const char *rc_last_error(void) { return g_last_error.c_str(); }
 int rc_abi_version(void) { return RC_ABI_VERSION; }
+int64_t rc_alloc_count(void) { return g_alloc_count.load(std::memory_order_relaxed); }
 
 int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t row_base, rc_index **out) {
     return guard([&] {
@@ -409,6 +421,8 @@ int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t ro
         RC_REQUIRE(dim > 0, RC_ERR_INVALID, "dimension must be positive");
         RC_REQUIRE(dtype == RC_F32 || dtype == RC_F16 || dtype == RC_BF16, RC_ERR_INVALID, "dtype must be RC_F32/RC_F16/RC_BF16");
         RC_REQUIRE(capacity > 0 && capacity < (int64_t(1) << 32), RC_ERR_INVALID, "capacity must be in [1, 2^32)");
+        RC_REQUIRE(row_base >= 0 && row_map_fits(row_base, 1, capacity), RC_ERR_INVALID,
+                   "row_base + capacity must stay below 2^32 - 1 (global rows key the top-k merge)");
         const int nch = pick_nch(dim);
         RC_REQUIRE(nch > 0, RC_ERR_UNSUPPORTED, "dimension > 2048 is not supported");
         DeviceScope ds(device);
@@ -478,6 +492,8 @@ int rc_index_set_row_map(rc_index *h, int64_t row_base, int64_t row_stride) {
         RC_REQUIRE(h, RC_ERR_INVALID, "null index");
         RC_REQUIRE(row_base >= 0 && row_stride >= 1, RC_ERR_INVALID, "row_base must be >= 0 and row_stride >= 1");
         std::lock_guard<std::mutex> lk(h->mu);
+        RC_REQUIRE(row_map_fits(row_base, row_stride, h->capacity), RC_ERR_INVALID,
+                   "row map exceeds 2^32 - 1 global rows (row_base + (capacity - 1) * row_stride)");
         h->row_base = row_base;
         h->row_stride = row_stride;
     });
@@ -489,6 +505,8 @@ int rc_index_grow(rc_index *h, int64_t new_capacity, void *stream) {
         RC_REQUIRE(new_capacity < (int64_t(1) << 32), RC_ERR_INVALID, "capacity must be < 2^32");
         std::lock_guard<std::mutex> lk(h->mu);
         if (new_capacity <= h->capacity) return;
+        RC_REQUIRE(row_map_fits(h->row_base, h->row_stride, new_capacity), RC_ERR_INVALID,
+                   "grown capacity exceeds 2^32 - 1 global rows under this shard's row map");
         DeviceScope ds(h->device);
         hipStream_t s = (hipStream_t)stream;
         const size_t rb = (size_t)h->ld * dtype_size(h->dtype);

@@ -97,7 +97,9 @@ void launch_scan_bf16(const ScanArgs &a);
 // ------------------------------------------- batched MFMA search (search_mfma.hip)
 constexpr int BATCH_CAND_CAP = 4096;  // candidate slots per query per stage
 constexpr int INDEX_ROW_PAD = 256;    // row storage is allocated in whole 256-row tiles
-constexpr int FB_BLOCKS = 256;        // blocks of the on-device exact fallback scan (overflowed queries)
+constexpr int FB_BLOCKS = 256;        // blocks of the on-device exact fallback scan (overflowed queries), at most
+constexpr int FB_MIN_BLOCKS = 32;     // ... and at least, whatever the memory budget below says
+constexpr int64_t FB_BUDGET_BYTES = int64_t(256) << 20;  // cap on its partial-key buffer per index
 constexpr int FB_QSTRIDE = 64;        // its grid.y: block (b, y) scans queries y, y + 64, ... that overflowed
 
 struct BatchWs {
@@ -113,7 +115,8 @@ struct BatchWs {
     uint64_t *keys = nullptr;   // [nq_cap][k_cap] running top-k keys (sorted)
     int *flags = nullptr;       // [nq_cap] 1 = candidate overflow, exact fallback needed
     int *ovf = nullptr;         // overflowed queries since the last timing read (device counter)
-    uint64_t *fb_partial = nullptr;  // [FB_BLOCKS][nq_cap][k_cap] partial keys of the exact fallback scan
+    int fb_blocks = 0;               // blocks of the fallback scan: FB_BUDGET_BYTES / (nq_cap * k_cap * 8), clamped
+    uint64_t *fb_partial = nullptr;  // [fb_blocks][nq_cap][k_cap] partial keys of the exact fallback scan
     void ensure(int nq, int k, int64_t ld, int dtype_bytes);
     void release();
 };

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -65,9 +66,14 @@ struct DeviceScope {
     }
 };
 
+// Device + pinned-host allocations made by the library (rc_alloc_count: tests check
+// that steady-state hot calls allocate nothing).
+inline std::atomic<int64_t> g_alloc_count{0};
+
 inline void *dmalloc(size_t bytes) {
     void *p = nullptr;
     if (bytes == 0) return nullptr;
+    g_alloc_count.fetch_add(1, std::memory_order_relaxed);
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -78,6 +84,23 @@ inline void *dmalloc(size_t bytes) {
 
 inline void dfree(void *p) {
     if (p) (void)hipFree(p);
+}
+
+// Pinned host memory (async H2D / D2H staging).
+inline void *hmalloc(size_t bytes) {
+    void *p = nullptr;
+    if (bytes == 0) return nullptr;
+    g_alloc_count.fetch_add(1, std::memory_order_relaxed);
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        throw Error(RC_ERR_OOM, "hipHostMalloc(" + std::to_string(bytes) + " B) failed: " + hipGetErrorString(e));
+    }
+    return p;
+}
+
+inline void hfree(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 // Host f32 → bf16 bits, round to nearest even (NaN kept NaN).

@@ -44,31 +44,11 @@ template <> struct MfmaOp<f16_t> {
     static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
     }
-    // A in VGPRs, B in AGPRs, C/D in VGPRs (filter_qs_kernel at QT = 4, whose query
-    // fragments fill the AGPR file).  The builtin would copy an AGPR-resident B to
-    // VGPRs first; inline asm is invisible to the hazard recognizer, so the caller
-    // waits out the XDL-write -> VALU-read latency before touching C.
-    static __device__ __forceinline__ void mma_vav(v8 a, v8 b, f32x4_t &c) {
-        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
-    }
-    static __device__ __forceinline__ void mma_vav0(v8 a, v8 b, f32x4_t &c) {
-        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
-    }
 };
 template <> struct MfmaOp<bf16_t> {
     typedef __bf16 v8 __attribute__((ext_vector_type(8)));
     static __device__ __forceinline__ f32x4_t mma(v8 a, v8 b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-    }
-    // A in VGPRs, B in AGPRs, C/D in VGPRs (filter_qs_kernel at QT = 4, whose query
-    // fragments fill the AGPR file).  The builtin would copy an AGPR-resident B to
-    // VGPRs first; inline asm is invisible to the hazard recognizer, so the caller
-    // waits out the XDL-write -> VALU-read latency before touching C.
-    static __device__ __forceinline__ void mma_vav(v8 a, v8 b, f32x4_t &c) {
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
-    }
-    static __device__ __forceinline__ void mma_vav0(v8 a, v8 b, f32x4_t &c) {
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
     }
 };
 
@@ -311,30 +291,20 @@ __global__ __launch_bounds__(512, 1) void filter_gemm_kernel(FilterArgs a) {
 // MFMA roles as above (A = index rows, B = queries): lane (li, g) of acc[rf][qt]
 // holds rows 16·rf + 4g + j of query 16·qt + li.  Same thresholds, candidate
 // appends and exactness argument as filter_gemm_kernel.
-// QT (queries per wave / 16) sets the LDS read rate: every row fragment read
-// feeds QT MFMAs.  QT = 2 (8 waves, 2 per SIMD) reads one ds_read_b128 per two
-// 16x16x32 MFMAs from each of 8 waves — 256 B/clk/CU, the LDS array's limit, which
-// held the round-1 kernel at mfma_busy 0.64; QT = 4 (4 waves, one per SIMD, the
-// 2·NKT query fragments of 64 queries in 256 VGPRs) halves that.
-// Row-tile height: 8 row fragments at QT = 2, 4 at QT = 4 (acc = 16·RF·QT f32 per
-// lane stays 64-128 registers next to the 64·QT·NKT/... query fragments).
-constexpr int qs_rows(int qt) { return qt == 4 ? 64 : 128; }
-// LDS ring depth in K-steps: QS_NS - 2 steps in flight (96-112 KB) cover the HBM
-// latency of a tile's first touch at either QT.
-constexpr int qs_stages(int qt) { return qt == 4 ? 16 : 8; }
+// Each wave holds 32 queries (2 x 16, QS_QT) for 128-row tiles: 8 waves, 2 per SIMD,
+// every row-fragment read feeds two MFMAs and the SIMD partner wave's MFMAs cover
+// its latency.  (A 4-wave form with 64 queries per wave pinned in AGPRs and
+// inline-asm MFMAs was measured against it in round 2 — within 1 %, behind after
+// the 2-GB sub-launches — and removed.)
+constexpr int QS_QT = 2, QS_RT = 128, QS_NS = 8;  // queries/16 per wave, rows per tile, LDS ring steps
 
 // ABL (A/B diagnostics, diagnostic builds only; 0 in production): bit0 no DMA in the
 // loop, bit1 no MFMA, bit2 no fragment reads (MFMAs on the query registers), bit3 no
 // epilogue.
-// (QS_WAVES is derived inside: a dependent default template argument on a __global__
-// template makes hipcc mangle the host stub differently from its launch sites.)
-template <typename T, int NKT, int QS_QT, int ABL = 0>  // 256 queries per block
-__global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a) {
+template <typename T, int NKT, int ABL = 0>  // 256 queries per block
+__global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
     constexpr int QS_WAVES = 16 / QS_QT;
-    constexpr int QS_RT = qs_rows(QS_QT), RF = QS_RT / 16, QS_NS = qs_stages(QS_QT);
-    // QT = 4: query fragments pinned in AGPRs, MFMAs by inline asm, row-fragment reads
-    // software-pipelined (one wave per SIMD: no partner wave hides their latency)
-    constexpr bool PIPE = QS_QT == 4;
+    constexpr int RF = QS_RT / 16;
     using Op = MfmaOp<T>;
     using v8 = typename Op::v8;
     constexpr int STEP_BYTES = QS_RT * 128;  // 16 KB at QT = 2
@@ -374,12 +344,8 @@ __global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a
     for (int qt = 0; qt < QS_QT; ++qt) {
         asm volatile("" ::"v"(thr[qt]));
 #pragma unroll
-        for (int kk = 0; kk < 2 * NKT; ++kk) {
-            if constexpr (PIPE) asm volatile("" ::"a"(qf[qt][kk]));
-            else asm volatile("" ::"v"(qf[qt][kk]));
-        }
+        for (int kk = 0; kk < 2 * NKT; ++kk) asm volatile("" ::"v"(qf[qt][kk]));
     }
-    if constexpr (PIPE) asm volatile("s_nop 7");  // AGPR writes -> MFMA B reads (inline asm: no hazard pass)
 
     // step t = (tile, k-step): 2·RF pieces of 1 KB (8 rows x 128 B); wave w issues pieces w + QS_WAVES·i.
     constexpr int PPW = 2 * RF / QS_WAVES;
@@ -404,14 +370,10 @@ __global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, 0);
         }
     };
-    // one barrier per SPS k-steps (2 at QT = 2, 4 at QT = 4; nsteps is a multiple):
-    // steps t..t+SPS-1 land together, steps t+NS-SPS..t+NS-1 go into the slots freed
-    // by t-SPS..t-1; NS - SPS steps in flight
-#ifdef RC_QS_SPS
-    constexpr int SPS = RC_QS_SPS;
-#else
-    constexpr int SPS = (PIPE && NKT % 4 == 0) ? 4 : 2;
-#endif
+    // one barrier per SPS = 2 k-steps (nsteps is a multiple): steps t..t+SPS-1 land
+    // together, steps t+NS-SPS..t+NS-1 go into the slots freed by t-SPS..t-1; NS - SPS
+    // steps in flight
+    constexpr int SPS = 2;
     for (int t = 0; t < min(QS_NS - SPS, nsteps); ++t) issue(t);
 
     f32x4_t acc[RF][QS_QT];
@@ -420,7 +382,7 @@ __global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a
         for (int rf = 0; rf < RF; ++rf)
 #pragma unroll
             for (int qt = 0; qt < QS_QT; ++qt)
-                if constexpr (!PIPE) acc[rf][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};  // PIPE: first MFMA takes C = 0
+                acc[rf][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kp = 0; kp < NKT / SPS; ++kp) {
             const int t = tile * NKT + SPS * kp;
@@ -439,9 +401,8 @@ __global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a
                 if (!(ABL & 1) && t + j < nsteps) issue(t + j);
             // groups of 4 row fragments, (k half kl, k sub-chunk sh, row quarter rh): 4 reads,
             // then their 4·QT MFMAs with counted lgkmcnt waits.  Row r = 16 rf + li: its
-            // swizzle (r >> 1) & 7 = (li >> 1) & 7 does not depend on rf.  At QT = 2 the
-            // SIMD partner wave's MFMAs cover the read latency; at QT = 4 (one wave per
-            // SIMD) the reads of group gi + 1 are issued before the MFMAs of group gi.
+            // swizzle (r >> 1) & 7 = (li >> 1) & 7 does not depend on rf.  The SIMD
+            // partner wave's MFMAs cover the read latency.
             constexpr int RH = RF / 4, NG = SPS * 2 * RH;
             auto frag_ptr = [&](int gi) {
                 const int kl = gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
@@ -456,43 +417,22 @@ __global__ __launch_bounds__(1024 / QS_QT, 1) void filter_qs_kernel(FilterArgs a
                     dst[i] = (ABL & 4) ? qf[i & 1][(ks * 2 + sh + i) % (2 * NKT)]
                                        : *reinterpret_cast<const v8 *>(Sr + i * 2048);
             };
-            v8 rfr[2][4];
-            if constexpr (PIPE) load_group(0, rfr[0]);
 #pragma unroll
             for (int gi = 0; gi < NG; ++gi) {
                 const int ks = SPS * kp + gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
-                v8 *cur = rfr[PIPE ? (gi & 1) : 0];
-                if constexpr (PIPE) {
-                    if (gi + 1 < NG) load_group(gi + 1, rfr[(gi + 1) & 1]);
-                } else {
-                    load_group(gi, cur);
-                }
+                v8 cur[4];
+                load_group(gi, cur);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int qt = 0; qt < QS_QT; ++qt)
                         if constexpr (ABL & 2)
                             asm volatile("" ::"v"(cur[i]));
-                        else if constexpr (!PIPE)
-                            acc[rh * 4 + i][qt] = Op::mma(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
-                        else if (kp == 0 && gi < RH)
-                            Op::mma_vav0(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
                         else
-                            Op::mma_vav(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
-                if constexpr (!PIPE) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-                }
+                            acc[rh * 4 + i][qt] = Op::mma(cur[i], qf[qt][ks * 2 + sh], acc[rh * 4 + i][qt]);
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
             }
-        }
-        if constexpr (PIPE) {
-            // XDL write -> VALU read of acc: >= 19 wait states for a 16-pass MFMA; the
-            // empty asm per accumulator keeps every epilogue read behind the nops
-            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
-#pragma unroll
-            for (int rf = 0; rf < RF; ++rf)
-#pragma unroll
-                for (int qt = 0; qt < QS_QT; ++qt) asm volatile("" : "+v"(acc[rf][qt]));
         }
         // ---- epilogue of row tile rt0 + tile: candidates s' >= thr[q]
         const int64_t rbase = a.r_begin + (rt0 + tile) * QS_RT + 4 * g;
@@ -659,17 +599,10 @@ void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipSt
     }
 }
 
-// Queries per wave of the query-stationary filter kernel (16·QT): 2 unless
-// RC_FILTER_QT=4 (read once).  With the 2-GB sub-launches the two forms are within
-// 1 % at config 4 (QT = 2 ahead, profiles/r02/r02_ab_results.txt), so the default is
-// the form whose MFMAs the compiler schedules (no inline asm, no manual hazard nops).
-inline int filter_qt() {
-    static const int v = [] {
-        const char *d = std::getenv("RC_FILTER_QT");
-        return d && std::atoi(d) == 4 ? 4 : 2;
-    }();
-    return v;
-}
+#if defined(RC_GEMM_ABLATION)
+// diagnostic builds only (tools/build_diag.sh): filter ablation variant from RC_FILTER_ABL
+static const int filter_abl = std::getenv("RC_FILTER_ABL") ? std::atoi(std::getenv("RC_FILTER_ABL")) : 0;
+#endif
 
 int batch_stage_ratio(int k, int cap) {
     const int g = cap / (5 * k / 2 + 1);
@@ -707,31 +640,19 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
         FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), c0, c1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
         const int nkt = (int)(p.ld / 64);
         if (nkt == 2 || nkt == 4 || nkt == 8) {
-            const int qt = filter_qt();
-            const int64_t rt = qs_rows(qt);
-            fa.tiles_per_chunk = ((c1 - c0 + rt - 1) / rt + nchunk - 1) / nchunk;
-            const dim3 gr((unsigned)(nchunk * nqb));
+            fa.tiles_per_chunk = ((c1 - c0 + QS_RT - 1) / QS_RT + nchunk - 1) / nchunk;
+            const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * 16 / QS_QT);
 #if defined(RC_GEMM_ABLATION)
-            static const int abl = std::getenv("RC_FILTER_ABL") ? std::atoi(std::getenv("RC_FILTER_ABL")) : 0;
-            if (abl && nkt == 8) {
-                const dim3 bl(64 * 16 / qt);
-#define RC_ABL(Q, A) \
-    if (qt == Q && abl == A) hipLaunchKernelGGL((filter_qs_kernel<T, 8, Q, A>), gr, bl, 0, s, fa);
-                RC_ABL(4, 8) RC_ABL(4, 9) RC_ABL(4, 12) RC_ABL(4, 13) RC_ABL(2, 8) RC_ABL(2, 9) RC_ABL(2, 12) RC_ABL(2, 13)
+            if (filter_abl != 0 && nkt == 8) {  // diagnostic builds: RC_FILTER_ABL
+#define RC_ABL(A) \
+    if (filter_abl == A) hipLaunchKernelGGL((filter_qs_kernel<T, 8, A>), gr, bl, 0, s, fa);
+                RC_ABL(8) RC_ABL(9) RC_ABL(12) RC_ABL(13)
 #undef RC_ABL
             } else
 #endif
-            if (qt == 4) {
-                const dim3 bl(64 * 4);
-                if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 4>), gr, bl, 0, s, fa);
-                else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4, 4>), gr, bl, 0, s, fa);
-                else hipLaunchKernelGGL((filter_qs_kernel<T, 2, 4>), gr, bl, 0, s, fa);
-            } else {
-                const dim3 bl(64 * 8);
-                if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8, 2>), gr, bl, 0, s, fa);
-                else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4, 2>), gr, bl, 0, s, fa);
-                else hipLaunchKernelGGL((filter_qs_kernel<T, 2, 2>), gr, bl, 0, s, fa);
-            }
+            if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8>), gr, bl, 0, s, fa);
+            else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4>), gr, bl, 0, s, fa);
+            else hipLaunchKernelGGL((filter_qs_kernel<T, 2>), gr, bl, 0, s, fa);
         } else {
             hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
         }
@@ -770,7 +691,11 @@ void BatchWs::ensure(int nq, int k, int64_t ld, int dtype_bytes) {
     flags = (int *)dmalloc((size_t)nq_cap * sizeof(int));
     ovf = (int *)dmalloc(sizeof(int));
     RC_HIP(hipMemset(ovf, 0, sizeof(int)));
-    fb_partial = (uint64_t *)dmalloc((size_t)FB_BLOCKS * nq_cap * k_cap * sizeof(uint64_t));
+    // the fallback scan's partial lists are sized by a memory budget, not by the row count:
+    // 1024 queries x top-100 keep all 256 blocks (210 MB); 4096 x 256 get 32 (268 MB) instead of 2.1 GB
+    const int64_t per_block = (int64_t)nq_cap * k_cap * (int64_t)sizeof(uint64_t);
+    fb_blocks = (int)std::max<int64_t>(FB_MIN_BLOCKS, std::min<int64_t>(FB_BLOCKS, FB_BUDGET_BYTES / per_block));
+    fb_partial = (uint64_t *)dmalloc((size_t)fb_blocks * per_block);
 }
 
 void BatchWs::release() {
@@ -791,6 +716,7 @@ void BatchWs::release() {
     keys = nullptr;
     flags = ovf = nullptr;
     fb_partial = nullptr;
+    fb_blocks = 0;
     nq_cap = k_cap = 0;
     ld_cap = 0;
 }

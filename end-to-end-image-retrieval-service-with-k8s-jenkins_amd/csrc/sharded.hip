@@ -24,6 +24,18 @@
 namespace rc {
 void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *rows,
                          hipStream_t s);
+
+// dst[i][:] = src[idx[i]][:] (one wave per row): a remote shard's subset of an upsert
+// batch, made contiguous on the leader so only those rows cross xGMI.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ src, const int64_t *__restrict__ idx,
+                                                         int64_t m, int dim, float *__restrict__ dst) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= m) return;
+    const float *s = src + idx[i] * dim;
+    float *d = dst + i * dim;
+    for (int c = lane; c < dim; c += 64) d[c] = s[c];
+}
 }
 
 using namespace rc;
@@ -44,11 +56,17 @@ struct rc_sharded {
     std::vector<int64_t *> r_loc;
     float *g_s = nullptr;         // leader [n][nq_cap][k_cap] gathered lists
     int64_t *g_r = nullptr;
-    // upsert / fetch staging
+    // upsert / fetch staging (grown on demand, reused: no allocation in steady state)
     int64_t st_cap = 0;
-    std::vector<int64_t *> idx_d;  // [st_cap] source index per shard
-    std::vector<int64_t *> row_d;  // [st_cap] local row per shard
-    std::vector<float *> vec_d;    // [st_cap][dim] vectors on a non-leader shard's device
+    std::vector<int64_t *> idx_d;  // [st_cap] source index per shard (on the leader for a remote shard)
+    std::vector<int64_t *> row_d;  // [st_cap] local row per shard (on the shard's device)
+    std::vector<float *> vec_d;    // [st_cap][dim] a remote shard's subset of the batch, on its device
+    std::vector<float *> gat_d;    // [st_cap][dim] that subset gathered on the leader (peer-copy source)
+    std::vector<float *> fo_d;     // [st_cap][dim] fetched rows on the shard's device
+    std::vector<int64_t *> idx_h;  // [st_cap] pinned host copies of the per-shard lists
+    std::vector<int64_t *> row_h;
+    std::vector<float *> fo_h;     // [st_cap][dim] pinned host landing of fetched rows
+    hipEvent_t ev_gather = nullptr;  // leader stream: the remote subsets are gathered
 };
 
 namespace {
@@ -92,24 +110,48 @@ void ensure_search(rc_sharded *h, int nq, int k) {
 void free_staging(rc_sharded *h) {
     for (int s = 0; s < h->n; ++s) {
         DeviceScope ds(h->dev[s]);
-        dfree(h->idx_d[s]);
         dfree(h->row_d[s]);
         dfree(h->vec_d[s]);
-        h->idx_d[s] = h->row_d[s] = nullptr;
-        h->vec_d[s] = nullptr;
+        dfree(h->fo_d[s]);
+        hfree(h->idx_h[s]);
+        hfree(h->row_h[s]);
+        hfree(h->fo_h[s]);
+        h->row_d[s] = nullptr;
+        h->vec_d[s] = h->fo_d[s] = h->fo_h[s] = nullptr;
+        h->idx_h[s] = h->row_h[s] = nullptr;
+    }
+    DeviceScope dl(h->dev[0]);
+    for (int s = 0; s < h->n; ++s) {
+        dfree(h->idx_d[s]);
+        dfree(h->gat_d[s]);
+        h->idx_d[s] = nullptr;
+        h->gat_d[s] = nullptr;
     }
     h->st_cap = 0;
 }
 
+// Per shard, room for m rows of one call: index lists (pinned host + device), the
+// remote shards' gathered subset (leader) and its landing (shard device), fetch
+// buffers.  Grows geometrically, so a steady stream of calls allocates nothing.
 void ensure_staging(rc_sharded *h, int64_t m) {
     if (m <= h->st_cap) return;
     const int64_t m2 = std::max<int64_t>(m, 2 * h->st_cap);
     free_staging(h);
+    const size_t vb = (size_t)m2 * h->dim * sizeof(float);
     for (int s = 0; s < h->n; ++s) {
-        DeviceScope ds(h->dev[s]);
+        const bool remote = h->dev[s] != h->dev[0];
+        {
+            DeviceScope ds(h->dev[s]);
+            h->row_d[s] = (int64_t *)dmalloc((size_t)m2 * sizeof(int64_t));
+            h->fo_d[s] = (float *)dmalloc(vb);
+            if (remote) h->vec_d[s] = (float *)dmalloc(vb);
+        }
+        DeviceScope dl(h->dev[0]);  // the source index lists are read on the leader (gather / local upsert)
         h->idx_d[s] = (int64_t *)dmalloc((size_t)m2 * sizeof(int64_t));
-        h->row_d[s] = (int64_t *)dmalloc((size_t)m2 * sizeof(int64_t));
-        if (h->dev[s] != h->dev[0]) h->vec_d[s] = (float *)dmalloc((size_t)m2 * h->dim * sizeof(float));
+        if (remote) h->gat_d[s] = (float *)dmalloc(vb);
+        h->idx_h[s] = (int64_t *)hmalloc((size_t)m2 * sizeof(int64_t));
+        h->row_h[s] = (int64_t *)hmalloc((size_t)m2 * sizeof(int64_t));
+        h->fo_h[s] = (float *)hmalloc(vb);
     }
     h->st_cap = m2;
 }
@@ -126,6 +168,10 @@ void destroy(rc_sharded *h) {
         if (h->ev_done[s]) (void)hipEventDestroy(h->ev_done[s]);
         if (h->ev_start[s]) (void)hipEventDestroy(h->ev_start[s]);
         if (h->shard[s]) (void)rc_index_destroy(h->shard[s]);
+    }
+    if (h->ev_gather) {
+        DeviceScope dl(h->dev[0]);
+        (void)hipEventDestroy(h->ev_gather);
     }
     delete h;
 }
@@ -160,6 +206,11 @@ int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int6
         h->idx_d.assign(n_shards, nullptr);
         h->row_d.assign(n_shards, nullptr);
         h->vec_d.assign(n_shards, nullptr);
+        h->gat_d.assign(n_shards, nullptr);
+        h->fo_d.assign(n_shards, nullptr);
+        h->idx_h.assign(n_shards, nullptr);
+        h->row_h.assign(n_shards, nullptr);
+        h->fo_h.assign(n_shards, nullptr);
         try {
             for (int s = 0; s < n_shards; ++s) {
                 check_status(rc_index_create(h->dev[s], dim, dtype, capacity_per_shard, s, &h->shard[s]));
@@ -175,6 +226,7 @@ int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int6
             }
             DeviceScope dl(h->dev[0]);
             for (int s = 0; s < n_shards; ++s) RC_HIP(hipEventCreateWithFlags(&h->ev_start[s], hipEventDisableTiming));
+            RC_HIP(hipEventCreateWithFlags(&h->ev_gather, hipEventDisableTiming));
         } catch (...) {
             destroy(h);
             throw;
@@ -224,38 +276,57 @@ int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t
         if (n == 0) return;
         RC_REQUIRE(vecs && rows, RC_ERR_INVALID, "null buffer");
         std::lock_guard<std::mutex> lk(h->mu);
-        std::vector<std::vector<int64_t>> src(h->n), loc(h->n);
+        std::vector<int64_t> cnt(h->n, 0);
         for (int64_t i = 0; i < n; ++i) {
             const int64_t g = rows[i];
             RC_REQUIRE(g >= 0 && g / h->n < h->cap, RC_ERR_INVALID, "row out of capacity");
-            src[g % h->n].push_back(i);
-            loc[g % h->n].push_back(g / h->n);
+            ++cnt[g % h->n];
         }
         int64_t m = 0;
-        for (int s = 0; s < h->n; ++s) m = std::max<int64_t>(m, (int64_t)src[s].size());
-        ensure_staging(h, std::max<int64_t>(m, n));
+        for (int s = 0; s < h->n; ++s) m = std::max<int64_t>(m, cnt[s]);
+        ensure_staging(h, m);
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (int64_t i = 0; i < n; ++i) {  // per-shard (source index, local row) lists, pinned
+            const int64_t g = rows[i];
+            const int s = (int)(g % h->n);
+            h->idx_h[s][cnt[s]] = i;
+            h->row_h[s][cnt[s]] = g / h->n;
+            ++cnt[s];
+        }
         hipStream_t ls = (hipStream_t)stream;
         {
+            // leader stream: source lists of every shard, then each remote shard's subset gathered
+            // contiguous (cnt[s] rows, not the whole batch, cross xGMI)
             DeviceScope dl(h->dev[0]);
-            for (int s = 0; s < h->n; ++s) RC_HIP(hipEventRecord(h->ev_start[s], ls));
+            for (int s = 0; s < h->n; ++s) {
+                if (cnt[s] == 0) continue;
+                RC_HIP(hipMemcpyAsync(h->idx_d[s], h->idx_h[s], cnt[s] * sizeof(int64_t), hipMemcpyHostToDevice, ls));
+                if (h->dev[s] != h->dev[0]) {
+                    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((cnt[s] + 3) / 4)), dim3(256), 0, ls, vecs,
+                                       h->idx_d[s], cnt[s], h->dim, h->gat_d[s]);
+                    RC_LAUNCH_CHECK();
+                }
+            }
+            RC_HIP(hipEventRecord(h->ev_gather, ls));
         }
         for (int s = 0; s < h->n; ++s) {
-            if (src[s].empty()) continue;
+            if (cnt[s] == 0) continue;
             DeviceScope ds(h->dev[s]);
-            const int64_t ms = (int64_t)src[s].size();
-            RC_HIP(hipStreamWaitEvent(h->st[s], h->ev_start[s], 0));
-            RC_HIP(hipMemcpyAsync(h->idx_d[s], src[s].data(), ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
-            RC_HIP(hipMemcpyAsync(h->row_d[s], loc[s].data(), ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
-            const float *v = vecs;
+            const int64_t ms = cnt[s];
+            RC_HIP(hipStreamWaitEvent(h->st[s], h->ev_gather, 0));
+            RC_HIP(hipMemcpyAsync(h->row_d[s], h->row_h[s], ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
             if (h->dev[s] != h->dev[0]) {
-                RC_HIP(hipMemcpyPeerAsync(h->vec_d[s], h->dev[s], vecs, h->dev[0], (size_t)n * h->dim * sizeof(float), h->st[s]));
-                v = h->vec_d[s];
+                RC_HIP(hipMemcpyPeerAsync(h->vec_d[s], h->dev[s], h->gat_d[s], h->dev[0], (size_t)ms * h->dim * sizeof(float),
+                                          h->st[s]));
+                index_upsert_gather(h->shard[s], h->vec_d[s], nullptr, ms, h->row_d[s], h->st[s]);
+            } else {
+                index_upsert_gather(h->shard[s], vecs, h->idx_d[s], ms, h->row_d[s], h->st[s]);
             }
-            index_upsert_gather(h->shard[s], v, h->idx_d[s], ms, h->row_d[s], h->st[s]);
         }
-        // the host index lists must outlive their async copies: finish here (upsert is synchronous,
+        // the pinned lists are reused by the next call: finish here (upsert is synchronous,
         // like the Pinecone call it replaces)
         for (int s = 0; s < h->n; ++s) {
+            if (cnt[s] == 0) continue;
             DeviceScope ds(h->dev[s]);
             RC_HIP(hipStreamSynchronize(h->st[s]));
         }
@@ -269,36 +340,40 @@ int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, 
         if (n == 0) return;
         RC_REQUIRE(rows && out, RC_ERR_INVALID, "null buffer");
         std::lock_guard<std::mutex> lk(h->mu);
-        std::vector<std::vector<int64_t>> dst(h->n), loc(h->n);
+        std::vector<int64_t> cnt(h->n, 0);
         for (int64_t i = 0; i < n; ++i) {
             const int64_t g = rows[i];
             RC_REQUIRE(g >= 0 && g / h->n < h->cap, RC_ERR_INVALID, "row out of capacity");
-            dst[g % h->n].push_back(i);
-            loc[g % h->n].push_back(g / h->n);
+            ++cnt[g % h->n];
         }
         int64_t m = 0;
-        for (int s = 0; s < h->n; ++s) m = std::max<int64_t>(m, (int64_t)dst[s].size());
+        for (int s = 0; s < h->n; ++s) m = std::max<int64_t>(m, cnt[s]);
         ensure_staging(h, m);
-        std::vector<float> tmp;
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t g = rows[i];
+            const int s = (int)(g % h->n);
+            h->idx_h[s][cnt[s]] = i;  // destination row of out
+            h->row_h[s][cnt[s]] = g / h->n;
+            ++cnt[s];
+        }
+        // every shard's fetch and D2H copy in flight at once, one wait at the end
         for (int s = 0; s < h->n; ++s) {
-            if (dst[s].empty()) continue;
+            if (cnt[s] == 0) continue;
             DeviceScope ds(h->dev[s]);
-            const int64_t ms = (int64_t)dst[s].size();
-            float *buf = (float *)dmalloc((size_t)ms * h->dim * sizeof(float));
-            try {
-                RC_HIP(hipMemcpyAsync(h->row_d[s], loc[s].data(), ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
-                check_status(stored ? rc_index_fetch_stored(h->shard[s], h->row_d[s], ms, buf, h->st[s])
-                                    : rc_index_fetch(h->shard[s], h->row_d[s], ms, buf, h->st[s]));
-                tmp.resize((size_t)ms * h->dim);
-                RC_HIP(hipMemcpyAsync(tmp.data(), buf, tmp.size() * sizeof(float), hipMemcpyDeviceToHost, h->st[s]));
-                RC_HIP(hipStreamSynchronize(h->st[s]));
-            } catch (...) {
-                dfree(buf);
-                throw;
-            }
-            dfree(buf);
-            for (int64_t j = 0; j < ms; ++j)
-                std::memcpy(out + dst[s][j] * h->dim, tmp.data() + j * h->dim, (size_t)h->dim * sizeof(float));
+            const int64_t ms = cnt[s];
+            RC_HIP(hipMemcpyAsync(h->row_d[s], h->row_h[s], ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
+            check_status(stored ? rc_index_fetch_stored(h->shard[s], h->row_d[s], ms, h->fo_d[s], h->st[s])
+                                : rc_index_fetch(h->shard[s], h->row_d[s], ms, h->fo_d[s], h->st[s]));
+            RC_HIP(hipMemcpyAsync(h->fo_h[s], h->fo_d[s], (size_t)ms * h->dim * sizeof(float), hipMemcpyDeviceToHost,
+                                  h->st[s]));
+        }
+        for (int s = 0; s < h->n; ++s) {
+            if (cnt[s] == 0) continue;
+            DeviceScope ds(h->dev[s]);
+            RC_HIP(hipStreamSynchronize(h->st[s]));
+            for (int64_t j = 0; j < cnt[s]; ++j)
+                std::memcpy(out + h->idx_h[s][j] * h->dim, h->fo_h[s] + j * h->dim, (size_t)h->dim * sizeof(float));
         }
     });
 }

@@ -107,7 +107,9 @@ struct Layer {
 
 constexpr int kMaxParts = 4;
 
-enum TimerId { T_GEMM = 0, T_FC1 = 1, T_ATTN = 2, T_LN = 3, T_PRE = 4, T_COUNT = 5 };
+// T_GEMM: every GEMM; T_QKV / T_OPROJ / T_FC1 / T_FC2: that projection's full-batch
+// launches (M = images x 197 rows), each priced on its own in the bench
+enum TimerId { T_GEMM = 0, T_FC1 = 1, T_ATTN = 2, T_LN = 3, T_PRE = 4, T_QKV = 5, T_OPROJ = 6, T_FC2 = 7, T_COUNT = 8 };
 
 }  // namespace
 
@@ -139,16 +141,15 @@ struct rc_model {
     float *ln_stats = nullptr;     // [Mp][3][2] LayerNorm-fold partials (per 256-column tile: mean, M2)
     bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
-    bool cls_only_last = true;     // rc_model_set_last_layer / RC_EMBED_FULL_LAST=1
+    bool cls_only_last = true;     // rc_model_set_last_layer
     float *cls_hidden = nullptr, *cls_stats = nullptr;
     float *cls_part = nullptr;     // split-K partials of the CLS-row fc2 [SKINNY_KS][Cp][H]
     uint16_t *cls_ln = nullptr, *cls_attn = nullptr, *cls_mlp = nullptr;
     uint8_t *resized = nullptr, *resize_tmp = nullptr;
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
-    int gemm_variant = GEMM_AUTO;  // RC_GEMM_VARIANT env overrides (A/B benchmarking)
-    int attn_variant = 2;          // RC_ATTN_VARIANT=1 selects the v1 kernel
-    int split = 2;                 // batch parts encoded concurrently (RC_EMBED_SPLIT / rc_model_set_parts);
+    int gemm_variant = GEMM_AUTO;  // diagnostic builds: RC_GEMM_VARIANT (ablation variants)
+    int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
     hipStream_t sp[4] = {};        // streams of parts 1..3 (part 0 runs on the caller's stream)
@@ -361,20 +362,21 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
     return m->resized;
 }
 
+// role: T_QKV / T_OPROJ / T_FC1 / T_FC2 (its own timer besides T_GEMM), or -1
 template <int EPI>
-void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, bool fc1 = false) {
+void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
-    const int t1 = fc1 ? m->timers[T_FC1].begin(s) : -1;
+    const int t1 = role >= 0 ? m->timers[role].begin(s) : -1;
     launch_gemm<EPI>(a, m->gemm_variant, s);
-    if (fc1) m->timers[T_FC1].end(t1, s, flops);
+    if (role >= 0) m->timers[role].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
 
 // residual-stream producer GEMM (O-proj, fc2): f32 stream, or bf16 pairs under the fold
-void resid_gemm(rc_model *m, const GemmArgs &a, hipStream_t s) {
-    if (a.res_lo != nullptr) gemm<EPI_RESID_HL>(m, a, s);
-    else gemm<EPI_RESID_F32>(m, a, s);
+void resid_gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role) {
+    if (a.res_lo != nullptr) gemm<EPI_RESID_HL>(m, a, s, role);
+    else gemm<EPI_RESID_F32>(m, a, s, role);
 }
 
 void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint16_t *y, int M, hipStream_t s) {
@@ -500,19 +502,17 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             a.ln_c = L.c_qkv + q0;
             a.ln_stats = st;
             a.ln_eps = c.ln_eps;
-            gemm<EPI_BF16_LN>(m, a, s);
+            gemm<EPI_BF16_LN>(m, a, s, kv_only ? -1 : T_QKV);
         } else {
             layernorm(m, hidden, L.ln1_w, L.ln1_b, ln, M, s);
-            gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s);
+            gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s, T_QKV);
         }
         if (m->cls_only_last && l == c.layers - 1) {
             last_layer_cls(m, L, i0, n, qkv, hidden, fold ? ln : nullptr, lo, st, scale, s);
             break;
         }
         const int ta = m->timers[T_ATTN].begin(s);
-        if (m->attn_variant == 1 || T > ATT2_ROWS)
-            hipLaunchKernelGGL(attention_kernel, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads, scale);
-        else if (T == 197)
+        if (T == 197)
             hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
         else
@@ -520,20 +520,20 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
                                scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
-        resid_gemm(m, produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true), s);
+        resid_gemm(m, produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true), s, T_OPROJ);
         if (fold) {
             GemmArgs a{ln, L.w_fc1_f, L.b_fc1_f, M, c.mlp, H, mlp, nullptr, nullptr, T};
             a.ln_c = L.c_fc1;
             a.ln_stats = st;
             a.ln_eps = c.ln_eps;
-            gemm<EPI_GELU_BF16_LN>(m, a, s, true);
+            gemm<EPI_GELU_BF16_LN>(m, a, s, T_FC1);
         } else {
             layernorm(m, hidden, L.ln2_w, L.ln2_b, ln, M, s);
-            gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, true);
+            gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, T_FC1);
         }
         // the last layer's fc2 feeds only the final LN of the CLS rows (cls_final_kernel)
         resid_gemm(m, produce(GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T},
-                              l + 1 < c.layers), s);
+                              l + 1 < c.layers), s, T_FC2);
     }
     // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
     const float *fin = m->cls_only_last ? m->cls_hidden + (int64_t)i0 * H : hidden;
@@ -584,8 +584,8 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
         RC_REQUIRE(cfg->hidden == 768 && cfg->patch == 16 && cfg->heads * 64 == cfg->hidden, RC_ERR_UNSUPPORTED,
                    "this build implements ViT-B/16 geometry (hidden 768, patch 16, head dim 64)");
         RC_REQUIRE(cfg->image_size % cfg->patch == 0 && cfg->image_size <= 224, RC_ERR_UNSUPPORTED,
-                   "image_size must be a multiple of 16 and <= 224 (tokens <= 224)");
-        RC_REQUIRE(cfg->mlp % GEMM_BN == 0 && cfg->layers >= 1 && cfg->max_batch >= 1, RC_ERR_INVALID, "bad config");
+                   "image_size must be a multiple of 16 and <= 224 (tokens <= 197: attention_v2_kernel's LDS)");
+        RC_REQUIRE(cfg->mlp % 256 == 0 && cfg->layers >= 1 && cfg->max_batch >= 1, RC_ERR_INVALID, "bad config");
         DeviceScope ds(device);
         auto *m = new rc_model();
         try {
@@ -619,7 +619,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->cls_ln, 0, (size_t)Cp * H * 2));
             RC_HIP(hipMemset(m->cls_attn, 0, (size_t)Cp * H * 2));
             RC_HIP(hipMemset(m->cls_mlp, 0, (size_t)Cp * cfg->mlp * 2));
-            if (const char *fl = std::getenv("RC_EMBED_FULL_LAST")) m->cls_only_last = std::atoi(fl) == 0;
             // pad rows are read by the GEMM tiles: keep them finite (zero) forever
             RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
             RC_HIP(hipMemset(m->ln, 0, (size_t)m->Mp * H * 2));
@@ -628,9 +627,9 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));
             build_lut(m);
+#if defined(RC_GEMM_ABLATION)
             if (const char *gv = std::getenv("RC_GEMM_VARIANT")) m->gemm_variant = std::atoi(gv);
-            if (const char *av = std::getenv("RC_ATTN_VARIANT")) m->attn_variant = std::atoi(av);
-            if (const char *sp = std::getenv("RC_EMBED_SPLIT")) m->split = std::atoi(sp);
+#endif
             RC_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
             for (int p = 1; p < kMaxParts; ++p) {
                 RC_HIP(hipStreamCreateWithFlags(&m->sp[p], hipStreamNonBlocking));

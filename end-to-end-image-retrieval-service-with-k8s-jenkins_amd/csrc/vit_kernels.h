@@ -4,10 +4,10 @@
 // from embedding/main.py:111-113):
 //   patch embed Conv2d(3,768,16,16) (:57)  → patch_gemm_kernel (gemm.h): implicit GEMM
 //                                            reading the u8 images through a bf16 LUT
-//   q/k/v/o, fc1, fc2 nn.Linear (:199-202,243-244) → gemm_bf16_kernel (bias / GELU /
-//                                            residual epilogues fused)
+//   q/k/v/o, fc1, fc2 nn.Linear (:199-202,243-244) → gemm_pp_kernel & co (gemm.h: bias /
+//                                            GELU / residual / LayerNorm-fold epilogues fused)
 //   LayerNorm eps 1e-6 (:258-259,327)      → layernorm_kernel (f32 in, bf16 out)
-//   eager attention, scale 1/8, fp32 softmax (:161-186) → attention_kernel
+//   eager attention, scale 1/8, fp32 softmax (:161-186) → attention_v2_kernel
 //   last_hidden_state[:,0,:] (main.py:113) → cls_final_kernel (final LN on the
 //                                            CLS rows, raw + L2-normalised outputs)
 // Preprocessing (ViTImageProcessor, main.py:107): resize_{h,v}_kernel (Pillow
@@ -151,121 +151,6 @@ __device__ __forceinline__ void ln_emit_row(const float4 v, uint16_t *__restrict
                                             int lane, bool store) {
     const float2 st = ln_row_stats(v);
     if (store) ln_row_store(v, st, xrow, strow, lane);
-}
-
-constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 64;
-
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-
-// C = A · Wᵀ (+ epilogue).  256 threads = 4 waves as 2 (M) × 2 (N), each wave a
-// 64×64 sub-tile of 4×4 mfma_f32_16x16x32_bf16 accumulators.  A/W tiles are
-// staged global→LDS with global_load_lds_dwordx4 (2-deep), rows of 128 B with
-// the 16-B chunk index XORed by (row>>1)&7 so the fragment ds_read_b128s are
-// bank-conflict-free; the XOR is applied to the per-lane SOURCE address because
-// the LDS-DMA destination is lane-linear.
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
-    constexpr int BM = GEMM_BM, BN = GEMM_BN, BK = GEMM_BK;
-    constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB (A) ; W tile same
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * TILE_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-
-    // XCD-aware, bijective block remap: blocks b and b+8 share an XCD, so give
-    // each XCD a contiguous run of tiles (tile = tm * ntn + tn: the N tiles of
-    // one A row-panel stay on one L2).
-    const int ntn = a.N / BN;
-    const int nwg = gridDim.x;
-    const int orig = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    const int tm = tile / ntn, tn = tile % ntn;
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    const int K = a.K;
-    const uint16_t *Ag = a.A + (int64_t)m0 * K;
-    const uint16_t *Wg = a.W + (int64_t)n0 * K;
-
-    // staging: wave w issues 4 A + 4 W LDS-DMA pieces of 1 KB (8 rows x 128 B)
-    auto stage = [&](int buf, int k0) {
-        uint8_t *As = smem + buf * 2 * TILE_BYTES;
-        uint8_t *Ws = As + TILE_BYTES;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int piece = wave * 4 + i;
-            const int r = piece * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            __builtin_amdgcn_global_load_lds((const void *)(Ag + (int64_t)r * K + k0 + c * 8),
-                                             (lds_void_t *)(As + piece * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void *)(Wg + (int64_t)r * K + k0 + c * 8),
-                                             (lds_void_t *)(Ws + piece * 1024), 16, 0, 0);
-        }
-    };
-
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = K / BK;
-    stage(0, 0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-        const uint8_t *As = smem + cur * 2 * TILE_BYTES;
-        const uint8_t *Ws = As + TILE_BYTES;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int c = s * 4 + (lane >> 4);
-            bf16x8 af[4], bfr[4];
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int r = wm * 64 + mi * 16 + (lane & 15);
-                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int r = wn * 64 + ni * 16 + (lane & 15);
-                bfr[ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-        }
-        __syncthreads();  // next tile landed (vmcnt(0)) and everyone is done reading `cur`
-    }
-
-    // epilogue: lane holds C[row = 4*(lane>>4) + j][col = lane&15] of each 16x16 tile
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-        const int col = n0 + wn * 64 + ni * 16 + (lane & 15);
-        const float bcol = a.bias[col];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int row = m0 + wm * 64 + mi * 16 + (lane >> 4) * 4 + j;
-                if (row >= a.M) continue;
-                float v = acc[mi][ni][j] + bcol;
-                if constexpr (EPI == EPI_BF16) {
-                    a.out_bf16[(int64_t)row * a.N + col] = f32_to_bf16(v);
-                } else if constexpr (EPI == EPI_GELU_BF16) {
-                    a.out_bf16[(int64_t)row * a.N + col] = f32_to_bf16(gelu_erf(v));
-                } else if constexpr (EPI == EPI_RESID_F32) {
-                    float *o = a.out_f32 + (int64_t)row * a.N + col;
-                    *o = *o + v;
-                } else {  // EPI_PATCH_F32: row = (image, patch) → hidden row image*tokens + 1 + patch
-                    const int np = a.tokens - 1;
-                    const int img = row / np, p = row - img * np;
-                    a.out_f32[((int64_t)img * a.tokens + 1 + p) * a.N + col] = v + a.pos[(int64_t)(1 + p) * a.N + col];
-                }
-            }
-        }
-    }
 }
 
 // One wave per row of H = 256*NV f32 values → bf16 LayerNorm output.
@@ -537,122 +422,6 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
         if (has_next) {
             qf[0] = qn[0];
             qf[1] = qn[1];
-        }
-    }
-}
-
-// Self-attention for one (image, head): S = 197 tokens, head dim 64.
-// K (XOR-swizzled 128-B rows) and V (160-B rows, conflict-free for the
-// transposed reads) of the head live in LDS; each wave takes 16-query tiles.
-// Sᵀ = K·Qᵀ puts the query on the MFMA column (lane&15), so softmax over keys
-// is a per-lane reduction plus two xor-shuffles, and Pᵀ sits in registers in
-// exactly the B-operand layout of Oᵀ = Vᵀ·Pᵀ (k order permuted per 32-key step:
-// element j of lane group g is key 16t+4g+j (j<4) or 16(t+1)+4g+j-4), whose A
-// operand comes from V by ds_read_b64_tr_b16.
-constexpr int ATT_TP = 224;  // keys padded to 14 tiles of 16
-constexpr int ATT_VROW = 160;
-
-__global__ __launch_bounds__(256, 2) void attention_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                       int tokens, int heads, float scale) {
-    constexpr int HD = 64;
-    __shared__ __attribute__((aligned(16))) uint8_t Ks[ATT_TP * 128];
-    __shared__ __attribute__((aligned(16))) uint8_t Vs[ATT_TP * ATT_VROW];
-    const int H = heads * HD, H3 = 3 * H;
-    const int img = blockIdx.x / heads, h = blockIdx.x % heads;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD;
-
-    for (int idx = tid; idx < ATT_TP * 8; idx += 256) {
-        const int r = idx >> 3, c = idx & 7;
-        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-        if (r < tokens) {
-            kv = *reinterpret_cast<const uint4 *>(base + (int64_t)r * H3 + H + c * 8);
-            vv = *reinterpret_cast<const uint4 *>(base + (int64_t)r * H3 + 2 * H + c * 8);
-        }
-        *reinterpret_cast<uint4 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = kv;
-        *reinterpret_cast<uint4 *>(Vs + r * ATT_VROW + c * 16) = vv;
-    }
-    __syncthreads();
-
-    const int g = lane >> 4, li = lane & 15;
-    const int nqt = (tokens + 15) / 16;
-    for (int qt = wave; qt < nqt; qt += 4) {
-        const int q = qt * 16 + li;
-        const int qc = q < tokens ? q : tokens - 1;
-        bf16x8 qf[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-            qf[s] = *reinterpret_cast<const bf16x8 *>(base + (int64_t)qc * H3 + s * 32 + g * 8);
-
-        f32x4 st[14];
-#pragma unroll
-        for (int t = 0; t < 14; ++t) {
-            st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const int r = t * 16 + li;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int c = s * 4 + g;
-                const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[t], 0, 0, 0);
-            }
-        }
-        // softmax over keys for query column li (keys spread over t, j and the 4 lane groups)
-        float mx = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 14; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = t * 16 + g * 4 + j;
-                const float v = key < tokens ? st[t][j] * scale : -INFINITY;
-                st[t][j] = v;
-                mx = fmaxf(mx, v);
-            }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        float sum = 0.f;
-#pragma unroll
-        for (int t = 0; t < 14; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float p = __expf(st[t][j] - mx);
-                st[t][j] = p;
-                sum += p;
-            }
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
-
-        f32x4 o[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int qq = li >> 2, pp = li & 3;
-#pragma unroll
-        for (int tp = 0; tp < 7; ++tp) {
-            const int t = tp * 2;
-            bf16x8 pf;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                pf[j] = (__bf16)st[t][j];
-                pf[j + 4] = (__bf16)st[t + 1][j];
-            }
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const int col = d * 16 + pp * 4;
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s16x4_t *)(Vs + (t * 16 + g * 4 + qq) * ATT_VROW + col * 2));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s16x4_t *)(Vs + (t * 16 + 16 + g * 4 + qq) * ATT_VROW + col * 2));
-                const short __attribute__((ext_vector_type(8))) vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
-            }
-        }
-        if (q < tokens) {
-            const float inv = 1.0f / sum;
-            uint16_t *orow = out + ((int64_t)img * tokens + q) * H + h * HD;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                *reinterpret_cast<uint2 *>(orow + d * 16 + g * 4) =
-                    make_uint2(pack_bf16x2(o[d][0] * inv, o[d][1] * inv), pack_bf16x2(o[d][2] * inv, o[d][3] * inv));
-            }
         }
     }
 }

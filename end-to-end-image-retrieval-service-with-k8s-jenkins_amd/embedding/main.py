@@ -26,7 +26,7 @@ from fastapi.exceptions import RequestValidationError
 from PIL import Image, UnidentifiedImageError
 
 from ..config import Config
-from ..multipart import parse_form
+from ..multipart import parse_form, parse_form_all
 
 app = FastAPI(title="ViT-MSN Embedding Service")
 
@@ -34,18 +34,57 @@ _embedder = None
 _embedder_lock = threading.Lock()
 
 
+def embed_devices(spec: str | None = None) -> list:
+    """GPUs of the embedding replicas: ``Config.EMBED_DEVICES`` ("all", "0,1", repeats allowed),
+    or by default the distinct GPUs the index shards live on (one model per GPU)."""
+    import torch
+
+    spec = Config.EMBED_DEVICES if spec is None else spec
+    if spec.strip() == "all":
+        return list(range(torch.cuda.device_count()))
+    if spec.strip():
+        return [int(x) for x in spec.split(",") if x.strip()]
+    from ..ingesting.utils import index_devices
+
+    out = []
+    for d in index_devices():
+        d = torch.cuda.current_device() if d is None else int(d)
+        if d not in out:
+            out.append(d)
+    return out
+
+
 def get_embedder():
-    """Process-wide model singleton (reference loads it at import, ``:37-39``; here on first use)."""
+    """Process-wide model singleton (reference loads it at import, ``:37-39``; here on first use).
+
+    One GPU: a ``VitMsnEmbedder``.  Several (``embed_devices()``): an ``EmbedderPool`` with
+    one model per GPU — the reference's embedding replicas (``helm_charts/embedding/
+    values.yaml:1``) as data parallelism inside the process, no collectives."""
     global _embedder
     with _embedder_lock:
         if _embedder is None:
-            from ..vit import VitMsnEmbedder, random_state_dict
+            from ..vit import EmbedderPool, VitMsnEmbedder, load_checkpoint_dir, random_state_dict
 
+            devs = embed_devices()
             if Config.MODEL_PATH:
-                _embedder = VitMsnEmbedder.from_pretrained(Config.MODEL_PATH, max_batch=Config.EMBED_MAX_BATCH)
+                sd, cfg, pre = load_checkpoint_dir(Config.MODEL_PATH)
             else:  # no checkpoint offline: deterministic seeded weights
-                _embedder = VitMsnEmbedder(random_state_dict(Config.WEIGHT_SEED), max_batch=Config.EMBED_MAX_BATCH)
+                sd, cfg, pre = random_state_dict(Config.WEIGHT_SEED), None, None
+            if len(devs) > 1:
+                _embedder = EmbedderPool(sd, devs, max_batch=Config.EMBED_MAX_BATCH, model_config=cfg, preprocess=pre)
+            else:
+                _embedder = VitMsnEmbedder(sd, device=devs[0] if devs else None, max_batch=Config.EMBED_MAX_BATCH,
+                                           model_config=cfg, preprocess=pre)
         return _embedder
+
+
+def reset_embedder() -> None:
+    """Drop the singleton (tests / reconfiguration); the next get_embedder() builds it anew."""
+    global _embedder
+    with _embedder_lock:
+        if _embedder is not None:
+            _embedder.close()
+        _embedder = None
 
 
 def _missing_file(field: str):
@@ -127,16 +166,7 @@ async def embed_image(request: Request):
 
 @app.post("/embed_batch", response_model=List[List[float]])
 async def embed_images(request: Request):
-    body = await request.body()
-    ctype = request.headers.get("content-type", "")
-    from email.parser import BytesParser
-    from email.policy import HTTP
-
-    if not ctype.lower().startswith("multipart/form-data"):
+    files = parse_form_all(await request.body(), request.headers.get("content-type", "")).get("files")
+    if not files:
         raise _missing_file("files")
-    msg = BytesParser(policy=HTTP).parsebytes(b"Content-Type: " + ctype.encode("latin-1") + b"\r\n\r\n" + body)
-    blobs = [p.get_payload(decode=True) or b"" for p in msg.iter_parts()
-             if p.get_param("name", header="content-disposition") == "files"]
-    if not blobs:
-        raise _missing_file("files")
-    return embed_many(blobs)
+    return embed_many([f.data for f in files])

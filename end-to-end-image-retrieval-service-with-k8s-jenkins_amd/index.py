@@ -305,6 +305,34 @@ class ShardSet:
             raise ValueError("rows and vectors differ in length")
         check(self.lib.rc_sharded_upsert(self.handle, ptr(vecs), vecs.shape[0], ptr(rows), stream_ptr(None)))
 
+    def upsert_parts(self, parts) -> None:
+        """Upsert vectors that already live on several devices (an ``EmbedderPool`` batch):
+        ``parts`` = [(global rows: host i64 [m], vecs: f32 [m, dim] on any GPU)].  Each part's
+        rows go straight to their shards: a shard on the part's own device takes its subset
+        in place (no copy at all when the pool member and the shard share the GPU, the
+        common case), any other shard gets only its subset copied over.  Synchronous per
+        shard device, like ``upsert_rows``."""
+        touched = set()
+        for rows, vecs in parts:
+            rows = torch.as_tensor(rows, dtype=torch.int64).cpu().reshape(-1)
+            if rows.numel() == 0:
+                continue
+            if vecs.dim() != 2 or vecs.shape[0] != rows.numel() or vecs.shape[1] != self.dim:
+                raise ValueError("each part needs vecs [len(rows), dim]")
+            if int(rows.min()) < 0 or int(rows.max()) // self.n >= self.capacity_per_shard:
+                raise ValueError("row out of capacity")
+            sh = torch.remainder(rows, self.n)
+            for s in torch.unique(sh).tolist():
+                sel = torch.nonzero(sh == s).reshape(-1)
+                d = self.devices[s]
+                v = vecs if sel.numel() == rows.numel() else vecs[sel.to(vecs.device)]
+                with torch.cuda.device(d):
+                    v = v.to(device=torch.device("cuda", d), dtype=torch.float32).contiguous()
+                    self._shards[s].upsert_rows(v, torch.div(rows[sel], self.n, rounding_mode="floor"))
+                touched.add(d)
+        for d in touched:
+            torch.cuda.synchronize(d)
+
     def fetch_rows(self, rows, stored: bool = False) -> torch.Tensor:
         """Host f32 [n, dim]: the upserted values (or, ``stored``, the normalised stored rows)."""
         rows = torch.as_tensor(rows, dtype=torch.int64).cpu().contiguous()
@@ -388,6 +416,11 @@ class Index:
         self._ids: list[str] = []
         self._meta: dict[str, dict] = {}
         self._mu = threading.Lock()
+        # values the last query(include_values=True) fetched, valid until the next upsert: the
+        # reference's search (retriever/utils.py:62-64) asks for values and its caller then
+        # fetches the same ids (retriever/main.py:142) — each row leaves the GPU once
+        self._gen = 0
+        self._recent: tuple[int, dict[str, list[float]]] = (-1, {})
 
     @property
     def shard_set(self) -> ShardSet:
@@ -400,6 +433,11 @@ class Index:
     @property
     def capacity(self) -> int:
         return self._set.capacity
+
+    @property
+    def shard_devices(self) -> list[int]:
+        """GPU of each shard (global row g lives on shard g % len(shard_devices))."""
+        return list(self._set.devices)
 
     def __len__(self) -> int:
         return len(self._ids)
@@ -446,10 +484,15 @@ class Index:
             self._upsert_locked(items, vecs)
         return {"upserted_count": len(items)}
 
-    def upsert_tensor(self, ids: Sequence[str], vecs: torch.Tensor, metadata: Sequence[dict] | None = None) -> dict:
+    def upsert_tensor(self, ids: Sequence[str], vecs, metadata: Sequence[dict] | None = None) -> dict:
         """Batched upsert of device-resident vectors (the ingest path: embeddings never leave HBM).
 
-        Same semantics as ``upsert`` (overwrite by id, last occurrence wins)."""
+        ``vecs``: f32 [len(ids), dimension] on a GPU, or a list of parts ``(positions,
+        tensor)`` — the vectors of ``ids[positions]`` on whatever GPU produced them (an
+        ``EmbedderPool`` batch): each goes straight to its shard's GPU.  Same semantics as
+        ``upsert`` (overwrite by id, last occurrence wins)."""
+        if isinstance(vecs, (list, tuple)):
+            return self._upsert_parts(ids, vecs, metadata)
         if vecs.dim() != 2 or vecs.shape[0] != len(ids) or vecs.shape[1] != self.dimension:
             raise ValueError("vecs must be [len(ids), dimension]")
         metadata = list(metadata) if metadata is not None else [{}] * len(ids)
@@ -471,19 +514,71 @@ class Index:
             self._upsert_locked(items, vecs)
         return {"upserted_count": len(items)}
 
-    def _upsert_locked(self, items, vecs: torch.Tensor) -> None:
-        new = sum(1 for vid, _, _ in items if vid not in self._rows)
-        self._ensure_capacity(len(self._ids) + new)
-        rows = []
-        for vid, _, md in items:
+    def _upsert_parts(self, ids, parts, metadata) -> dict:
+        metadata = list(metadata) if metadata is not None else [{}] * len(ids)
+        if len(metadata) != len(ids):
+            raise ValueError("metadata and ids differ in length")
+        where: dict[int, tuple[int, int]] = {}  # position -> (part, offset)
+        for pi, (pos, t) in enumerate(parts):
+            pos = [int(p) for p in pos]
+            if t.dim() != 2 or t.shape[0] != len(pos) or t.shape[1] != self.dimension:
+                raise ValueError("each part needs vectors [len(positions), dimension]")
+            for o, p in enumerate(pos):
+                where[p] = (pi, o)
+        if sorted(where) != list(range(len(ids))):
+            raise ValueError("the parts must cover every position of ids exactly once")
+        last: dict[str, int] = {}
+        for i, vid in enumerate(ids):
+            if not isinstance(vid, str) or not vid:
+                raise ValueError("vector id must be a non-empty string")
+            last[vid] = i
+        keep = list(last.values())
+        for _, t in parts:
+            if t.shape[0] and not bool((t != 0).any(dim=1).all()):
+                raise ValueError("Dense vectors must contain at least one non-zero value for the cosine metric")
+        items = [(ids[i], None, dict(metadata[i] or {})) for i in keep]
+        with self._mu:
+            rows = self._plan_rows(items)
+            sel = [[] for _ in parts]  # per part: (offset, global row) of the kept positions
+            for i, r in zip(keep, rows):
+                pi, o = where[i]
+                sel[pi].append((o, r))
+            out = []
+            for (pos, t), lst in zip(parts, sel):
+                if not lst:
+                    continue
+                offs = torch.tensor([o for o, _ in lst], dtype=torch.int64)
+                v = t if len(lst) == t.shape[0] and offs.tolist() == list(range(t.shape[0])) else t[offs.to(t.device)]
+                out.append((torch.tensor([r for _, r in lst], dtype=torch.int64), v))
+            self._set.upsert_parts(out)  # raises before anything below registers the ids
+            self._commit_rows(items, rows)
+        return {"upserted_count": len(items)}
+
+    def _plan_rows(self, items) -> list[int]:
+        """Row of each (deduplicated) item: its existing row, or the next free rows; grows the
+        shards if needed.  Registers nothing (see _commit_rows)."""
+        rows, nxt = [], len(self._ids)
+        for vid, _, _ in items:
             r = self._rows.get(vid)
             if r is None:
-                r = len(self._ids)
+                r, nxt = nxt, nxt + 1
+            rows.append(r)
+        self._ensure_capacity(nxt)
+        return rows
+
+    def _commit_rows(self, items, rows) -> None:
+        for (vid, _, md), r in zip(items, rows):
+            if vid not in self._rows:
                 self._rows[vid] = r
                 self._ids.append(vid)
-            rows.append(r)
             self._meta[vid] = md
+        self._gen += 1
+
+    def _upsert_locked(self, items, vecs: torch.Tensor) -> None:
+        # device write first: if it raises, no id is registered (no zero rows behind live ids)
+        rows = self._plan_rows(items)
         self._set.upsert_rows(vecs, rows)
+        self._commit_rows(items, rows)
 
     def query(self, vector=None, top_k: int = 10, include_values: bool = False, include_metadata: bool = False,
               id: str | None = None, namespace: str = "", **_: Any) -> dict:
@@ -528,9 +623,12 @@ class Index:
         scores = scores.cpu().tolist()
         rows = rows.cpu().tolist()
         out = []
+        recent: dict[str, list[float]] = {}
         for sq, rq in zip(scores, rows):
             sel = [(s, r) for s, r in zip(sq, rq) if r >= 0]
             vals = self._set.fetch_rows([r for _, r in sel]).tolist() if include_values and sel else None
+            if vals is not None:
+                recent.update((self._ids[r], v) for (_, r), v in zip(sel, vals))
             matches = []
             for j, (s, r) in enumerate(sel):
                 m = {"id": self._ids[r], "score": float(s)}
@@ -540,14 +638,20 @@ class Index:
                     m["metadata"] = dict(self._meta.get(self._ids[r], {}))
                 matches.append(m)
             out.append(matches)
+        if include_values:
+            self._recent = (self._gen, recent)
         return out
 
     def fetch(self, ids: Sequence[str], namespace: str = "") -> dict:
         with self._mu:
             found = [(i, self._rows[i]) for i in ids if i in self._rows]
             vectors = {}
-            if found:
+            gen, recent = self._recent
+            if found and gen == self._gen and all(i in recent for i, _ in found):
+                vals = [list(recent[i]) for i, _ in found]  # fetched by the query just before: no second device read
+            elif found:
                 vals = self._set.fetch_rows([r for _, r in found]).tolist()
+            if found:
                 for (vid, _), v in zip(found, vals):
                     vectors[vid] = {"id": vid, "values": v, "metadata": dict(self._meta.get(vid, {}))}
         return {"vectors": vectors, "namespace": namespace}

@@ -20,7 +20,9 @@ deployment passes an object that uploads and signs.
 from __future__ import annotations
 
 import sys
+import threading
 import uuid
+from contextlib import contextmanager
 from typing import Callable, Iterable, Iterator, Sequence
 
 from fastapi import HTTPException
@@ -78,6 +80,21 @@ def _prepare(files: Sequence[tuple]):
     return names, blobs, ctypes_, exts, images
 
 
+def _embed_for(embedder, images, index):
+    """The batch's vectors in the form ``Index.upsert_tensor`` takes: one device tensor, or with
+    an ``EmbedderPool`` the per-GPU slices, each image embedded on the GPU of the shard its new
+    row will live on (rows are taken in order from len(index), global row g on shard g % S), so
+    the vectors go from the embedding straight into that shard.  A concurrent ingest can shift
+    the rows; the index then copies the few vectors that landed elsewhere."""
+    from ..vit import EmbedderPool
+
+    if isinstance(embedder, EmbedderPool):
+        assign = embedder.assign(len(images), base=len(index), shard_devices=getattr(index, "shard_devices", None))
+        return [(pos, r) for pos, r, _ in embedder.embed_parts(images, normalized=False, assign=assign)]
+    raw, _ = embedder.embed_images(images)
+    return raw
+
+
 def _finish(prep, index, storage: StorageHook, id_factory: Callable[[], str]) -> list[dict]:
     """Embed the decoded batch, then ids, storage hook and ONE upsert (ingesting/main.py:124-168)."""
     from ..embedding import main as emb
@@ -85,15 +102,15 @@ def _finish(prep, index, storage: StorageHook, id_factory: Callable[[], str]) ->
     names, blobs, ctypes_, exts, images = prep
     if not blobs:
         return []
-    raw, _ = emb.get_embedder().embed_images(images)
+    index = index() if callable(index) else index
+    vecs = _embed_for(emb.get_embedder(), images, index)
     ids = [id_factory() for _ in blobs]
     paths = [f"images/{fid}.{ext}" for fid, ext in zip(ids, exts)]
     urls = []
     for p, data, ct, name in zip(paths, blobs, ctypes_, names):
         storage.upload(p, data, ct)
         urls.append(storage.signed_url(p, name))
-    index = index() if callable(index) else index
-    index.upsert_tensor(ids, raw, [{"gcs_path": p, "filename": n} for p, n in zip(paths, names)])
+    index.upsert_tensor(ids, vecs, [{"gcs_path": p, "filename": n} for p, n in zip(paths, names)])
     return [{"message": "Successfully!", "file_id": fid, "gcs_path": p, "signed_url": u}
             for fid, p, u in zip(ids, paths, urls)]
 
@@ -134,15 +151,36 @@ def ingest_stream(batches: Iterable[Sequence[tuple]], index, storage: StorageHoo
         return prep, ev
 
     it = iter(batches)
-    # both threads hold the GIL for short Python stretches between ctypes calls (which release
-    # it); at the default 5 ms switch interval each hand-off can stall the other thread for
-    # that long (tools/ingest_probe.py: 17.1k images/s at 5 ms, 18.4k at 1 ms)
-    old_switch = sys.getswitchinterval()
-    sys.setswitchinterval(min(old_switch, 1e-3))
-    try:
+    with _short_gil_switch():
         yield from _pipeline(it, prepare, main, index, storage, id_factory)
+
+
+_switch_lock = threading.Lock()
+_switch_users = 0
+_switch_saved = None
+
+
+@contextmanager
+def _short_gil_switch():
+    """GIL switch interval <= 1 ms while any ingest stream runs.  Both pipeline threads hold
+    the GIL for short Python stretches between ctypes calls (which release it); at the
+    default 5 ms each hand-off can stall the other thread that long (tools/ingest_probe.py:
+    17.1k images/s at 5 ms, 18.4k at 1 ms).  Process-wide setting, so it is reference-
+    counted: the first stream lowers it, the last one to finish (or be closed / collected)
+    restores the value it found."""
+    global _switch_users, _switch_saved
+    with _switch_lock:
+        if _switch_users == 0:
+            _switch_saved = sys.getswitchinterval()
+            sys.setswitchinterval(min(_switch_saved, 1e-3))
+        _switch_users += 1
+    try:
+        yield
     finally:
-        sys.setswitchinterval(old_switch)
+        with _switch_lock:
+            _switch_users -= 1
+            if _switch_users == 0:
+                sys.setswitchinterval(_switch_saved)
 
 
 def _pipeline(it, prepare, main, index, storage, id_factory):

@@ -16,14 +16,11 @@ OTel/Prometheus instrumentation is out of scope.
 """
 from __future__ import annotations
 
-from email.parser import BytesParser
-from email.policy import HTTP
-
 from fastapi import FastAPI, Request
 from fastapi.exceptions import RequestValidationError
 
 from ..config import Config
-from ..multipart import parse_form
+from ..multipart import parse_form, parse_form_all
 from . import core
 from .utils import embed_locally, get_index
 from .utils import get_feature_vector as _remote_feature_vector
@@ -63,13 +60,7 @@ async def push_image(request: Request):
 
 @app.post("/push_images")
 async def push_images(request: Request):
-    ctype = request.headers.get("content-type", "")
-    if not ctype.lower().startswith("multipart/form-data"):
+    parts = parse_form_all(await request.body(), request.headers.get("content-type", "")).get("files")
+    if not parts:
         raise _missing_file("files")
-    msg = BytesParser(policy=HTTP).parsebytes(b"Content-Type: " + ctype.encode("latin-1") + b"\r\n\r\n" +
-                                              await request.body())
-    files = [(p.get_filename(), p.get_payload(decode=True) or b"", p.get_content_type()) for p in msg.iter_parts()
-             if p.get_param("name", header="content-disposition") == "files"]
-    if not files:
-        raise _missing_file("files")
-    return core.ingest_many(files, index, storage=storage)
+    return core.ingest_many([(f.filename, f.data, f.content_type) for f in parts], index, storage=storage)

@@ -36,6 +36,11 @@ class ShardedIndex:
         self.host_exchange = dist.is_initialized() and dist.get_backend(group) == "gloo"
         self.dim = int(dim)
         self.capacity = int(capacity_per_rank)
+        # global rows key the cross-rank merge in 32 bits (merge_lists_kernel): the last
+        # global row, (capacity - 1) * world + rank, must stay below 2^32 - 1
+        if self.capacity < 1 or (self.capacity - 1) * self.world + self.world - 1 >= (1 << 32) - 1:
+            raise ValueError(f"capacity_per_rank x world = {self.capacity} x {self.world} exceeds the 2^32 - 1 "
+                             "global rows the top-k merge can key")
         if backend_factory is None:
             from .index import DeviceIndex, topk_merge
 
@@ -45,6 +50,7 @@ class ShardedIndex:
         self.local = backend_factory()
         self.merge = merge_fn
         self.n_rows = 0  # global rows [0, n_rows) hold data (the same value on every rank)
+        self.written = 0  # local rows [0, written) of this rank's shard hold data (high-water mark)
 
     @property
     def n_local(self) -> int:
@@ -64,23 +70,58 @@ class ShardedIndex:
         mine = self.owner(gr) == self.rank
         if bool(mine.any()):
             idx = torch.nonzero(mine).reshape(-1)
-            self.local.upsert_rows(vecs[idx.to(vecs.device)], torch.div(gr[idx], self.world, rounding_mode="floor"))
+            loc = torch.div(gr[idx], self.world, rounding_mode="floor")
+            self.local.upsert_rows(vecs[idx.to(vecs.device)], loc)
+            self.written = max(self.written, int(loc.max()) + 1)
         self.n_rows = max(self.n_rows, int(gr.max()) + 1)
         return int(mine.sum())
 
     def upsert_local(self, vecs: torch.Tensor, local_rows: torch.Tensor) -> None:
         """Rank-local ingest (data-parallel embed → own shard, no collective): vecs go to this
-        rank's local rows, i.e. global rows local * W + rank.  Call ``set_rows`` once every
-        rank has ingested to publish the global row count."""
-        self.local.upsert_rows(vecs, local_rows)
+        rank's local rows, i.e. global rows local * W + rank.  Rows are checked against the
+        shard's capacity on the host (one small device→host read when they live on the GPU).
+        Call ``publish_rows`` (or ``set_rows``) once every rank has ingested."""
+        lr = torch.as_tensor(local_rows)
+        if lr.numel() == 0:
+            return
+        lo, hi = (int(v) for v in torch.aminmax(lr.reshape(-1)))
+        if lo < 0 or hi >= self.capacity:
+            raise ValueError(f"local rows [{lo}, {hi}] outside the shard's capacity {self.capacity}")
+        self.local.upsert_rows(vecs, lr)
+        self.written = max(self.written, hi + 1)
+
+    def _rows_ok(self, n_rows: int) -> bool:
+        return (n_rows - self.rank + self.world - 1) // self.world <= self.written if n_rows > self.rank else True
 
     def set_rows(self, n_rows: int) -> None:
-        self.n_rows = int(n_rows)
+        """Publish the global row count (the same value on every rank).  Raises if this rank's
+        part of [0, n_rows) reaches past the local rows it has written: those slots are
+        zero rows that would score 0 and come back as matches with ids that do not exist."""
+        n_rows = int(n_rows)
+        if n_rows < 0 or not self._rows_ok(n_rows):
+            raise ValueError(f"rank {self.rank} has written {self.written} local rows: global rows [0, {n_rows}) "
+                             f"need {(n_rows - self.rank + self.world - 1) // self.world}")
+        self.n_rows = n_rows
+
+    def publish_rows(self) -> int:
+        """Collective: the largest global row count every rank's shard covers, from the ranks'
+        written counts (rank r holds global rows r, r + W, ...: n_rows = min_r written_r·W + r),
+        set on every rank and returned.  Ranks that ingested different counts stay consistent."""
+        if self.world == 1:
+            self.n_rows = self.written
+            return self.n_rows
+        dev = "cpu" if self.host_exchange else self.local.device
+        t = torch.tensor([self.written], dtype=torch.int64, device=dev)
+        allw = torch.empty((self.world,), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allw, t, group=self.group)
+        self.n_rows = min(int(w) * self.world + r for r, w in enumerate(allw.cpu().tolist()))
+        return self.n_rows
 
     def fill_random(self, seed: int, n_local: int) -> None:
         """Synthetic shard (benchmarks): every rank fills n_local rows, so the index holds
         n_local * W global rows."""
         self.local.fill_random(seed, 0, n_local)
+        self.written = max(self.written, int(n_local))
         self.n_rows = n_local * self.world
 
     def search(self, queries: torch.Tensor, k: int, **kw):
@@ -133,6 +174,7 @@ class ShardedIndex:
         self.n_rows = int(man["n_rows"])
         if self.n_local:
             self.local.import_rows(0, torch.from_numpy(rows), torch.from_numpy(norms))
+        self.written = self.n_local
 
     def close(self) -> None:
         close = getattr(self.local, "close", None)

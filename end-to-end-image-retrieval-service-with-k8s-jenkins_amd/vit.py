@@ -21,7 +21,7 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 from .config import VIT_MSN_BASE, VIT_MSN_PREPROCESS
 
-TIMER_IDS = {"gemm": 0, "fc1": 1, "attention": 2, "layernorm": 3, "preprocess": 4}
+TIMER_IDS = {"gemm": 0, "fc1": 1, "attention": 2, "layernorm": 3, "preprocess": 4, "qkv": 5, "oproj": 6, "fc2": 7}
 
 
 def _to_f32_numpy(t) -> np.ndarray:
@@ -69,6 +69,72 @@ def load_checkpoint_dir(path: str) -> tuple[dict, dict, dict]:
     return dict(sd), cfg, pre
 
 
+# transformers-5 module names → the checkpoint (legacy) layout rc_model_set_weight keys on
+# (TR/conversion_mapping.py maps ViTMSNModel to the ViTModel rules); the same table as
+# canonical_name() in csrc/vit.hip
+_V5_RENAMES = (
+    ("attention.q_proj", "attention.attention.query"), ("attention.k_proj", "attention.attention.key"),
+    ("attention.v_proj", "attention.attention.value"), ("attention.o_proj", "attention.output.dense"),
+    ("mlp.fc1", "intermediate.dense"), ("mlp.fc2", "output.dense"),
+)
+# checkpoint entries that are not part of the embedding model (ViTMSNForImageClassification's
+# head, the masked-pretraining token)
+_IGNORED_KEYS = ("classifier.", "vit.classifier.")
+_IGNORED_SUFFIXES = ("mask_token",)
+
+
+def canonical_key(name: str) -> str:
+    n = name[4:] if name.startswith("vit.") else name
+    if n.startswith("layers."):
+        n = "encoder.layer." + n[len("layers."):]
+    for a, b in _V5_RENAMES:
+        if a in n:
+            n = n.replace(a, b, 1)
+            break
+    return n
+
+
+def expected_keys(num_layers: int) -> set[str]:
+    """Every tensor ViTMSNModel's state dict holds (legacy layout, embedding/main.py:37-38)."""
+    keys = {"embeddings.cls_token", "embeddings.position_embeddings", "embeddings.patch_embeddings.projection.weight",
+            "embeddings.patch_embeddings.projection.bias", "layernorm.weight", "layernorm.bias"}
+    for i in range(num_layers):
+        p = f"encoder.layer.{i}."
+        for nm in ("query", "key", "value"):
+            keys |= {p + f"attention.attention.{nm}.weight", p + f"attention.attention.{nm}.bias"}
+        for nm in ("attention.output.dense", "intermediate.dense", "output.dense"):
+            keys |= {p + nm + ".weight", p + nm + ".bias"}
+        for nm in ("layernorm_before", "layernorm_after"):
+            keys |= {p + nm + ".weight", p + nm + ".bias"}
+    return keys
+
+
+def canonical_state_dict(state_dict: Mapping, num_layers: int | None = None) -> dict:
+    """A checkpoint's tensors under the legacy key layout: accepts the legacy names, the
+    transformers-5 names (``layers.N.attention.q_proj`` …) and a ``vit.`` prefix; drops the
+    classifier head and mask token; raises ValueError on any other unknown key, on a
+    missing key and on a key that two names map to."""
+    out: dict = {}
+    for name, t in state_dict.items():
+        if name.startswith(_IGNORED_KEYS) or name.endswith(_IGNORED_SUFFIXES):
+            continue
+        k = canonical_key(name)
+        if k in out:
+            raise ValueError(f"checkpoint holds {k!r} twice (as {name!r} and another name)")
+        out[k] = t
+    if num_layers is None:
+        num_layers = sum(1 for k in out if k.endswith("layernorm_before.weight"))
+    want = expected_keys(num_layers)
+    unknown = sorted(set(out) - want)
+    missing = sorted(want - set(out))
+    if unknown:
+        raise ValueError(f"unknown checkpoint keys (not a ViT-MSN state dict?): {unknown[:8]}"
+                         + (" …" if len(unknown) > 8 else ""))
+    if missing:
+        raise ValueError(f"checkpoint is missing {len(missing)} tensors, e.g. {missing[:8]}")
+    return out
+
+
 def _packed_view(ims: Sequence, device) -> "torch.Tensor | None":
     """[n, H, W, 3] view when ``ims`` are equal-size contiguous u8 device tensors lying back to
     back in one buffer (what JpegDecoder.decode returns for a chunk), else None."""
@@ -96,6 +162,7 @@ class VitMsnEmbedder:
         cfg.update(model_config or {})
         if model_config is None:
             cfg["num_hidden_layers"] = sum(1 for k in state_dict if k.endswith("layernorm_before.weight"))
+        state_dict = canonical_state_dict(state_dict, cfg["num_hidden_layers"])  # key errors before any GPU work
         self.config = cfg
         self.preprocess_params = dict(VIT_MSN_PREPROCESS)
         self.preprocess_params.update(preprocess or {})
@@ -113,8 +180,6 @@ class VitMsnEmbedder:
         self._h = h
         try:
             for name, t in state_dict.items():
-                if name.endswith("mask_token") or name.startswith("classifier"):
-                    continue
                 a = _to_f32_numpy(t)
                 check(self.lib.rc_model_set_weight(self._h, name.encode(), a.ctypes.data, a.size))
             p = self.preprocess_params
@@ -296,6 +361,139 @@ class VitMsnEmbedder:
         w = _lib.C.c_double()
         check(self.lib.rc_model_timing_read(self._h, TIMER_IDS[kernel], _lib.C.byref(ms), _lib.C.byref(n), _lib.C.byref(w)))
         return ms.value, n.value, w.value
+
+
+class EmbedderPool:
+    """Data-parallel embedding over several GPUs in one process: one ``VitMsnEmbedder``
+    (``rc_model``) per device, weights replicated, no collectives (image
+    embedding is plain data parallel).  The reference scales its embedding pod by
+    replicas behind one Service (``helm_charts/embedding/values.yaml:1``); here a
+    batch is split over the pool's GPUs, which run their ``rc_embed`` calls concurrently
+    (each call returns once its kernels are queued).
+
+    ``embed_images`` returns the vectors gathered on the first device (the /embed body);
+    ``embed_parts`` leaves each slice on the GPU that embedded it, so an ingest can hand
+    the slices straight to the index shards on those GPUs (``Index.upsert_tensor`` with
+    parts).  Devices may repeat (two models on one GPU: the parity test)."""
+
+    def __init__(self, state_dict: Mapping, devices: Sequence, max_batch: int = 32, model_config: dict | None = None,
+                 preprocess: dict | None = None):
+        if not devices:
+            raise ValueError("an embedder pool needs at least one device")
+        self.members: list[VitMsnEmbedder] = []
+        try:
+            for d in devices:
+                self.members.append(VitMsnEmbedder(state_dict, device=d, max_batch=max_batch,
+                                                   model_config=model_config, preprocess=preprocess))
+        except Exception:
+            self.close()
+            raise
+        lead = self.members[0]
+        self.device, self.hidden, self.max_batch, self.config = lead.device, lead.hidden, lead.max_batch, lead.config
+        self.preprocess_params = lead.preprocess_params
+
+    @classmethod
+    def from_pretrained(cls, path: str, devices: Sequence, max_batch: int = 32) -> "EmbedderPool":
+        sd, cfg, pre = load_checkpoint_dir(path)
+        return cls(sd, devices, max_batch=max_batch, model_config=cfg, preprocess=pre)
+
+    @property
+    def devices(self) -> list[int]:
+        return [m.device.index for m in self.members]
+
+    def close(self) -> None:
+        for m in getattr(self, "members", []):
+            m.close()
+
+    def assign(self, n: int, base: int = 0, shard_devices: Sequence[int] | None = None) -> list[int]:
+        """Member of each of n images.  With ``shard_devices`` (an index's shard GPUs, global row
+        g on shard g % S) image j, which will take row base + j, goes to a member on the GPU of
+        its shard, so its vector never leaves that GPU; otherwise round-robin."""
+        D = len(self.members)
+        if not shard_devices:
+            return [(base + j) % D for j in range(n)]
+        if [int(d) for d in shard_devices] == self.devices:  # one member per shard, same GPUs
+            return [(base + j) % D for j in range(n)]
+        by_dev: dict[int, list[int]] = {}
+        for i, m in enumerate(self.members):
+            by_dev.setdefault(m.device.index, []).append(i)
+        S = len(shard_devices)
+        seen: dict[int, int] = {}
+        out = []
+        for j in range(n):
+            s = (base + j) % S
+            cands = by_dev.get(int(shard_devices[s]))
+            if cands:  # several members on this GPU: take turns
+                k = seen.get(s, 0)
+                seen[s] = k + 1
+                out.append(cands[k % len(cands)])
+            else:
+                out.append((base + j) % D)
+        return out
+
+    def embed_parts(self, images: Sequence, normalized: bool = True, assign: Sequence[int] | None = None):
+        """[(positions, raw [m, H], normed [m, H] or None)] per member that got images, each on
+        its member's GPU (queued on that GPU's current stream; no host synchronisation)."""
+        n = len(images)
+        assign = list(assign) if assign is not None else self.assign(n)
+        if len(assign) != n:
+            raise ValueError("assign needs one member per image")
+        out = []
+        for mi, m in enumerate(self.members):
+            pos = [j for j in range(n) if assign[j] == mi]
+            if not pos:
+                continue
+            with torch.cuda.device(m.device):
+                r, nr = m.embed_images([images[j] for j in pos], normalized=normalized)
+            out.append((pos, r, nr))
+        return out
+
+    def embed_images(self, images: Sequence, normalized: bool = False, assign: Sequence[int] | None = None):
+        """Same contract as ``VitMsnEmbedder.embed_images``: (raw, normed or None) on the first
+        device, input order; the batch is embedded over every member concurrently."""
+        n = len(images)
+        raw = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device)
+        nrm = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device) if normalized else None
+        for pos, r, nr in self.embed_parts(images, normalized=normalized, assign=assign):
+            sel = torch.tensor(pos, dtype=torch.int64, device=self.device)
+            raw.index_copy_(0, sel, r.to(self.device))
+            if normalized:
+                nrm.index_copy_(0, sel, nr.to(self.device))
+        return raw, nrm
+
+    def embed(self, images_u8: torch.Tensor, normalized: bool = True, stream=None, out=None):
+        """u8 [n,h,w,3] → (raw, normed) on the first device, slices embedded on every member."""
+        if out is not None or stream is not None:
+            raise ValueError("EmbedderPool.embed: out / stream are per-member; use embed_parts")
+        return self.embed_images(list(images_u8.unbind(0)), normalized=normalized)
+
+    def embed_pil(self, images: Sequence) -> list[list[float]]:
+        raw, _ = self.embed_images([np.asarray(im.convert("RGB"), dtype=np.uint8) for im in images])
+        return raw.cpu().tolist()
+
+    def decode_jpeg(self, datas: Sequence[bytes]) -> list[torch.Tensor]:
+        """Decoded on the first member's GPU (the host Huffman pass is the shared cost; the
+        slices move to their members inside embed_parts, 150 KB per 224x224 image)."""
+        return self.members[0].decode_jpeg(datas)
+
+    def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
+        raw, _ = self.embed_images(self.decode_jpeg(datas))
+        return raw.cpu().tolist()
+
+    def preprocess(self, images_u8: torch.Tensor, stream=None) -> torch.Tensor:
+        return self.members[0].preprocess(images_u8, stream=stream)
+
+    def set_parts(self, parts: int) -> None:
+        for m in self.members:
+            m.set_parts(parts)
+
+    def set_ln_fold(self, on: bool) -> None:
+        for m in self.members:
+            m.set_ln_fold(on)
+
+    def set_last_layer(self, cls_only: bool) -> None:
+        for m in self.members:
+            m.set_last_layer(cls_only)
 
 
 def gflop_per_image(cfg: dict = VIT_MSN_BASE, cls_only_last: bool = False) -> float:

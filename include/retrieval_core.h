@@ -54,6 +54,10 @@ typedef struct rc_model rc_model;
 
 const char *rc_last_error(void);
 int rc_abi_version(void);
+/* Device and pinned-host allocations the library has made so far (all handles).
+ * Diagnostic: the tests check that steady-state hot calls (search, fetch,
+ * upsert, embed once their workspaces exist) leave it unchanged. */
+int64_t rc_alloc_count(void);
 
 /* ------------------------------------------------------------------------
  * In-HBM exact cosine index.  Replaces the Pinecone index:
@@ -148,7 +152,8 @@ int rc_index_fill_random(rc_index *h, uint64_t seed, int64_t row0, int64_t n, vo
 /* Merge nlists top-k lists per query into one (cross-shard merge after the
  * all-gather; no reference counterpart — Pinecone merges server-side).
  * scores/rows: device [nlists, nq, k_in] of (score, global row); rows < 0 are
- * empty slots; global rows must be < 2^32.  Result ordered score desc, then
+ * empty slots; global rows must be < 2^32 - 1 (every rc_index row map is
+ * checked against that bound at create / set_row_map / grow).  Result ordered score desc, then
  * row asc — whatever the routing of rows to lists.  out: device [nq, k]. */
 int rc_topk_merge(const float *scores, const int64_t *rows, int nlists, int nq, int k_in, int k,
                   float *out_scores, int64_t *out_rows, void *stream);
@@ -237,8 +242,7 @@ int rc_model_set_parts(rc_model *m, int parts);
  * layer (modeling_vit_msn.py:254-283) reads only its own query row plus every
  * token's K/V: with cls_only = 1 the last layer runs LN1 + QKV on all rows, then
  * CLS-query attention, O-proj, LN2 and the MLP on the CLS rows alone.
- * cls_only = 0 runs the whole layer (A/B and parity tests).  Env override at
- * create: RC_EMBED_FULL_LAST=1. */
+ * cls_only = 0 runs the whole layer (A/B and parity tests). */
 int rc_model_set_last_layer(rc_model *m, int cls_only);
 
 /* LayerNorm fold (default 1): the two LayerNorms of each layer
@@ -250,8 +254,9 @@ int rc_model_set_last_layer(rc_model *m, int cls_only);
 int rc_model_set_ln_fold(rc_model *m, int on);
 
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
- * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM (dominant), 2 = attention,
- * 3 = layernorm, 4 = preprocess; `mask` bit i enables id i (-1 = all, 0 = off). */
+ * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM, 2 = attention, 3 = layernorm,
+ * 4 = preprocess, 5 = QKV GEMM, 6 = O-proj GEMM, 7 = fc2 GEMM (5-7 and 1: the
+ * full-batch launches of that projection); `mask` bit i enables id i (-1 = all, 0 = off). */
 int rc_model_timing(rc_model *m, int mask);
 int rc_model_timing_read(rc_model *m, int kernel_id, double *total_ms, int64_t *launches, double *flops);
 int rc_model_timing_reset(rc_model *m);
@@ -260,8 +265,8 @@ int rc_model_timing_reset(rc_model *m);
  * inside rc_embed this is every nn.Linear of modeling_vit_msn.py:199-202,243-244).
  * out = epilogue(A[M][K] · W[N][K]ᵀ + bias): epi 0 → bf16 out, 1 → bf16 GELU(out),
  * 2 → f32 out += (residual, in place), 3 → f32 patch scatter (+pos, tokens/image).
- * A must have round_up(M, 256) readable rows.  variant: 0 auto, 1 128x128 tiles,
- * 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256). */
+ * A must have round_up(M, 256) readable rows; N % 256 == 0 (M > 256), K % 64 == 0.
+ * variant: 0 auto, 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256). */
 int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N, int K,
                  void *out, const float *pos, int tokens, void *stream);
 

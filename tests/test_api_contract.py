@@ -208,6 +208,35 @@ def test_ingest_health_and_root(ingest_client):
     assert ingest_client.get("/").json() == {"message": "Welcome to the Image Ingestion API. Visit /docs to test."}
 
 
+def test_batched_routes_share_the_single_route_contract(client, ingest_client):
+    """/embed_batch and /push_images parse with the same parser as /embed and /push_image:
+    422 without the field or without a multipart body, 400 with the reference's detail for
+    a non-image (GPU-free: validation runs before the model)."""
+    assert client.post("/embed_batch").status_code == 422
+    assert client.post("/embed_batch", content=b"x", headers={"content-type": "text/plain"}).status_code == 422
+    assert client.post("/embed_batch", files=[("file", ("a.jpg", b"x", "image/jpeg"))]).status_code == 422
+    r = client.post("/embed_batch", files=[("files", ("a.txt", b"This is not an image at all.", "text/plain"))])
+    assert r.status_code == 400 and r.json() == {"detail": "Uploaded file is not a valid image."}
+    r = client.post("/embed", files={"file": ("a.txt", b"This is not an image at all.", "text/plain")})
+    assert r.status_code == 400 and r.json() == {"detail": "Uploaded file is not a valid image."}
+    assert ingest_client.post("/push_images", files=[("file", ("a.jpg", b"x", "image/jpeg"))]).status_code == 422
+    r = ingest_client.post("/push_images", files=[("files", ("a.jpg", b"This is not an image.", "image/jpeg"))])
+    assert r.status_code == 400 and r.json()["detail"] == "Invalid image file"
+
+
+def test_parse_form_all_keeps_repeated_fields():
+    mp = import_pkg("multipart")
+    from urllib3 import encode_multipart_formdata
+
+    body, ctype = encode_multipart_formdata([("files", ("a.jpg", b"A", "image/jpeg")), ("other", "x"),
+                                             ("files", ("b.png", b"BB", "image/png"))])
+    allf = mp.parse_form_all(body, ctype)
+    assert [(f.filename, f.data, f.content_type) for f in allf["files"]] == [("a.jpg", b"A", "image/jpeg"),
+                                                                             ("b.png", b"BB", "image/png")]
+    assert mp.parse_form(body, ctype)["files"].data == b"BB"  # one part per field: the last, as form.get
+    assert mp.parse_form_all(b"x", "text/plain") == {}
+
+
 def test_push_no_file(ingest_client):
     assert ingest_client.post("/push_image").status_code == 422
     assert ingest_client.post("/push_images").status_code == 422

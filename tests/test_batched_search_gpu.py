@@ -200,13 +200,15 @@ def test_recall_vs_unquantised_fp32_oracle(idxmod, cuda):
     f16.close()
 
 
-_QT4_SCRIPT = r"""
-import sys, torch
-sys.path.insert(0, {repo!r})
-from conftest import import_pkg
-idx = import_pkg("index")
-for dtype, dim, n, nq in (("float16", 512, 2_200_000, 700), ("bfloat16", 256, 90_000, 300), ("float16", 128, 20_000, 257)):
-    d = idx.DeviceIndex(dim, dtype=dtype, capacity=n, device=0)
+
+@pytest.mark.parametrize("dtype,dim,n,nq", [("float16", 512, 2_200_000, 700), ("bfloat16", 256, 90_000, 300),
+                                             ("float16", 128, 20_000, 257)])
+def test_mfma_equals_scan_sublaunches_and_query_blocks(idxmod, cuda, dtype, dim, n, nq):
+    """The batched path returns the scan's results bit for bit at ld 512 (NKT 8: several
+    query blocks and 2-GB filter sub-launches over 2.2M rows), 256 and 128."""
+    import torch
+
+    d = idxmod.DeviceIndex(dim, dtype=dtype, capacity=n, device=0)
     d.fill_random(11, 0, n)
     g = torch.Generator(device="cuda").manual_seed(12)
     q = torch.randn((nq, dim), device="cuda", generator=g)
@@ -214,22 +216,3 @@ for dtype, dim, n, nq in (("float16", 512, 2_200_000, 700), ("bfloat16", 256, 90
     s2, r2 = d.search(q, 50, n, mode="scan")
     assert torch.equal(r1, r2) and torch.equal(s1, s2), (dtype, dim)
     d.close()
-print("QT4-OK")
-"""
-
-
-def test_mfma_qt4_form_equals_scan(cuda):
-    """The 4-wave form of the filter (RC_FILTER_QT=4: query fragments in AGPRs, MFMAs by inline
-    asm with manual hazard waits; read once per process, hence a child process) returns the
-    scan's results bit for bit at ld 512 (NKT 8, several query blocks and sub-launch row
-    ranges), 256 and 128."""
-    import os
-    import subprocess
-    import sys
-
-    from conftest import REPO
-
-    env = dict(os.environ, RC_FILTER_QT="4")
-    out = subprocess.run([sys.executable, "-c", _QT4_SCRIPT.format(repo=os.path.join(REPO, "tests"))],
-                         env=env, capture_output=True, text=True, timeout=240, cwd=REPO)
-    assert out.returncode == 0 and "QT4-OK" in out.stdout, out.stderr[-2000:]

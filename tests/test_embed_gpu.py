@@ -153,7 +153,7 @@ def test_embed_full_batch_256_properties(vitmod, weights12, cuda):
 
 
 @pytest.mark.parametrize("parts", [2, 3, 4])
-def test_embed_split_streams_bitwise_equal(vitmod, cuda, parts, monkeypatch):
+def test_embed_split_streams_bitwise_equal(vitmod, cuda, parts):
     """A batch encoded as 2-4 concurrent parts on separate streams equals the one-stream result bit for bit."""
     import torch
 
@@ -162,11 +162,11 @@ def test_embed_split_streams_bitwise_equal(vitmod, cuda, parts, monkeypatch):
     sd = seeded_vit_msn_weights(1907, num_layers=2)
     rng = np.random.default_rng(parts)
     imgs = torch.from_numpy(rng.integers(0, 256, (250, 224, 224, 3), dtype=np.uint8))
-    monkeypatch.setenv("RC_EMBED_SPLIT", "1")
     m1 = vitmod.VitMsnEmbedder(sd, device=0, max_batch=250)
+    m1.set_parts(1)
     a, an = m1.embed(imgs)
-    monkeypatch.setenv("RC_EMBED_SPLIT", str(parts))
     mp = vitmod.VitMsnEmbedder(sd, device=0, max_batch=250)
+    mp.set_parts(parts)
     b, bn = mp.embed(imgs)
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(an, bn)
@@ -264,3 +264,34 @@ def test_embed_massive_activation_channels(vitmod, weights12, cuda):
         assert 1.0 - cosine(outs[True][i][keep], outs[False][i][keep]) <= 1e-4
     m.close()
 
+
+
+def test_from_pretrained_v5_layout_matches_golden(vitmod, cuda, tmp_path):
+    """VitMsnEmbedder.from_pretrained on a local checkpoint directory in the transformers-5 key
+    layout (config.json + model.safetensors: the offline stand-in for the reference's
+    from_pretrained("facebook/vit-msn-base"), embedding/main.py:37-38) embeds the committed
+    2-layer golden images like the seeded weights handed over directly."""
+    import json as _json
+
+    import torch
+    from safetensors.numpy import save_file
+
+    from oracle.weights import to_hf_v5
+
+    sd2 = seeded_vit_msn_weights(1907, num_layers=2)
+    d = tmp_path / "ckpt"
+    d.mkdir()
+    (d / "config.json").write_text(_json.dumps({"num_hidden_layers": 2, "hidden_size": 768}))
+    save_file({k: np.ascontiguousarray(v) for k, v in to_hf_v5(sd2).items()}, str(d / "model.safetensors"))
+    m = vitmod.VitMsnEmbedder.from_pretrained(str(d), device=0, max_batch=2)
+    direct = vitmod.VitMsnEmbedder(sd2, device=0, max_batch=2)
+    imgs = torch.from_numpy(np.load(os.path.join(GOLDEN, "synthetic_u8_2x224.npy")))
+    ref = np.load(os.path.join(GOLDEN, "synthetic_embedding_2layer_seed1907.npy"))
+    raw, _ = m.embed(imgs)
+    raw2, _ = direct.embed(imgs)
+    assert torch.equal(raw, raw2)
+    raw = raw.cpu().numpy()
+    for i in range(2):
+        assert 1.0 - cosine(raw[i], ref[i]) <= BF16_COS_TOL
+    m.close()
+    direct.close()

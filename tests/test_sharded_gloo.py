@@ -124,3 +124,61 @@ def test_sharded_search_equals_global_oracle(world, n):
         assert np.all(r[:, kk:] == -1) and np.all(np.isneginf(s[:, kk:]))
     if n > cap + 11:
         assert outs[0][4][0, :2].tolist() == [5, cap + 11]  # tie → lower global row first
+
+
+def _worker_local(rank, world, counts, port, result_q):
+    import sys
+
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sharded = import_pkg("sharded")
+        cap, dim, k = 300, 64, 5
+        idx = sharded.ShardedIndex(dim, capacity_per_rank=cap,
+                                   backend_factory=lambda: OracleShard(dim, cap, rank, world), merge_fn=cpu_merge)
+        X, Q = _data(world, cap * world)
+        mine = X[rank::world][:counts[rank]]  # rank r's local row j is global row j * W + r
+        idx.upsert_local(torch.from_numpy(mine), torch.arange(counts[rank]))
+        errors = []
+        try:
+            idx.upsert_local(torch.from_numpy(mine[:1]), torch.tensor([cap]))
+        except ValueError:
+            errors.append("capacity")
+        try:
+            idx.set_rows(world * (counts[rank] + 1))
+        except ValueError:
+            errors.append("set_rows")
+        n_rows = idx.publish_rows()
+        s, r = idx.search(torch.from_numpy(Q), k)
+        result_q.put((rank, n_rows, errors, s.numpy(), r.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,counts", [(2, (40, 37)), (4, (10, 12, 9, 11))])
+def test_rank_local_ingest_publishes_consistent_rows(world, counts):
+    """Data-parallel ingest (upsert_local per rank, no collective) with UNEVEN per-rank counts:
+    publish_rows agrees on the largest global range every shard covers (min_r written_r*W + r),
+    the search over it equals one exact index; out-of-capacity rows and an over-long set_rows
+    are rejected instead of exposing unwritten (zero) rows as matches."""
+    from oracle.cosine_topk import cosine_topk
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_local, args=(r, world, counts, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = min(c * world + r for r, c in enumerate(counts))
+    X, Q = _data(world, 300 * world)
+    ref_r, ref_s = cosine_topk(X[:want], Q, 5)
+    for rank, n_rows, errors, s, r in outs:
+        assert n_rows == want
+        assert errors == ["capacity", "set_rows"]
+        assert np.array_equal(r, ref_r)
+        assert np.allclose(s, ref_s, atol=1e-6)

@@ -229,3 +229,49 @@ def test_world2_real_shards_equal_single_index(idxmod, cuda, n):
     if n > 40:
         assert r_ref[0, :2].tolist() == [3, 40]
     single.close()
+
+
+def test_search_image_steady_state_allocates_nothing_and_fetches_once(cuda, monkeypatch):
+    """/search_image over a multi-shard index (reference retriever/main.py:104-169): once the
+    workspaces exist, a request makes no device / pinned allocation in the library
+    (rc_alloc_count), and the search's include_values fetch (retriever/utils.py:62-64)
+    serves the handler's fetch(ids) (retriever/main.py:142): each row is read from the GPU
+    once per request."""
+    import io
+
+    from fastapi.testclient import TestClient
+    from PIL import Image
+
+    L = import_pkg("_lib")
+    lib = L.load()
+    utils = import_pkg("ingesting.utils")
+    main = import_pkg("retriever.main")
+    idxmod = import_pkg("index")
+    monkeypatch.setattr(utils.Config, "INDEX_SHARDS", 3)
+    ix = utils.get_index("alloc-free-search", capacity=64)
+    monkeypatch.setattr(main, "index", lambda: ix)
+    rng = np.random.default_rng(8)
+    imgs = [rng.integers(0, 256, (224, 224, 3), dtype=np.uint8) for _ in range(6)]
+    blobs = []
+    for a in imgs:
+        b = io.BytesIO()
+        Image.fromarray(a).save(b, format="PNG")
+        blobs.append(b.getvalue())
+    for i, b in enumerate(blobs):
+        ix.upsert([(f"img-{i}", main.get_feature_vector(b), {"gcs_path": f"images/img-{i}.png"})])
+    client = TestClient(main.app)
+    fetches = []
+    real_fetch = idxmod.ShardSet.fetch_rows
+    monkeypatch.setattr(idxmod.ShardSet, "fetch_rows",
+                        lambda self, rows, stored=False: fetches.append(len(rows)) or real_fetch(self, rows, stored))
+    first = client.post("/search_image", files={"file": ("q.png", blobs[2], "image/png")})
+    assert first.status_code == 200 and first.json()[0].endswith("images/img-2.png")
+    client.post("/search_image", files={"file": ("q.png", blobs[3], "image/png")})  # warm
+    fetches.clear()
+    n0 = lib.rc_alloc_count()
+    for b in blobs:
+        r = client.post("/search_image", files={"file": ("q.png", b, "image/png")})
+        assert r.status_code == 200 and len(r.json()) == 5
+    assert lib.rc_alloc_count() == n0
+    assert fetches == [5] * len(blobs)  # one device fetch of the 5 matches per request
+    ix.close()

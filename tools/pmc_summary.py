@@ -64,10 +64,12 @@ def main():
     if "--json" in sys.argv:
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
     if "--latest" in sys.argv:
-        # fc1 is EPI_GELU_BF16_LN (5) with LayerNorm folded (default), EPI_GELU_BF16 (1) without
-        keys = {"fc1": ("gemm_pp_kernel<5, 0>", "gemm_pp_kernel<1, 0>"),
+        # the model's projections (LayerNorm folded, bf16-pair residual stream): EPI 4 QKV,
+        # 5 fc1, 6 O-proj (NKT 12) / fc2 (NKT 48)
+        keys = {"fc1": ("gemm_pp_kernel<5, 0, 12>",), "qkv": ("gemm_pp_kernel<4, 0, 12>",),
+                "oproj": ("gemm_pp_kernel<6, 0, 12>",), "fc2": ("gemm_pp_kernel<6, 0, 48>",),
                 "scan_f16": ("scan_topk_kernel<f16_t, 4, 1, 128>",),
-                "filter_f16": ("filter_qs_kernel<f16_t, 8, 2, 0>", "filter_qs_kernel<f16_t, 8, 4, 0>")}
+                "filter_f16": ("filter_qs_kernel<f16_t, 8, 0>",)}
         latest = {}
         for key, knames in keys.items():
             kname = next((k for k in knames if any(r["kernel"] == k for r in out.values())), knames[0])
