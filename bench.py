@@ -107,17 +107,36 @@ def torch_vit_forward(sd):
     return forward
 
 
+def _cgroup_cpu_quota():
+    """CPUs the job's cgroup may use (cgroup v2 cpu.max / v1 cfs quota), or None if unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // p)
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores() -> dict:
-    """The cores this process may run on (affinity / cgroup cpuset), which is what the CPU
-    baselines use: torch's intra-op pool is set to that count explicitly."""
+    """The cores this job may use: the smallest of its CPU affinity, its cgroup CPU quota and
+    OMP_NUM_THREADS (the GPU box sets 16 per GPU; affinity and os.cpu_count() show the whole
+    machine there).  The CPU baselines run torch's intra-op pool at exactly that count."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    return {"affinity": aff, "os_cpu_count": os.cpu_count()}
+    quota = _cgroup_cpu_quota()
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    use = min(x for x in (aff, quota, omp) if x)
+    return {"use": use, "affinity": aff, "cgroup_quota": quota, "omp_num_threads": omp, "os_cpu_count": os.cpu_count()}
 
 
 def _torch_threads():
     import torch
 
-    torch.set_num_threads(host_cores()["affinity"])
+    torch.set_num_threads(host_cores()["use"])
     return torch.get_num_threads()
 
 
@@ -146,8 +165,8 @@ def cpu_embed_baseline(budget_s: float = 15.0, batch: int = 16):
     el = time.perf_counter() - t0
     return {"value": done / el, "unit": "images/s", "cores": threads, "kind": "reference-lib",
             "cpu": cpu_model_name(), "host_cores": host_cores(),
-            "cores_note": "torch intra-op threads = the process's CPU affinity (os.sched_getaffinity): the cores "
-                          "this job may use on the box (its cgroup cpuset), not the machine's total",
+            "cores_note": "torch intra-op threads = min(CPU affinity, cgroup CPU quota, OMP_NUM_THREADS): the cores "
+                          "this job may use on the box (16 per GPU there), not the machine's total",
             "sample": f"{done} synthetic 224x224 images (batches of {batch}) through rescale/normalize + a torch fp32 "
                       f"ViT-MSN-base forward (torch.nn.functional, the library the reference's transformers path "
                       f"runs on), {el:.1f}s"}
@@ -281,6 +300,7 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
     img_path = os.path.join(REPO, "tests", "golden", "test_image.jpeg")  # the reference's fixture
     data = open(img_path, "rb").read()
     out = {}
+    log("bench: latency /embed")
     out["embed"] = dict(_lat(lambda: emb.embed_bytes(data), reps), what="embed_bytes (the /embed core): 300x168 "
                         "baseline JPEG -> GPU decode -> device resize -> ViT-MSN-base -> 768 floats on the host")
     vec = emb.embed_bytes(data)
@@ -289,12 +309,14 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
     ix.upsert_tensor([f"r{i}" for i in range(len(X))], torch.from_numpy(X).to(torch.cuda.current_device()),
                      [{"gcs_path": f"images/r{i}.jpg"} for i in range(len(X))])
     got = ret.search(ix, vec, top_k=5)
+    log("bench: latency search top-5")
     out["search_top5"] = dict(_lat(lambda: ret.search(ix, vec, top_k=5), reps * 5),
                               what="retriever.utils.search(index, emb, top_k=5) over 10,000 x 768 f32 rows "
                                    "(index.query with include_values=True, as the reference calls it)",
                               planted_found=sorted(got) == sorted(f"r{r}" for r in planted))
     from fastapi.testclient import TestClient
 
+    log("bench: latency /search_image")
     client = TestClient(retmain.app)
     old_index = retmain.index
     retmain.index = lambda: ix
@@ -307,6 +329,7 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
     finally:
         retmain.index = old_index
     if cpu:
+        log("bench: latency CPU baselines")
         from PIL import Image
 
         from oracle.cosine_topk import cosine_topk_f32
@@ -391,6 +414,9 @@ def jpeg_300x168_line(model, B: int, world: int, rank: int, barrier, max_over_ra
 
 
 def main():
+    import faulthandler
+
+    faulthandler.dump_traceback_later(120, repeat=True, file=sys.stderr)  # a stuck stage names itself
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -471,6 +497,8 @@ def main():
     index = importlib.import_module(f"{PKG}.index")
 
     # ------------------------------------------------------ embed (value) --
+    if rank == 0:
+        log("bench: stage: embed (timed steps)")
     B = args.batch
     model = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=local, max_batch=B)
     model.set_parts(args.parts)
@@ -531,6 +559,8 @@ def main():
     model_tflops = imgs_per_s / world * gflop / 1e3
 
     # ------------------------------------ config 5: end-to-end ingest + retrieve --
+    if rank == 0:
+        log("bench: stage: config 5 ingest")
     ingest = None
     if args.ingest_images > 0:
         sharded_mod = importlib.import_module(f"{PKG}.sharded")
@@ -586,6 +616,8 @@ def main():
         del sidx5
 
     # --------------------------- JPEG decode + decode→embed --
+    if rank == 0:
+        log("bench: stage: JPEG decode + ingest core")
     jpeg = None
     if args.jpeg_images > 0:
         J = importlib.import_module(f"{PKG}.jpeg")
@@ -696,6 +728,8 @@ def main():
         ix.close()
 
     if jpeg is not None:
+        if rank == 0:
+            log("bench: stage: 168x300 JPEG line")
         jpeg["fixture_shape"] = jpeg_300x168_line(model, B, world, rank, barrier, max_over_ranks,
                                                   cpu=rank == 0 and world == 1 and not args.no_cpu)
     latency = None
@@ -760,6 +794,8 @@ def main():
         result["latency"] = latency
 
     # ------------------------------------------------- search (secondary) --
+    if rank == 0:
+        log("bench: stage: search")
     if not args.no_search:
         dim = 512
         rows = args.rows_per_gpu
@@ -873,6 +909,7 @@ def main():
                     "rounding (2 x 2^-11) of the 10th (tests/test_batched_search_gpu.py)"}
 
     if rank == 0 and world == 1 and not args.no_cpu:
+        log("bench: stage: CPU baselines")
         try:
             result["cpu_baseline"] = cpu_embed_baseline()
             if "search" in result:

@@ -680,8 +680,11 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
 // (ky, kx, c), so the 16 K-values a lane needs per step are 16 CONTIGUOUS bytes of
 // one image row (48 bytes per patch row in HWC), and the weight matrix is permuted
 // to the same order once at finalize (W′[n][(ky·P + kx)·3 + c] = W[n][c][ky][kx]).
-// Each byte becomes the exact f32 of ViTImageProcessor's rescale→normalize rounded
-// to bf16 — a [3][256] LUT in LDS, the values the im2col kernel wrote before.
+// Each byte u of channel c becomes bf16(fma(u, pre_a[c], pre_b[c])): rc_model picks the
+// f32 pair (pre_a, pre_b) so that this equals, for every u, the bf16 of ViTImageProcessor's
+// f32 rescale→normalize value — exactly the values the im2col kernel once wrote and the
+// [3][256] LDS table after it read (round 2: 52 % of that kernel's LDS cycles were bank
+// conflicts of the table's random-address reads; now the conversion is VALU only).
 // 128 x 256 tile, 4 waves (as gemm_w2_kernel, whose fragment layout and epilogue it
 // shares), two workgroups per CU; both operands register-staged (one 16-B A load
 // and four 16-B W loads per lane per 32-deep K-step, issued two steps ahead and
@@ -691,9 +694,8 @@ template <int P, int EPI>
 __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     constexpr int BM = 128, BN = 256, BK = 32, KC = 3 * P * P;
     constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 KB + 16 KB
-    static_assert(2 * SLOT + 3 * 256 * 2 <= 64 * 1024, "ring + LUT within the epilogue's 64 KB");
+    static_assert(2 * SLOT <= 64 * 1024, "ring within the epilogue's 64 KB");
     __shared__ __attribute__((aligned(16))) uint8_t smem[64 * 1024];
-    uint16_t *lut = reinterpret_cast<uint16_t *>(smem + 2 * SLOT);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -708,8 +710,6 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     const int gm = min(GM, ntm - grp * GM);
     const int tm = grp * GM + in % gm, tn = in / gm;
     const int m0 = tm * BM, n0 = tn * BN;
-
-    for (int i = tid; i < 3 * 256; i += 256) lut[i] = a.lut[i];
 
     // A: lane pair (row ar, half ah) loads K [32 kt + 16 ah, +16) of patch row m0 + ar
     const int S = a.img_size, gp = S / P, np = gp * gp;
@@ -737,14 +737,24 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     auto store = [&](int slot, int kt, const Regs &r) {
         uint8_t *As = smem + slot * SLOT;
         uint8_t *Ws = As + A_BYTES;
-        const int c0 = (kt * BK + 16 * ah) % 3;  // channel of the first byte (k = ky·3P + kx·3 + c)
+        // channel of byte j is (c0 + j) % 3 with c0 = (32 kt + 16 ah) % 3 (k = ky·3P + kx·3 + c):
+        // rotate the three (a, b) pairs once, then byte j takes pair j % 3 (a constant index)
+        const int c0 = (2 * kt + ah) % 3;
+        const float a0 = c0 == 0 ? a.pre_a[0] : (c0 == 1 ? a.pre_a[1] : a.pre_a[2]);
+        const float a1 = c0 == 0 ? a.pre_a[1] : (c0 == 1 ? a.pre_a[2] : a.pre_a[0]);
+        const float a2 = c0 == 0 ? a.pre_a[2] : (c0 == 1 ? a.pre_a[0] : a.pre_a[1]);
+        const float b0 = c0 == 0 ? a.pre_b[0] : (c0 == 1 ? a.pre_b[1] : a.pre_b[2]);
+        const float b1 = c0 == 0 ? a.pre_b[1] : (c0 == 1 ? a.pre_b[2] : a.pre_b[0]);
+        const float b2 = c0 == 0 ? a.pre_b[2] : (c0 == 1 ? a.pre_b[0] : a.pre_b[1]);
+        const float ra[3] = {a0, a1, a2}, rb[3] = {b0, b1, b2};
         const uint32_t w4[4] = {r.av.x, r.av.y, r.av.z, r.av.w};
         uint32_t o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int cA = (c0 + 2 * j) % 3, cB = (c0 + 2 * j + 1) % 3;
-            const uint32_t bA = (w4[j >> 1] >> (16 * (j & 1))) & 0xffu, bB = (w4[j >> 1] >> (16 * (j & 1) + 8)) & 0xffu;
-            o[j] = (uint32_t)lut[cA * 256 + bA] | ((uint32_t)lut[cB * 256 + bB] << 16);
+            const int e = 2 * j;
+            const float uA = (float)((w4[e >> 2] >> (8 * (e & 3))) & 0xffu);
+            const float uB = (float)((w4[(e + 1) >> 2] >> (8 * ((e + 1) & 3))) & 0xffu);
+            o[j] = pack_bf16x2(fmaf(uA, ra[e % 3], rb[e % 3]), fmaf(uB, ra[(e + 1) % 3], rb[(e + 1) % 3]));
         }
         *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah) ^ asw) << 4)) = make_uint4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah + 1) ^ asw) << 4)) = make_uint4(o[4], o[5], o[6], o[7]);
@@ -764,7 +774,6 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     Regs r0, r1;
     load(0, r0);
     load(1, r1);
-    __syncthreads();  // the LUT
     store(0, 0, r0);
     __syncthreads();
     // one K-step: the MFMAs on slot kt & 1, with `nxt` (step kt + 1) written to the
@@ -985,7 +994,7 @@ inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
 
 // Implicit-GEMM patch embedding: M = images × patches rows, N = hidden, K = 3·P² (P = 16)
 inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
-    RC_REQUIRE(a.img && a.lut && a.img_size % 16 == 0 && a.N % 256 == 0 && a.K == 3 * 16 * 16 && a.M >= 1,
+    RC_REQUIRE(a.img && a.img_size % 16 == 0 && a.N % 256 == 0 && a.K == 3 * 16 * 16 && a.M >= 1,
                RC_ERR_UNSUPPORTED, "patch GEMM: 16x16 patches, N % 256 == 0");
     const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
     if (a.res_lo != nullptr) {

@@ -131,7 +131,7 @@ struct rc_model {
     double rescale = 1.0 / 255.0;
     float mean[3] = {0.485f, 0.456f, 0.406f}, std_[3] = {0.229f, 0.224f, 0.225f};
     float *lut = nullptr;          // [3][256] f32: rescale→normalize of each u8 (pixel_values)
-    uint16_t *lut16 = nullptr;     // the same rounded to bf16 (the patch GEMM's A operand)
+    float pre_a[3] = {}, pre_b[3] = {};  // the patch GEMM's A operand: bf16(fma(u, pre_a[c], pre_b[c]))
     std::map<std::pair<int, int>, DeviceCoeffs> coeff_cache;  // (in, out) → coeffs
     // workspace
     int Mp = 0;
@@ -245,6 +245,39 @@ uint16_t *upload_bf16(rc_model *m, const std::vector<const std::vector<float> *>
     return d;
 }
 
+float bits_f32(uint32_t u) {
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+uint32_t f32_bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+// The patch GEMM converts a byte u of channel c as bf16(fmaf(u, a_c, b_c)).  Find f32 (a_c, b_c)
+// near 1 / (rescale⁻¹·std) and −mean / std for which that equals, for ALL 256 values of u, the
+// bf16 of ViTImageProcessor's f32 value h(u) (exact for the ImageNet parameters at ±0 ulp; the
+// search covers ±16 ulp of each).  Parameters with no exact pair are refused rather than
+// approximated.
+bool exact_affine(const float *h, double a0, double b0, float *a_out, float *b_out) {
+    const float a = (float)a0, b = (float)b0;
+    for (int da = 0; da <= 32; ++da)
+        for (int db = 0; db <= 32; ++db) {
+            const float aa = bits_f32(f32_bits(a) + (uint32_t)((da & 1) ? -(da + 1) / 2 : da / 2));
+            const float bb = bits_f32(f32_bits(b) + (uint32_t)((db & 1) ? -(db + 1) / 2 : db / 2));
+            bool ok = true;
+            for (int u = 0; u < 256 && ok; ++u) ok = host_f2bf(std::fmaf((float)u, aa, bb)) == host_f2bf(h[u]);
+            if (ok) {
+                *a_out = aa;
+                *b_out = bb;
+                return true;
+            }
+        }
+    return false;
+}
+
 void build_lut(rc_model *m) {
     float h[3 * 256];
     for (int c = 0; c < 3; ++c)
@@ -253,12 +286,18 @@ void build_lut(rc_model *m) {
             const float x = (float)((double)u * m->rescale);
             h[c * 256 + u] = (x - m->mean[c]) / m->std_[c];
         }
+    float pa[3], pb[3];
+    for (int c = 0; c < 3; ++c)
+        RC_REQUIRE(exact_affine(h + c * 256, m->rescale / m->std_[c], -(double)m->mean[c] / m->std_[c], &pa[c], &pb[c]),
+                   RC_ERR_UNSUPPORTED,
+                   "preprocess parameters: no f32 affine form reproduces ViTImageProcessor's bf16-rounded values "
+                   "for every byte of channel " + std::to_string(c));
     if (!m->lut) m->lut = (float *)m->alloc(sizeof(h));
     RC_HIP(hipMemcpy(m->lut, h, sizeof(h), hipMemcpyHostToDevice));
-    uint16_t h16[3 * 256];
-    for (int i = 0; i < 3 * 256; ++i) h16[i] = host_f2bf(h[i]);
-    if (!m->lut16) m->lut16 = (uint16_t *)m->alloc(sizeof(h16));
-    RC_HIP(hipMemcpy(m->lut16, h16, sizeof(h16), hipMemcpyHostToDevice));
+    for (int c = 0; c < 3; ++c) {
+        m->pre_a[c] = pa[c];
+        m->pre_b[c] = pb[c];
+    }
 }
 
 // LayerNorm fold of one nn.Linear W [N][K] after LayerNorm(γ, β) (vit_kernels.h):
@@ -482,7 +521,10 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
         GemmArgs a = produce(GemmArgs{nullptr, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden, m->pos,
                                       T}, true);
         a.img = images + (int64_t)i0 * S * S * 3;
-        a.lut = m->lut16;
+        for (int c = 0; c < 3; ++c) {
+            a.pre_a[c] = m->pre_a[c];
+            a.pre_b[c] = m->pre_b[c];
+        }
         a.img_size = S;
         const int t0 = m->timers[T_GEMM].begin(s);
         launch_patch_gemm(a, s);
@@ -672,13 +714,28 @@ int rc_model_set_preprocess(rc_model *m, int resample, double rescale_factor, co
                    "resample must be BICUBIC (3) or BILINEAR (2)");
         std::lock_guard<std::mutex> lk(m->mu);
         DeviceScope ds(m->device);
-        m->resample = resample;
-        m->rescale = rescale_factor;
+        const int old_resample = m->resample;
+        const double old_rescale = m->rescale;
+        float old_mean[3], old_std[3];
         for (int c = 0; c < 3; ++c) {
+            old_mean[c] = m->mean[c];
+            old_std[c] = m->std_[c];
             m->mean[c] = mean[c];
             m->std_[c] = std_[c];
         }
-        build_lut(m);
+        m->resample = resample;
+        m->rescale = rescale_factor;
+        try {
+            build_lut(m);
+        } catch (...) {  // refused parameters leave the model as it was
+            m->resample = old_resample;
+            m->rescale = old_rescale;
+            for (int c = 0; c < 3; ++c) {
+                m->mean[c] = old_mean[c];
+                m->std_[c] = old_std[c];
+            }
+            throw;
+        }
     });
 }
 

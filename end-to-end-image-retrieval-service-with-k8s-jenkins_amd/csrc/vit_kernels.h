@@ -62,9 +62,11 @@ struct GemmArgs {
     const float *ln_c = nullptr;
     float ln_eps = 1e-6f;
     // implicit-GEMM patch embedding (patch_gemm_kernel): A[m][k] is read from the u8
-    // HWC images through a bf16 LUT of rescale→normalize instead of an im2col buffer
+    // HWC images, rescale→normalize as bf16(fma(u, pre_a[c], pre_b[c])) per channel c — an
+    // affine form rc_model verifies, for all 256 byte values, to give exactly the bf16 of
+    // ViTImageProcessor's f32 value (transformers rescale in f64 → f32, normalize in f32)
     const uint8_t *img = nullptr;  // [images][S][S][3]
-    const uint16_t *lut = nullptr; // [3][256] bf16 bits
+    float pre_a[3] = {}, pre_b[3] = {};
     int img_size = 0;              // S
 };
 

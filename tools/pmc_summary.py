@@ -54,12 +54,21 @@ def main():
             rec["clock_GHz"] = m["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9
             if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
                 rec["mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 256 * 4)
+        if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"] > 0:
+            # SQ_ACTIVE_INST_* and SQ_WAVE_CYCLES count quad-cycles per wave: the share of wave lifetime
+            # spent issuing each instruction class (VALU includes MFMA issue on gfx9 counters)
+            for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
+                if c in m:
+                    rec[c.replace("SQ_ACTIVE_INST_", "").lower() + "_issue_frac"] = m[c] / m["SQ_WAVE_CYCLES"]
+        if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
+            rec["valu_non_mfma_insts"] = m["SQ_INSTS_VALU"] - m["SQ_INSTS_MFMA"]
         out[f"{key[0]}@{key[1]}"] = rec
     for k, r in out.items():
         if r["dur_us"] < 20:
             continue
         keys = ["dur_us", "hbm_read_bytes", "hbm_write_bytes", "l2_hit", "clock_GHz", "mfma_busy", "SQ_WAIT_ANY",
-                "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"]
+                "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "valu_issue_frac",
+                "lds_issue_frac", "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "valu_non_mfma_insts", "SQ_VALU_MFMA_COEXEC_CYCLES"]
         print(k, {x: (round(r[x], 3) if isinstance(r.get(x), float) else r.get(x)) for x in keys if x in r})
     if "--json" in sys.argv:
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
