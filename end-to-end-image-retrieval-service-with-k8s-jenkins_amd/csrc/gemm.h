@@ -146,6 +146,189 @@ __device__ __forceinline__ void resid_copy_out(const GemmArgs &a, const uint8_t 
     }
 }
 
+// Epilogue of the 256x256 tile the 8 waves of gemm_pp_kernel / gemm_ring_kernel hold as
+// acc[mq][nq][mi][ni] (wave = grp * 4 + wc: rows grp*128 + mq*64 + mi*16 + li, columns
+// wc*64 + nq*32 + ni*16 + 4g + j).  smem: the ring (>= 128 KB, every read and DMA of the
+// K loop retired by its final barrier); ln_off: the LayerNorm-fold row scales (EPI_*_LN);
+// biasr: the bf16 epilogues' bias, loaded before the K loop.
+template <int EPI, int ABL>
+__device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2][4][2], uint8_t *smem, int ln_off,
+                                            int m0, int n0, const float4 (&biasr)[2][2]) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+    // epilogue: acc[mq][nq][mi][ni][j] = C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
+    // fc1 (GELU + LayerNorm-fold consumer): no LDS staging — bf16 pairs of 16-lane rows
+    // swapped with v_permlane16_swap so each lane stores 16 B (8 consecutive columns);
+    // lane (g, li) of rows 16-block holds columns 4g..4g+3 of both 16-column halves ni, the
+    // swap of rows 1<->0 and 3<->2 between the ni halves makes them 8 contiguous columns.
+    // (Also ABL 64 for the other bf16 epilogues in diagnostic builds.)
+    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN || (epi_bf16_out(EPI) && (ABL & 64) != 0 && !epi_ln(EPI));
+    if constexpr (DIRECT) {
+        float4 bq[2][2], cq[2][2];
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                if constexpr (epi_ln(EPI)) {
+                    bq[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+                    cq[nq][ni] = *reinterpret_cast<const float4 *>(a.ln_c + n0 + cl);
+                } else {
+                    bq[nq][ni] = biasr[nq][ni];
+                }
+            }
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int rl = grp * 128 + mq * 64 + mi * 16 + li;
+                const int row = m0 + rl;
+                float2 r = make_float2(1.f, 0.f);
+                if constexpr (epi_ln(EPI)) r = *reinterpret_cast<const float2 *>(smem + ln_off + rl * 8);
+#pragma unroll
+                for (int nq = 0; nq < 2; ++nq) {
+                    uint32_t u[2][2];
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const f32x4 v4 = acc[mq][nq][mi][ni];
+                        const float4 b4 = bq[nq][ni];
+                        f32x2 lo, hi;
+                        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′, as the staged epilogue
+                            const float4 c4 = cq[nq][ni];
+                            lo = f32x2{fmaf(r.x, v4[0], fmaf(r.y, c4.x, b4.x)), fmaf(r.x, v4[1], fmaf(r.y, c4.y, b4.y))};
+                            hi = f32x2{fmaf(r.x, v4[2], fmaf(r.y, c4.z, b4.z)), fmaf(r.x, v4[3], fmaf(r.y, c4.w, b4.w))};
+                        } else {
+                            lo = f32x2{v4[0] + b4.x, v4[1] + b4.y};
+                            hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
+                        }
+                        if constexpr (epi_gelu(EPI) && !(ABL & 16)) {
+                            lo = gelu_fast2(lo);
+                            hi = gelu_fast2(hi);
+                        }
+                        u[ni][0] = pack_bf16x2(lo.x, lo.y);
+                        u[ni][1] = pack_bf16x2(hi.x, hi.y);
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
+                        u[0][h] = r2[0];
+                        u[1][h] = r2[1];
+                    }
+                    const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
+                    if (row < a.M) {
+                        uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + col);
+                        const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
+                        if constexpr ((ABL & 32) != 0) nt_store16(dst, val);
+                        else *dst = val;
+                    }
+                }
+            }
+        return;
+    }
+    if constexpr (epi_bf16_out(EPI)) {
+        // Stage the 256x256 bf16 tile in LDS (512-B rows, 16-B chunk XOR (row & 31)),
+        // then every wave stores whole 512-B row segments with 16-B stores.
+        // (The K loop's final barrier retired every ds_read and DMA: LDS is free.)
+        float2 lrs[2][4];  // LayerNorm fold: (rstd, -rstd*mu) of this lane's 8 rows
+        if constexpr (epi_ln(EPI)) {
+#pragma unroll
+            for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    lrs[mq][mi] = *reinterpret_cast<const float2 *>(smem + ln_off + (grp * 128 + mq * 64 + mi * 16 + li) * 8);
+        }
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;  // tile-local column
+                float4 bias, lc;
+                if constexpr (epi_ln(EPI)) {
+                    bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+                    lc = *reinterpret_cast<const float4 *>(a.ln_c + n0 + cl);
+                } else {
+                    bias = biasr[nq][ni];
+                }
+#pragma unroll
+                for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi) {
+                        const int rl = grp * 128 + mq * 64 + mi * 16 + li;
+                        const f32x4 v4 = acc[mq][nq][mi][ni];
+                        float v0, v1, v2, v3;
+                        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′
+                            const float2 r = lrs[mq][mi];
+                            v0 = fmaf(r.x, v4[0], fmaf(r.y, lc.x, bias.x));
+                            v1 = fmaf(r.x, v4[1], fmaf(r.y, lc.y, bias.y));
+                            v2 = fmaf(r.x, v4[2], fmaf(r.y, lc.z, bias.z));
+                            v3 = fmaf(r.x, v4[3], fmaf(r.y, lc.w, bias.w));
+                        } else {
+                            v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
+                        }
+                        if constexpr (epi_gelu(EPI) && !(ABL & 16)) {
+                            const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
+                            v0 = lo.x;
+                            v1 = lo.y;
+                            v2 = hi.x;
+                            v3 = hi.y;
+                        }
+                        const int off = rl * 512 + ((((cl >> 3) ^ (rl & 31))) << 4) + (cl & 7) * 2;
+                        *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+                    }
+            }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 512 + tid;
+            const int rl = id >> 5, ch = id & 31;
+            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
+            if constexpr ((ABL & 8) != 0) {
+                asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+            } else if (m0 + rl < a.M) {
+                uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8);
+                if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
+                else *dst = v;
+            }
+        }
+        return;
+    }
+    // f32 epilogues (residual add / patch scatter): the 256x256 f32 tile is 256 KB,
+    // so each group's 128 rows are staged in turn (1-KB rows, 16-B chunk XOR
+    // (row & 63)) and copied out by all 512 threads as whole 1-KB row segments:
+    // 16-B residual/pos loads issued back to back, then 16-B stores.
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (grp == h) {
+#pragma unroll
+            for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                    const float4 bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
+#pragma unroll
+                    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+                        for (int mi = 0; mi < 4; ++mi) {
+                            const int rl = mq * 64 + mi * 16 + li;  // row within the half
+                            const f32x4 v4 = acc[mq][nq][mi][ni];
+                            const int off = rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4);
+                            *reinterpret_cast<float4 *>(smem + off) =
+                                make_float4(v4[0] + bias.x, v4[1] + bias.y, v4[2] + bias.z, v4[3] + bias.w);
+                        }
+                }
+        }
+        __syncthreads();
+        // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
+        // may still be live): 8 residual loads back to back, then the adds, the LN statistics
+        // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
+        // (bf16 pairs: passes of 4 rows; 8 would spill beside the other group's accumulators)
+        resid_copy_out<EPI, 512, 16, epi_hl(EPI) ? 4 : 8>(a, smem, tid, m0 + h * 128, n0);
+        if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
+    }
+}
+
 // ----------------------------------------------------------- ping-pong GEMM --
 // 256x256x64 tile, 8 waves in two groups: G0 = waves 0-3 (output rows 0-127),
 // G1 = waves 4-7 (rows 128-255); wave w and w+4 share a SIMD.  Each wave owns
@@ -315,177 +498,172 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         return;
     }
 
-    // epilogue: acc[mq][nq][mi][ni][j] = C[m0 + grp*128 + mq*64 + mi*16 + li][n0 + wc*64 + nq*32 + ni*16 + 4g + j]
-    // fc1 (GELU + LayerNorm-fold consumer): no LDS staging — bf16 pairs of 16-lane rows
-    // swapped with v_permlane16_swap so each lane stores 16 B (8 consecutive columns);
-    // lane (g, li) of rows 16-block holds columns 4g..4g+3 of both 16-column halves ni, the
-    // swap of rows 1<->0 and 3<->2 between the ni halves makes them 8 contiguous columns.
-    // (Also ABL 64 for the other bf16 epilogues in diagnostic builds.)
-    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN || (epi_bf16_out(EPI) && (ABL & 64) != 0 && !epi_ln(EPI));
-    if constexpr (DIRECT) {
-        float4 bq[2][2], cq[2][2];
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni) {
-                const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
-                if constexpr (epi_ln(EPI)) {
-                    bq[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
-                    cq[nq][ni] = *reinterpret_cast<const float4 *>(a.ln_c + n0 + cl);
-                } else {
-                    bq[nq][ni] = biasr[nq][ni];
-                }
-            }
-#pragma unroll
-        for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int rl = grp * 128 + mq * 64 + mi * 16 + li;
-                const int row = m0 + rl;
-                float2 r = make_float2(1.f, 0.f);
-                if constexpr (epi_ln(EPI)) r = *reinterpret_cast<const float2 *>(smem + 2 * STAGE + rl * 8);
-#pragma unroll
-                for (int nq = 0; nq < 2; ++nq) {
-                    uint32_t u[2][2];
-#pragma unroll
-                    for (int ni = 0; ni < 2; ++ni) {
-                        const f32x4 v4 = acc[mq][nq][mi][ni];
-                        const float4 b4 = bq[nq][ni];
-                        f32x2 lo, hi;
-                        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′, as the staged epilogue
-                            const float4 c4 = cq[nq][ni];
-                            lo = f32x2{fmaf(r.x, v4[0], fmaf(r.y, c4.x, b4.x)), fmaf(r.x, v4[1], fmaf(r.y, c4.y, b4.y))};
-                            hi = f32x2{fmaf(r.x, v4[2], fmaf(r.y, c4.z, b4.z)), fmaf(r.x, v4[3], fmaf(r.y, c4.w, b4.w))};
-                        } else {
-                            lo = f32x2{v4[0] + b4.x, v4[1] + b4.y};
-                            hi = f32x2{v4[2] + b4.z, v4[3] + b4.w};
-                        }
-                        if constexpr (epi_gelu(EPI) && !(ABL & 16)) {
-                            lo = gelu_fast2(lo);
-                            hi = gelu_fast2(hi);
-                        }
-                        u[ni][0] = pack_bf16x2(lo.x, lo.y);
-                        u[ni][1] = pack_bf16x2(hi.x, hi.y);
-                    }
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const auto r2 = __builtin_amdgcn_permlane16_swap(u[0][h], u[1][h], false, false);
-                        u[0][h] = r2[0];
-                        u[1][h] = r2[1];
-                    }
-                    const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
-                    if (row < a.M) {
-                        uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + col);
-                        const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
-                        if constexpr ((ABL & 32) != 0) nt_store16(dst, val);
-                        else *dst = val;
-                    }
-                }
-            }
-        return;
-    }
-    if constexpr (epi_bf16_out(EPI)) {
-        // Stage the 256x256 bf16 tile in LDS (512-B rows, 16-B chunk XOR (row & 31)),
-        // then every wave stores whole 512-B row segments with 16-B stores.
-        // (The K loop's final barrier retired every ds_read and DMA: LDS is free.)
-        float2 lrs[2][4];  // LayerNorm fold: (rstd, -rstd*mu) of this lane's 8 rows
-        if constexpr (epi_ln(EPI)) {
-#pragma unroll
-            for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-                    lrs[mq][mi] = *reinterpret_cast<const float2 *>(smem + 2 * STAGE + (grp * 128 + mq * 64 + mi * 16 + li) * 8);
-        }
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni) {
-                const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;  // tile-local column
-                float4 bias, lc;
-                if constexpr (epi_ln(EPI)) {
-                    bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
-                    lc = *reinterpret_cast<const float4 *>(a.ln_c + n0 + cl);
-                } else {
-                    bias = biasr[nq][ni];
-                }
-#pragma unroll
-                for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi) {
-                        const int rl = grp * 128 + mq * 64 + mi * 16 + li;
-                        const f32x4 v4 = acc[mq][nq][mi][ni];
-                        float v0, v1, v2, v3;
-                        if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′
-                            const float2 r = lrs[mq][mi];
-                            v0 = fmaf(r.x, v4[0], fmaf(r.y, lc.x, bias.x));
-                            v1 = fmaf(r.x, v4[1], fmaf(r.y, lc.y, bias.y));
-                            v2 = fmaf(r.x, v4[2], fmaf(r.y, lc.z, bias.z));
-                            v3 = fmaf(r.x, v4[3], fmaf(r.y, lc.w, bias.w));
-                        } else {
-                            v0 = v4[0] + bias.x, v1 = v4[1] + bias.y, v2 = v4[2] + bias.z, v3 = v4[3] + bias.w;
-                        }
-                        if constexpr (epi_gelu(EPI) && !(ABL & 16)) {
-                            const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
-                            v0 = lo.x;
-                            v1 = lo.y;
-                            v2 = hi.x;
-                            v3 = hi.y;
-                        }
-                        const int off = rl * 512 + ((((cl >> 3) ^ (rl & 31))) << 4) + (cl & 7) * 2;
-                        *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-                    }
-            }
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int id = it * 512 + tid;
-            const int rl = id >> 5, ch = id & 31;
-            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
-            if constexpr ((ABL & 8) != 0) {
-                asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-            } else if (m0 + rl < a.M) {
-                uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8);
-                if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
-                else *dst = v;
-            }
-        }
-        return;
-    }
-    // f32 epilogues (residual add / patch scatter): the 256x256 f32 tile is 256 KB,
-    // so each group's 128 rows are staged in turn (1-KB rows, 16-B chunk XOR
-    // (row & 63)) and copied out by all 512 threads as whole 1-KB row segments:
-    // 16-B residual/pos loads issued back to back, then 16-B stores.
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (grp == h) {
-#pragma unroll
-            for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                for (int ni = 0; ni < 2; ++ni) {
-                    const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
-                    const float4 bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
-#pragma unroll
-                    for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-                        for (int mi = 0; mi < 4; ++mi) {
-                            const int rl = mq * 64 + mi * 16 + li;  // row within the half
-                            const f32x4 v4 = acc[mq][nq][mi][ni];
-                            const int off = rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4);
-                            *reinterpret_cast<float4 *>(smem + off) =
-                                make_float4(v4[0] + bias.x, v4[1] + bias.y, v4[2] + bias.z, v4[3] + bias.w);
-                        }
-                }
-        }
-        __syncthreads();
-        // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
-        // may still be live): 8 residual loads back to back, then the adds, the LN statistics
-        // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
-        // (bf16 pairs: passes of 4 rows; 8 would spill beside the other group's accumulators)
-        resid_copy_out<EPI, 512, 16, epi_hl(EPI) ? 4 : 8>(a, smem, tid, m0 + h * 128, n0);
-        if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
-    }
+    pp_epilogue<EPI, ABL>(a, acc, smem, 2 * STAGE, m0, n0, biasr);
 }
 
+// --------------------------------------------------------------- ring GEMM --
+// The ping-pong tile (256x256, 8 waves in two staggered groups, the same wave ->
+// output map and epilogue) with a deeper DMA pipeline.  gemm_pp_kernel keeps one
+// 64-deep K-tile in flight and drains it (vmcnt(0)) every K-tile: the L2 -> LDS fill
+// is latency-bound (its no-MFMA ablation moves fc1's 1.86 GB in 137 us, 53 GB/s per
+// CU, against the ~70 GB/s per CU an LDS-DMA gather from L2 reaches with ~72 KB in
+// flight).  Here the ring has NS slots of one 32-deep K-step (A 256 x 32 + W 256 x 32,
+// 32 KB, 64-B rows with the 16-B chunk XOR ((row >> 3) & 1) << 1 of gemm_w2_kernel:
+// conflict-free ds_read_b128 fragments) and NS - 2 K-steps stay in flight across
+// every barrier: counted vmcnt, never 0 inside the loop.
+// A K-step is 2 phases (rows mq*64.. of the wave's 128); a phase is an M segment
+// (the phase's 4 A fragments, at phase 0 also the step's 4 W fragments, kept for both
+// phases; this wave's 2 DMA pieces of step t + NS - 1) and a C segment (16 MFMAs),
+// each closed by a barrier; G1 runs one segment behind G0.
+// Hazards: step t + NS - 1 goes to slot (t - 1) % NS, issued in step t's M segments
+// — after the barrier that closed both groups' last reads of step t - 1 (their phase-1
+// M segments).  Step t + 1 is read first by G0 in its (t + 1, 0) M segment; every
+// wave waits for its own pieces of step t + 1 (vmcnt(4 (NS - 3)) after issuing step
+// t + NS - 1's last pieces) in its (t, 1) M segment, and the barrier closing G1's (t, 1)
+// M segment precedes G0's (t + 1, 0) M segment.
+template <int EPI, int NS, int NKS = 0>
+__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
+    constexpr int BM = 256, BN = 256, BK = 32;
+    constexpr int A_BYTES = BM * BK * 2, SLOT = 2 * A_BYTES;  // 16 KB + 16 KB
+    constexpr int LN_LDS = epi_ln(EPI) ? BM * 8 : 0;
+    // the epilogue stages up to 128 KB from offset 0: the LayerNorm row scales live past both
+    constexpr int LN_OFF = NS * SLOT > 128 * 1024 ? NS * SLOT : 128 * 1024;
+    constexpr int SMEM = LN_OFF + LN_LDS;
+    static_assert(NS >= 3 && NS <= 4 && SMEM <= 160 * 1024, "ring of 3..4 slots");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int ntn = a.N / BN;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    int tm = tile / ntn, tn = tile % ntn;
+    if (a.group_m > 0) {
+        const int ntm = (a.M + BM - 1) / BM;
+        const int gt = a.group_m * ntn, gi = tile / gt, in = tile - gi * gt;
+        const int gm = min(a.group_m, ntm - gi * a.group_m);
+        tm = gi * a.group_m + in % gm;
+        tn = in / gm;
+    }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int K = a.K;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+
+    // 32 pieces of 1 KB (16 rows x 64 B) per slot: A rows 0-255 = pieces 0-15, W = 16-31;
+    // wave w issues pieces w + 8 i, i = 0..3 (two per phase).  Lane l writes LDS bytes
+    // [16 l, 16 l + 16): row l >> 2 of the piece, stored chunk l & 3 = source chunk
+    // (l & 3) ^ (((l >> 5) & 1) << 1) (the row's bit 3 is bit 5 of the lane).
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    auto stage2 = [&](int slot, int k0, int i0) {
+        uint8_t *base = smem + slot * SLOT;
+#pragma unroll
+        for (int i = i0; i < i0 + 2; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = piece < 16;
+            const uint16_t *src = (is_a ? Ag + (int64_t)(piece * 16 + prow) * K : Wg + (int64_t)((piece - 16) * 16 + prow) * K);
+            __builtin_amdgcn_global_load_lds((const void *)(src + k0 + pchunk * 8), (lds_void_t *)(base + piece * 1024), 16,
+                                             0, 0);
+        }
+    };
+    auto bar = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // fragment of rows r0 + li (r0 % 16 == 0), k chunk g: 16 B at row * 64 + (g ^ ((li >> 3) & 1) << 1) * 16
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+        for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+            for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 biasr[2][2];
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                biasr[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
+    }
+
+    const int nk = NKS > 0 ? NKS : K / BK;
+    // prologue: steps 0 .. NS - 2 in flight, wait for step 0
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) {
+        if (t < nk) {
+            stage2(t, t * BK, 0);
+            stage2(t, t * BK, 2);
+        }
+    }
+    if constexpr (epi_ln(EPI)) {
+        if (tid < BM)
+            *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) =
+                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * (2 * LN_TILES), a.ln_eps);
+    }
+    if (nk >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (grp == 1) bar();  // stagger: G1 one segment behind
+
+    bf16x8 af[4], wf[2][2];  // [mi], [nq][ni]
+#pragma nounroll
+    for (int t = 0; t < nk; ++t) {
+        const int cur = t % NS;
+        const uint8_t *As = smem + cur * SLOT;
+        const uint8_t *Ws = As + A_BYTES;
+        const int tn_ = t + NS - 1;  // the step whose DMA this step issues
+        const int nslot = (t + NS - 1) % NS;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            // ---- M segment
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = grp * 128 + p * 64 + mi * 16 + li;
+                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 64 + fchunk);
+            }
+            if (p == 0) {
+#pragma unroll
+                for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                        wf[nq][ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 64 + fchunk);
+                    }
+            }
+            if (tn_ < nk) stage2(nslot, tn_ * BK, 2 * p);
+            if (p == 1) {  // this wave's pieces of step t + 1 have landed (the younger steps may fly)
+                if (t + NS - 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
+                else if (t + NS - 2 < nk && NS >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 3)) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            // ---- C segment: rows p*64 .. +64 of the wave's 128, all 64 columns
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        acc[p][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nq][ni], af[mi], acc[p][nq][mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+    }
+    if (grp == 0) bar();  // balance the stagger barrier
+    pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr);
+}
 
 // Epilogue of a 128 x 256 tile held as acc[mi][ni] by 4 waves (wave w: columns
 // [64w, 64w + 64)): acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + w*64 + ni*16 + 4g + j].
@@ -969,7 +1147,7 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 // (Rounds 1-2 also measured a 128x128 4-wave kernel, a 256x256 / 128x256 single-
 // barrier kernel, a persistent kernel, Stream-K and a deferred-store persistent
 // kernel: each lost on every shape and was removed.)
-enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9 };
+enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9 };
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
@@ -1020,10 +1198,27 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_SKINNY) && a.ln_c && a.ln_stats, RC_ERR_UNSUPPORTED,
-                   "LayerNorm-fold consumers run on the ping-pong or skinny kernel");
+        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
+                       a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
     }
     switch (pick) {
+        case GEMM_RING4:
+        case GEMM_RING3: {
+            RC_REQUIRE(a.N % 256 == 0 && a.K % 32 == 0, RC_ERR_UNSUPPORTED, "ring GEMM: N % 256 == 0, K % 32 == 0");
+            a.group_m = gemm_group_m(a);
+            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
+            const dim3 gr(ntm * ntn), bl(512);
+            if (pick == GEMM_RING4) {
+                if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 24>), gr, bl, 0, s, a);
+                else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 96>), gr, bl, 0, s, a);
+                else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4>), gr, bl, 0, s, a);
+            } else {
+                if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 24>), gr, bl, 0, s, a);
+                else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 96>), gr, bl, 0, s, a);
+                else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3>), gr, bl, 0, s, a);
+            }
+            break;
+        }
         case GEMM_W2: {
             if constexpr (!epi_ln(EPI)) {
                 RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");

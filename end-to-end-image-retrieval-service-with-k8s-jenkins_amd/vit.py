@@ -352,6 +352,10 @@ class VitMsnEmbedder:
         """Run the last encoder layer on the CLS rows only (default) or on every row."""
         check(self.lib.rc_model_set_last_layer(self._h, int(bool(cls_only))))
 
+    def set_gemm_variant(self, variant: int) -> None:
+        """Full-batch projection GEMM kernel: 0 auto, 4 ping-pong, 5 / 6 ring (A/B; same bits)."""
+        check(self.lib.rc_model_set_gemm_variant(self._h, int(variant)))
+
     def timing_reset(self) -> None:
         check(self.lib.rc_model_timing_reset(self._h))
 

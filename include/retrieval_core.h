@@ -253,6 +253,12 @@ int rc_model_set_last_layer(rc_model *m, int cls_only);
  * parity tests). */
 int rc_model_set_ln_fold(rc_model *m, int on);
 
+/* Projection-GEMM kernel for the full-batch GEMMs (A/B measurements; results are
+ * bit-identical across variants: every kernel accumulates K in the same order):
+ * 0 auto, 4 ping-pong (one 64-deep K-tile in flight), 5 ring (4 slots of 32-deep
+ * K-steps, 2 in flight), 6 ring (3 slots, 1 in flight). */
+int rc_model_set_gemm_variant(rc_model *m, int variant);
+
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM, 2 = attention, 3 = layernorm,
  * 4 = preprocess, 5 = QKV GEMM, 6 = O-proj GEMM, 7 = fc2 GEMM (5-7 and 1: the
@@ -266,7 +272,8 @@ int rc_model_timing_reset(rc_model *m);
  * out = epilogue(A[M][K] · W[N][K]ᵀ + bias): epi 0 → bf16 out, 1 → bf16 GELU(out),
  * 2 → f32 out += (residual, in place), 3 → f32 patch scatter (+pos, tokens/image).
  * A must have round_up(M, 256) readable rows; N % 256 == 0 (M > 256), K % 64 == 0.
- * variant: 0 auto, 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256). */
+ * variant: 0 auto, 4 256x256 ping-pong, 5 / 6 256x256 ring (4 / 3 slots), 8 128x256
+ * two-workgroup, 9 skinny (M <= 256). */
 int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N, int K,
                  void *out, const float *pos, int tokens, void *stream);
 
