@@ -134,6 +134,7 @@ SIGNATURES = {
     "rc_jpeg_decoder_create": (C.c_int, [_i32, _i32, _i64, C.POINTER(_vp)]),
     "rc_jpeg_decoder_destroy": (C.c_int, [_vp]),
     "rc_jpeg_decode": (C.c_int, [_vp, _i32, C.POINTER(C.c_char_p), _pi64, _vp, _pi64, _vp]),
+    "rc_jpeg_decode_resized": (C.c_int, [_vp, _i32, C.POINTER(C.c_char_p), _pi64, _i32, _i32, _vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -19,6 +19,11 @@
 // triangle filters with replicated edge rows/columns, plain replication when the
 // downsampled width is <= 2) and jdcolor.c's fixed-point YCbCr -> RGB, writing
 // HWC u8 RGB straight into the caller's buffer (the input of rc_embed's resize).
+// rc_jpeg_decode_resized fuses the colour pass with Pillow's horizontal resample
+// (jpeg_color_resize_h_kernel: a source row's RGB built in LDS, each output pixel
+// filtered from it) and runs the vertical pass per image (jpeg_resize_v_kernel):
+// the full-size RGB image is never written, and the result equals PIL decode +
+// Image.resize (ViTImageProcessor's resize, embedding/main.py:97,107) bit for bit.
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -27,7 +32,11 @@
 #include <thread>
 #include <vector>
 
+#include <map>
+#include <tuple>
+
 #include "rc_common.h"
+#include "resample.h"
 
 namespace rc {
 namespace jpeg {
@@ -554,6 +563,126 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t *__restri
     o[2] = (uint8_t)min(max(B, 0), 255);
 }
 
+// Per-image plan of the fused decode → resize (rc_jpeg_decode_resized), Pillow's
+// ImagingResample order: horizontal pass over the source rows the vertical pass reads
+// ([y0, y0 + Hs)), into tmp [Hs][S][3], then the vertical pass into out [S][S][3]; an
+// axis whose size already is S is skipped (need_h / need_v), as Pillow skips it.
+struct RDesc {
+    int32_t S, need_h, need_v, y0, Hs, hk, vk, pad;
+    const int *hb, *hc;  // horizontal bounds [S][2] (xmin, count) / coefficients [S][hk]
+    const int *vb, *vc;  // vertical bounds relative to y0 / coefficients [S][vk]
+    int64_t tmp_off, out_off;
+};
+
+__device__ __forceinline__ uint8_t clip8_22(int acc) {
+    const int v = acc >> 22;
+    return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+__device__ __forceinline__ void ycc_rgb(const uint8_t *__restrict__ planes, const Desc &d, int x, int y, int &R, int &G,
+                                        int &B) {
+    const int Y = upsampled(planes, d, 0, x, y);
+    if (d.ncomp == 1) {
+        R = G = B = Y;
+        return;
+    }
+    const int cb = upsampled(planes, d, 1, x, y) - 128, cr = upsampled(planes, d, 2, x, y) - 128;
+    R = min(max(Y + ((91881 * cr + 32768) >> 16), 0), 255);
+    G = min(max(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16), 0), 255);
+    B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
+}
+
+constexpr int RS_WIN = 16384;  // source pixels of one row staged in LDS at a time (48 KB)
+
+// grid (max rows, n), 256 lanes: block (y, i) produces row y of image i's horizontal pass
+// (or, without one, its colour row).  The source row's RGB is built in LDS over windows
+// of RS_WIN pixels; every output pixel whose taps lie inside the window is filtered from
+// it (Pillow's fixed-point sum, 22 fractional bits, rounding 1 << 21, clip).
+__global__ __launch_bounds__(256) void jpeg_color_resize_h_kernel(const uint8_t *__restrict__ planes,
+                                                                 const Desc *__restrict__ descs,
+                                                                 const RDesc *__restrict__ rdescs, uint8_t *__restrict__ tmp,
+                                                                 uint8_t *__restrict__ out) {
+    __shared__ uint8_t row[RS_WIN * 3];
+    __shared__ int span[2];
+    const Desc d = descs[blockIdx.y];
+    const RDesc r = rdescs[blockIdx.y];
+    const int y = blockIdx.x;
+    if (y >= r.Hs) return;  // block-uniform
+    const int sy = r.y0 + y, S = r.S;
+    uint8_t *dst = (r.need_v ? tmp + r.tmp_off : out + r.out_off) + (int64_t)y * S * 3;
+    if (!r.need_h) {  // width already S: the colour row as it is
+        for (int x = threadIdx.x; x < d.W; x += 256) {
+            int R, G, B;
+            ycc_rgb(planes, d, x, sy, R, G, B);
+            dst[3 * x] = (uint8_t)R;
+            dst[3 * x + 1] = (uint8_t)G;
+            dst[3 * x + 2] = (uint8_t)B;
+        }
+        return;
+    }
+    for (int xo0 = 0; xo0 < S;) {
+        if (threadIdx.x == 0) {  // outputs [xo0, xo1) whose taps fit one window from xmin(xo0)
+            const int w0 = r.hb[2 * xo0];
+            int xo1 = xo0 + 1;
+            while (xo1 < S && r.hb[2 * xo1] + r.hb[2 * xo1 + 1] <= w0 + RS_WIN) ++xo1;
+            span[0] = w0;
+            span[1] = xo1;
+        }
+        __syncthreads();
+        const int w0 = span[0], xo1 = span[1];
+        const int w1 = min(d.W, w0 + RS_WIN);
+        for (int x = w0 + (int)threadIdx.x; x < w1; x += 256) {
+            int R, G, B;
+            ycc_rgb(planes, d, x, sy, R, G, B);
+            row[3 * (x - w0)] = (uint8_t)R;
+            row[3 * (x - w0) + 1] = (uint8_t)G;
+            row[3 * (x - w0) + 2] = (uint8_t)B;
+        }
+        __syncthreads();
+        for (int xo = xo0 + (int)threadIdx.x; xo < xo1; xo += 256) {
+            const int xmin = r.hb[2 * xo] - w0, xn = r.hb[2 * xo + 1];
+            const int *c = r.hc + xo * r.hk;
+            int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+            for (int k = 0; k < xn; ++k) {
+                const uint8_t *p = row + 3 * (xmin + k);
+                a0 += p[0] * c[k];
+                a1 += p[1] * c[k];
+                a2 += p[2] * c[k];
+            }
+            dst[3 * xo] = clip8_22(a0);
+            dst[3 * xo + 1] = clip8_22(a1);
+            dst[3 * xo + 2] = clip8_22(a2);
+        }
+        __syncthreads();  // the window is rebuilt next
+        xo0 = xo1;
+    }
+}
+
+// grid (ceil(S*S / 256), n): Pillow's vertical pass of image blockIdx.y (need_v only).
+__global__ __launch_bounds__(256) void jpeg_resize_v_kernel(const RDesc *__restrict__ rdescs,
+                                                           const uint8_t *__restrict__ tmp, uint8_t *__restrict__ out) {
+    const RDesc r = rdescs[blockIdx.y];
+    if (!r.need_v) return;
+    const int S = r.S;
+    const int p = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (p >= S * S) return;
+    const int yo = p / S, x = p - yo * S;
+    const int ymin = r.vb[2 * yo], yn = r.vb[2 * yo + 1];
+    const int *c = r.vc + yo * r.vk;
+    const uint8_t *col = tmp + r.tmp_off + ((int64_t)ymin * S + x) * 3;
+    int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+    for (int k = 0; k < yn; ++k) {
+        const uint8_t *q = col + (int64_t)k * S * 3;
+        a0 += q[0] * c[k];
+        a1 += q[1] * c[k];
+        a2 += q[2] * c[k];
+    }
+    uint8_t *o = out + r.out_off + (int64_t)p * 3;
+    o[0] = clip8_22(a0);
+    o[1] = clip8_22(a1);
+    o[2] = clip8_22(a2);
+}
+
 }  // namespace jpeg
 
 // Batched decoder: pinned host staging + device buffers sized at create.
@@ -572,6 +701,16 @@ struct JpegDecoder {
     uint8_t *d_planes = nullptr;
     hipEvent_t staged = nullptr;  // the last H2D copy out of the pinned staging
     std::mutex mu;
+    // fused decode → resize: per-image plans (pinned + device), the horizontal pass's output,
+    // Pillow coefficient tables per (size in, size out, filter, y0 shift) built on first use
+    jpeg::RDesc *h_rdesc = nullptr, *d_rdesc = nullptr;
+    uint8_t *d_tmp = nullptr;
+    size_t tmp_bytes = 0;
+    struct Coeffs {
+        int ksize = 0, first = 0, last = 0;
+        int *bounds = nullptr, *coef = nullptr;
+    };
+    std::map<std::tuple<int, int, int, int>, Coeffs> coeffs;
 };
 
 }  // namespace rc
@@ -618,6 +757,8 @@ extern "C" int rc_jpeg_decoder_create(int device, int max_images, int64_t max_bl
             h->d_qtab = (uint16_t *)dmalloc((size_t)max_images * 3 * 128);
             h->d_desc = (jpeg::Desc *)dmalloc((size_t)max_images * sizeof(jpeg::Desc));
             h->d_planes = (uint8_t *)dmalloc((size_t)max_blocks * 64);
+            h->h_rdesc = (jpeg::RDesc *)hmalloc((size_t)max_images * sizeof(jpeg::RDesc));
+            h->d_rdesc = (jpeg::RDesc *)dmalloc((size_t)max_images * sizeof(jpeg::RDesc));
             RC_HIP(hipEventCreateWithFlags(&h->staged, hipEventDisableTiming));
         } catch (...) {
             rc_jpeg_decoder_destroy(h);
@@ -641,6 +782,13 @@ extern "C" int rc_jpeg_decoder_destroy(rc_jpeg_decoder *h) {
         dfree(h->d_qtab);
         dfree(h->d_desc);
         dfree(h->d_planes);
+        hfree(h->h_rdesc);
+        dfree(h->d_rdesc);
+        dfree(h->d_tmp);
+        for (auto &kv : h->coeffs) {
+            dfree(kv.second.bounds);
+            dfree(kv.second.coef);
+        }
         if (h->staged) (void)hipEventDestroy(h->staged);
         delete h;
     });
@@ -660,6 +808,106 @@ static int huffman_threads() {
     return n;
 }
 
+namespace {
+
+// Header parse, host Huffman (threaded), pinned staging and H2D copies, IDCT into
+// h->d_planes; fills h->h_desc / h->d_desc (rgb_off from rgb_offsets, or 0).  The caller
+// records h->staged after its own uploads from pinned memory and launches the colour pass.
+void stage_idct(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens, const int64_t *rgb_offsets,
+                hipStream_t s, std::vector<jpeg::Header> &hd, int &maxpix) {
+    // headers first (cheap, serial): geometry, block offsets, capacity check
+    hd.assign(n, jpeg::Header{});
+    std::vector<int64_t> base(n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        jpeg::parse(jpgs[i], lens[i], hd[i]);
+        RC_REQUIRE(hd[i].supported, RC_ERR_UNSUPPORTED, "JPEG " + std::to_string(i) + " not decodable here: " + hd[i].why);
+        base[i + 1] = base[i] + hd[i].blocks;
+    }
+    RC_REQUIRE(base[n] <= h->max_blocks, RC_ERR_INVALID, "batch exceeds the decoder's max_blocks");
+    // the pinned staging is reused: wait for the previous call's upload
+    RC_HIP(hipEventSynchronize(h->staged));
+    // Huffman decode, one image per worker
+    std::vector<std::string> errs(n);
+    auto work = [&](int i) {
+        try {
+            jpeg::decode_coefficients(hd[i], h->h_coef + base[i] * 64);
+        } catch (const std::exception &e) {
+            errs[i] = e.what();
+        }
+    };
+    const int nthreads = std::max(1, std::min<int>(n, huffman_threads()));
+    if (nthreads == 1) {
+        for (int i = 0; i < n; ++i) work(i);
+    } else {
+        std::vector<std::thread> pool;
+        std::atomic<int> next{0};
+        for (int t = 0; t < nthreads; ++t)
+            pool.emplace_back([&] {
+                for (int i; (i = next.fetch_add(1)) < n;) work(i);
+            });
+        for (auto &t : pool) t.join();
+    }
+    for (int i = 0; i < n; ++i)
+        RC_REQUIRE(errs[i].empty(), RC_ERR_INVALID, "JPEG " + std::to_string(i) + ": " + errs[i]);
+    maxpix = 0;
+    for (int i = 0; i < n; ++i) {
+        const jpeg::Header &H = hd[i];
+        jpeg::Desc &d = h->h_desc[i];
+        std::memset(&d, 0, sizeof(d));
+        d.W = H.width;
+        d.H = H.height;
+        d.ncomp = H.ncomp;
+        for (int c = 0; c < H.ncomp; ++c) {
+            d.rx[c] = H.hmax / H.c[c].h;
+            d.ry[c] = H.vmax / H.c[c].v;
+            d.dw[c] = (int)(((int64_t)H.width * H.c[c].h + H.hmax - 1) / H.hmax);
+            d.dh[c] = (int)(((int64_t)H.height * H.c[c].v + H.vmax - 1) / H.vmax);
+            d.bw[c] = H.c[c].bw;
+            d.blk0[c] = base[i] + H.c[c].blk0;
+            std::memcpy(h->h_qtab + (int64_t)(3 * i + c) * 64, H.qt[H.c[c].tq], 128);
+            const int64_t nb = (int64_t)H.c[c].bw * H.c[c].bh;
+            std::fill(h->h_qsel + d.blk0[c], h->h_qsel + d.blk0[c] + nb, 3 * i + c);
+        }
+        d.rgb_off = rgb_offsets ? rgb_offsets[i] : 0;
+        RC_REQUIRE((int64_t)H.width * H.height < (int64_t)1 << 31, RC_ERR_INVALID, "image too large");
+        maxpix = std::max(maxpix, H.width * H.height);
+    }
+    const int64_t nb = base[n];
+    RC_HIP(hipMemcpyAsync(h->d_coef, h->h_coef, (size_t)nb * 128, hipMemcpyHostToDevice, s));
+    RC_HIP(hipMemcpyAsync(h->d_qsel, h->h_qsel, (size_t)nb * 4, hipMemcpyHostToDevice, s));
+    RC_HIP(hipMemcpyAsync(h->d_qtab, h->h_qtab, (size_t)n * 3 * 128, hipMemcpyHostToDevice, s));
+    RC_HIP(hipMemcpyAsync(h->d_desc, h->h_desc, (size_t)n * sizeof(jpeg::Desc), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(jpeg::jpeg_idct_kernel, dim3((unsigned)((nb + 7) / 8)), dim3(64), 0, s, h->d_coef, h->d_qsel,
+                       h->d_qtab, nb, h->d_planes);
+    RC_LAUNCH_CHECK();
+}
+
+// Pillow coefficients for in_size -> out_size (bounds shifted down by `shift`), built once.
+const rc_jpeg_decoder::Coeffs &resize_coeffs(rc_jpeg_decoder *h, int in_size, int out_size, int resample, int shift) {
+    const auto key = std::make_tuple(in_size, out_size, resample, shift);
+    auto it = h->coeffs.find(key);
+    if (it != h->coeffs.end()) return it->second;
+    ResampleCoeffs c = precompute_coeffs(in_size, out_size, resample);
+    rc_jpeg_decoder::Coeffs d;
+    d.ksize = c.ksize;
+    d.first = c.bounds[0];
+    d.last = c.bounds[2 * (out_size - 1)] + c.bounds[2 * (out_size - 1) + 1];
+    for (int i = 0; i < out_size; ++i) c.bounds[2 * i] -= shift;
+    d.bounds = (int *)dmalloc(c.bounds.size() * sizeof(int));
+    try {
+        d.coef = (int *)dmalloc(c.coef.size() * sizeof(int));
+        RC_HIP(hipMemcpy(d.bounds, c.bounds.data(), c.bounds.size() * sizeof(int), hipMemcpyHostToDevice));
+        RC_HIP(hipMemcpy(d.coef, c.coef.data(), c.coef.size() * sizeof(int), hipMemcpyHostToDevice));
+    } catch (...) {
+        dfree(d.bounds);
+        dfree(d.coef);
+        throw;
+    }
+    return h->coeffs.emplace(key, d).first->second;
+}
+
+}  // namespace
+
 extern "C" int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens,
                               uint8_t *rgb, const int64_t *rgb_offsets, void *stream) {
     return guard([&] {
@@ -669,75 +917,81 @@ extern "C" int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *j
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceScope ds(h->device);
         hipStream_t s = (hipStream_t)stream;
-        // headers first (cheap, serial): geometry, block offsets, capacity check
-        std::vector<jpeg::Header> hd(n);
-        std::vector<int64_t> base(n + 1, 0);
-        for (int i = 0; i < n; ++i) {
-            jpeg::parse(jpgs[i], lens[i], hd[i]);
-            RC_REQUIRE(hd[i].supported, RC_ERR_UNSUPPORTED,
-                       "JPEG " + std::to_string(i) + " not decodable here: " + hd[i].why);
-            base[i + 1] = base[i] + hd[i].blocks;
-        }
-        RC_REQUIRE(base[n] <= h->max_blocks, RC_ERR_INVALID, "batch exceeds the decoder's max_blocks");
-        // the pinned staging is reused: wait for the previous call's upload
-        RC_HIP(hipEventSynchronize(h->staged));
-        // Huffman decode, one image per worker
-        std::vector<std::string> errs(n);
-        auto work = [&](int i) {
-            try {
-                jpeg::decode_coefficients(hd[i], h->h_coef + base[i] * 64);
-            } catch (const std::exception &e) {
-                errs[i] = e.what();
-            }
-        };
-        const int nthreads = std::max(1, std::min<int>(n, huffman_threads()));
-        if (nthreads == 1) {
-            for (int i = 0; i < n; ++i) work(i);
-        } else {
-            std::vector<std::thread> pool;
-            std::atomic<int> next{0};
-            for (int t = 0; t < nthreads; ++t)
-                pool.emplace_back([&] {
-                    for (int i; (i = next.fetch_add(1)) < n;) work(i);
-                });
-            for (auto &t : pool) t.join();
-        }
-        for (int i = 0; i < n; ++i)
-            RC_REQUIRE(errs[i].empty(), RC_ERR_INVALID, "JPEG " + std::to_string(i) + ": " + errs[i]);
+        std::vector<jpeg::Header> hd;
         int maxpix = 0;
-        for (int i = 0; i < n; ++i) {
-            const jpeg::Header &H = hd[i];
-            jpeg::Desc &d = h->h_desc[i];
-            std::memset(&d, 0, sizeof(d));
-            d.W = H.width;
-            d.H = H.height;
-            d.ncomp = H.ncomp;
-            for (int c = 0; c < H.ncomp; ++c) {
-                d.rx[c] = H.hmax / H.c[c].h;
-                d.ry[c] = H.vmax / H.c[c].v;
-                d.dw[c] = (int)(((int64_t)H.width * H.c[c].h + H.hmax - 1) / H.hmax);
-                d.dh[c] = (int)(((int64_t)H.height * H.c[c].v + H.vmax - 1) / H.vmax);
-                d.bw[c] = H.c[c].bw;
-                d.blk0[c] = base[i] + H.c[c].blk0;
-                std::memcpy(h->h_qtab + (int64_t)(3 * i + c) * 64, H.qt[H.c[c].tq], 128);
-                const int64_t nb = (int64_t)H.c[c].bw * H.c[c].bh;
-                std::fill(h->h_qsel + d.blk0[c], h->h_qsel + d.blk0[c] + nb, 3 * i + c);
-            }
-            d.rgb_off = rgb_offsets[i];
-            RC_REQUIRE((int64_t)H.width * H.height < (int64_t)1 << 31, RC_ERR_INVALID, "image too large");
-            maxpix = std::max(maxpix, H.width * H.height);
-        }
-        const int64_t nb = base[n];
-        RC_HIP(hipMemcpyAsync(h->d_coef, h->h_coef, (size_t)nb * 128, hipMemcpyHostToDevice, s));
-        RC_HIP(hipMemcpyAsync(h->d_qsel, h->h_qsel, (size_t)nb * 4, hipMemcpyHostToDevice, s));
-        RC_HIP(hipMemcpyAsync(h->d_qtab, h->h_qtab, (size_t)n * 3 * 128, hipMemcpyHostToDevice, s));
-        RC_HIP(hipMemcpyAsync(h->d_desc, h->h_desc, (size_t)n * sizeof(jpeg::Desc), hipMemcpyHostToDevice, s));
+        stage_idct(h, n, jpgs, lens, rgb_offsets, s, hd, maxpix);
         RC_HIP(hipEventRecord(h->staged, s));
-        hipLaunchKernelGGL(jpeg::jpeg_idct_kernel, dim3((unsigned)((nb + 7) / 8)), dim3(64), 0, s, h->d_coef, h->d_qsel,
-                           h->d_qtab, nb, h->d_planes);
-        RC_LAUNCH_CHECK();
         hipLaunchKernelGGL(jpeg::jpeg_color_kernel, dim3((unsigned)((maxpix + 255) / 256), (unsigned)n), dim3(256), 0, s,
                            h->d_planes, h->d_desc, rgb);
+        RC_LAUNCH_CHECK();
+    });
+}
+
+extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens,
+                                      int out_size, int resample, uint8_t *out, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h && jpgs && lens && out, RC_ERR_INVALID, "null argument");
+        RC_REQUIRE(n >= 0 && n <= h->max_images, RC_ERR_INVALID, "batch exceeds the decoder's max_images");
+        RC_REQUIRE(out_size >= 1 && out_size <= 4096, RC_ERR_INVALID, "out_size must be in [1, 4096]");
+        RC_REQUIRE(resample == RC_RESAMPLE_BICUBIC || resample == RC_RESAMPLE_BILINEAR, RC_ERR_UNSUPPORTED,
+                   "resample must be BICUBIC (3) or BILINEAR (2)");
+        if (n == 0) return;
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        hipStream_t s = (hipStream_t)stream;
+        std::vector<jpeg::Header> hd;
+        int maxpix = 0;
+        stage_idct(h, n, jpgs, lens, nullptr, s, hd, maxpix);
+        const int S = out_size;
+        int64_t tmp_need = 0;
+        int maxrows = 1;
+        for (int i = 0; i < n; ++i) {
+            const int W = hd[i].width, H = hd[i].height;
+            jpeg::RDesc &r = h->h_rdesc[i];
+            std::memset(&r, 0, sizeof(r));
+            r.S = S;
+            r.need_h = W != S;
+            r.need_v = H != S;
+            r.Hs = H;
+            if (r.need_h) {
+                const auto &ch = resize_coeffs(h, W, S, resample, 0);
+                r.hb = ch.bounds;
+                r.hc = ch.coef;
+                r.hk = ch.ksize;
+            }
+            if (r.need_v) {
+                const auto &cv = resize_coeffs(h, H, S, resample, 0);
+                // ImagingResampleInner: the horizontal pass covers just the rows the vertical one reads
+                if (r.need_h) {
+                    r.y0 = cv.first;
+                    r.Hs = cv.last - cv.first;
+                }
+                const auto &cvs = r.y0 != 0 ? resize_coeffs(h, H, S, resample, r.y0) : cv;
+                r.vb = cvs.bounds;
+                r.vc = cvs.coef;
+                r.vk = cvs.ksize;
+                r.tmp_off = tmp_need;
+                tmp_need += (int64_t)r.Hs * S * 3;
+            }
+            r.out_off = (int64_t)i * S * S * 3;
+            maxrows = std::max(maxrows, r.Hs);
+        }
+        if ((size_t)tmp_need > h->tmp_bytes) {  // grows with the largest batch seen; steady state allocates nothing
+            RC_HIP(hipStreamSynchronize(s));
+            dfree(h->d_tmp);
+            h->d_tmp = nullptr;
+            h->tmp_bytes = 0;
+            const size_t want = std::max<size_t>((size_t)tmp_need, 2 * h->tmp_bytes);
+            h->d_tmp = (uint8_t *)dmalloc(want);
+            h->tmp_bytes = want;
+        }
+        RC_HIP(hipMemcpyAsync(h->d_rdesc, h->h_rdesc, (size_t)n * sizeof(jpeg::RDesc), hipMemcpyHostToDevice, s));
+        RC_HIP(hipEventRecord(h->staged, s));
+        hipLaunchKernelGGL(jpeg::jpeg_color_resize_h_kernel, dim3((unsigned)maxrows, (unsigned)n), dim3(256), 0, s,
+                           h->d_planes, h->d_desc, h->d_rdesc, h->d_tmp, out);
+        RC_LAUNCH_CHECK();
+        hipLaunchKernelGGL(jpeg::jpeg_resize_v_kernel, dim3((unsigned)((S * S + 255) / 256), (unsigned)n), dim3(256), 0, s,
+                           h->d_rdesc, h->d_tmp, out);
         RC_LAUNCH_CHECK();
     });
 }

@@ -107,9 +107,11 @@ def _gpu_jpeg(data: bytes) -> bool:
 
 
 def decode_many(blobs: List[bytes]) -> list:
-    """Image bytes → u8 HWC RGB images, validated as the reference validates them: baseline
-    JPEGs decoded on the GPU (device tensors, bit-exact with PIL), anything else — and any
-    stream the GPU decoder rejects — through PIL on the host (``UnidentifiedImageError`` → 400)."""
+    """Image bytes → the embedder's u8 HWC RGB inputs, validated as the reference validates
+    them: baseline JPEGs decoded AND resized to the model's input size on the GPU in one pass
+    (device tensors, bit-exact with PIL decode + the processor's resize), anything else — and
+    any stream the GPU decoder rejects — through PIL on the host at its own size
+    (``UnidentifiedImageError`` → 400), resized later inside rc_embed."""
     import numpy as np
 
     out: list = [None] * len(blobs)
@@ -120,7 +122,7 @@ def decode_many(blobs: List[bytes]) -> list:
         out[i] = np.asarray(decode_image(blobs[i]), dtype=np.uint8)
     if gpu:
         try:
-            for i, im in zip(gpu, get_embedder().decode_jpeg([blobs[i] for i in gpu])):
+            for i, im in zip(gpu, get_embedder().decode_jpeg_for_embed([blobs[i] for i in gpu]).unbind(0)):
                 out[i] = im
         except ValueError:  # a damaged stream: the reference's host decode decides (image or 400)
             for i in gpu:

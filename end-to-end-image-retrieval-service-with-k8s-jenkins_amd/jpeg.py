@@ -104,6 +104,28 @@ class JpegDecoder:
                 outs.append(buf[o:o + z].view(inf.height, inf.width, 3))
         return outs
 
+    def decode_resized(self, datas: Sequence[bytes], size: int, resample: int, stream=None) -> torch.Tensor:
+        """JPEG byte strings (any, mixed sizes) -> device u8 [n, size, size, 3]: the decode followed
+        by Pillow's resample to size x size (ViTImageProcessor's resize), the colour pass fused
+        with the horizontal resample (rc_jpeg_decode_resized); bit-exact with PIL decode +
+        Image.resize."""
+        infos = [probe(d) for d in datas]
+        for i, inf in enumerate(infos):
+            if not inf.supported:
+                raise JpegUnsupported(f"image {i}: JPEG stream outside the GPU decoder's scope")
+        out = torch.empty((len(datas), size, size, 3), dtype=torch.uint8, device=self.device)
+        for s in range(0, len(datas), self.max_images):
+            chunk = datas[s:s + self.max_images]
+            n = len(chunk)
+            ptrs = (C.c_char_p * n)(*chunk)
+            lens = (C.c_int64 * n)(*[len(d) for d in chunk])
+            status = self.lib.rc_jpeg_decode_resized(self._h, n, ptrs, lens, int(size), int(resample),
+                                                     out[s:s + n].data_ptr(), stream_ptr(stream))
+            if status == RC_ERR_UNSUPPORTED:
+                raise JpegUnsupported(self.lib.rc_last_error().decode())
+            check(status)
+        return out
+
     def decode_batch(self, datas: Sequence[bytes], stream=None) -> torch.Tensor:
         """Equal-size JPEGs -> one device u8 [n, H, W, 3] tensor.  Within one chunk the
         images are packed back to back, so the batch is a view of the decode buffer

@@ -280,39 +280,47 @@ class VitMsnEmbedder:
         raw, _ = self.embed_images([np.asarray(im.convert("RGB"), dtype=np.uint8) for im in images])
         return raw.cpu().tolist()
 
-    def decode_jpeg(self, datas: Sequence[bytes]) -> list[torch.Tensor]:
-        """Baseline-JPEG byte strings → device HWC RGB u8 images (rc_jpeg_decode, bit-exact with
-        the reference's PIL decode).  Raises jpeg.JpegUnsupported / ValueError like the decoder."""
+    def _decoder(self):
         from .jpeg import JpegDecoder
 
         if self._jpeg is None:
             self._jpeg = JpegDecoder(self.device, max_images=max(self.max_batch, 32), max_pixels=1 << 24)
-        return self._jpeg.decode(datas)
+        return self._jpeg
+
+    def decode_jpeg(self, datas: Sequence[bytes]) -> list[torch.Tensor]:
+        """Baseline-JPEG byte strings → device HWC RGB u8 images at their own size (rc_jpeg_decode,
+        bit-exact with the reference's PIL decode).  Raises jpeg.JpegUnsupported / ValueError."""
+        return self._decoder().decode(datas)
+
+    def decode_jpeg_for_embed(self, datas: Sequence[bytes]) -> torch.Tensor:
+        """Baseline-JPEG byte strings (any sizes) → device u8 [n, S, S, 3], the model's input:
+        decode fused with the processor's resize (rc_jpeg_decode_resized, bit-exact with PIL
+        decode + Image.resize); rc_embed then runs no resize."""
+        S = self.config["image_size"]
+        return self._decoder().decode_resized(datas, S, int(self.preprocess_params["resample"]))
 
     def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
-        """Baseline-JPEG byte strings → raw CLS vectors, decoded on the GPU and embedded without a
-        host RGB copy.  Raises jpeg.JpegUnsupported for streams the GPU decoder does not handle."""
-        raw, _ = self.embed_images(self.decode_jpeg(datas))
+        """Baseline-JPEG byte strings → raw CLS vectors, decoded (and resized) on the GPU and
+        embedded without a host RGB copy.  Raises jpeg.JpegUnsupported for streams the GPU
+        decoder does not handle."""
+        raw, _ = self.embed_images(list(self.decode_jpeg_for_embed(datas).unbind(0)))
         return raw.cpu().tolist()
 
     def embed_jpeg_stream(self, batches: Iterable[Sequence[bytes]], normalized: bool = True):
-        """Pipelined JPEG bytes → embeddings for a stream of equal-size-image batches
-        (bulk ingest): batch i+1 is Huffman-decoded on a host worker thread and
-        reconstructed on a side stream while the GPU embeds batch i.  Yields
-        (raw, normed) device tensors per batch (valid until the next iteration)."""
+        """Pipelined JPEG bytes → embeddings for a stream of batches (bulk ingest; images of any
+        sizes): batch i+1 is Huffman-decoded on a host worker thread and reconstructed +
+        resized on a side stream (rc_jpeg_decode_resized) while the GPU embeds batch i.
+        Yields (raw, normed) device tensors per batch (valid until the next iteration)."""
         import concurrent.futures as cf
 
-        from .jpeg import JpegDecoder
-
-        if self._jpeg is None:
-            self._jpeg = JpegDecoder(self.device, max_images=max(self.max_batch, 32), max_pixels=1 << 24)
-        dec = self._jpeg
+        dec = self._decoder()
+        S, resample = self.config["image_size"], int(self.preprocess_params["resample"])
         side = torch.cuda.Stream(device=self.device)
         main = torch.cuda.current_stream(self.device)
 
         def decode(datas):
             with torch.cuda.device(self.device), torch.cuda.stream(side):
-                x = dec.decode_batch(datas, stream=side)
+                x = dec.decode_resized(datas, S, resample, stream=side)
                 ev = torch.cuda.Event()
                 ev.record(side)
             return x, ev
@@ -476,12 +484,15 @@ class EmbedderPool:
         return raw.cpu().tolist()
 
     def decode_jpeg(self, datas: Sequence[bytes]) -> list[torch.Tensor]:
-        """Decoded on the first member's GPU (the host Huffman pass is the shared cost; the
-        slices move to their members inside embed_parts, 150 KB per 224x224 image)."""
         return self.members[0].decode_jpeg(datas)
 
+    def decode_jpeg_for_embed(self, datas: Sequence[bytes]) -> torch.Tensor:
+        """Decoded + resized on the first member's GPU (the host Huffman pass is the shared
+        cost; the slices move to their members inside embed_parts, 150 KB per image)."""
+        return self.members[0].decode_jpeg_for_embed(datas)
+
     def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
-        raw, _ = self.embed_images(self.decode_jpeg(datas))
+        raw, _ = self.embed_images(list(self.decode_jpeg_for_embed(datas).unbind(0)))
         return raw.cpu().tolist()
 
     def preprocess(self, images_u8: torch.Tensor, stream=None) -> torch.Tensor:

@@ -322,6 +322,14 @@ int rc_jpeg_decoder_destroy(rc_jpeg_decoder *h);
  * handles (probe first), RC_ERR_INVALID for damaged or truncated data. */
 int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens, uint8_t *rgb,
                    const int64_t *rgb_offsets, void *stream);
+/* Decode n JPEGs (any sizes, mixed) straight to out_size x out_size: the decode above
+ * followed by Pillow's resample (`resample` = RC_RESAMPLE_BICUBIC / _BILINEAR, the
+ * ViTImageProcessor resize of embedding/main.py:107), with the colour pass fused into
+ * the horizontal resample (the full-size RGB image is never written).  out: device u8
+ * [n][out_size][out_size][3], bit-exact with PIL decode + Image.resize.  A horizontal
+ * pass buffer grows with the largest batch seen (no allocation once warm). */
+int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens, int out_size,
+                           int resample, uint8_t *out, void *stream);
 
 #ifdef __cplusplus
 }

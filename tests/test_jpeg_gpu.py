@@ -101,3 +101,62 @@ def test_decode_batch_is_a_packed_view(dec):
     assert np.array_equal(y[dec.max_images + 1].cpu().numpy(), pil_rgb(datas[(dec.max_images + 1) % 6]))
     with pytest.raises(ValueError):
         dec.decode_batch([datas[0], synthetic(32, 32, 1)])
+
+
+def _pil_resized(data, size=224, resample=3):
+    """PIL decode (embedding/main.py:97) + the processor's resize (ViTImageProcessorPil, :107)."""
+    import io
+
+    from PIL import Image
+
+    im = Image.open(io.BytesIO(data)).convert("RGB")
+    return np.asarray(im.resize((size, size), resample)) if im.size != (size, size) else np.asarray(im)
+
+
+@pytest.mark.parametrize("resample", [3, 2])
+def test_decode_resized_bit_exact_mixed_sizes(dec, resample):
+    """rc_jpeg_decode_resized (colour pass fused with the horizontal resample, per-image vertical
+    pass) == PIL decode + Image.resize, for every stream of the decode cases in ONE mixed batch
+    (up- and downscale on either axis, one axis already 224, grayscale, 4:4:4 / 4:2:2 / 4:2:0)."""
+    cs = cases()
+    got = dec.decode_resized([d for _, d in cs], 224, resample)
+    for (name, data), g in zip(cs, got):
+        assert np.array_equal(g.cpu().numpy(), _pil_resized(data, 224, resample)), name
+
+
+def test_decode_resized_wide_rows_and_reuse(J, cuda):
+    """Rows wider than one LDS window (16384 px: several windows per row), a tall image, the
+    reference fixture's 168 x 300, and repeated calls reusing the staging and the h-pass buffer."""
+    d = J.JpegDecoder(device=0, max_images=8, max_pixels=1 << 22)
+    datas = [synthetic(17000, 12, 41, quality=90, subsampling=2), synthetic(40, 3000, 42, quality=90, subsampling=1),
+             dict(cases())["test_image"], synthetic(224, 224, 43, quality=95, subsampling=0)]
+    for _ in range(2):
+        got = d.decode_resized(datas, 224, 3)
+        got2 = d.decode_resized(datas[::-1], 224, 3)
+        for x, data in zip(got, datas):
+            assert np.array_equal(x.cpu().numpy(), _pil_resized(data))
+        for x, data in zip(got2, datas[::-1]):
+            assert np.array_equal(x.cpu().numpy(), _pil_resized(data))
+    d.close()
+
+
+def test_fused_decode_embedding_equals_pil_path(cuda):
+    """Embedding of the fused decode→resize equals the embedding of PIL-decoded pixels resized on
+    the device (rc_embed's resize): the bulk stream and the per-request path use the fused one."""
+    import torch
+
+    vit = import_pkg("vit")
+    from oracle.weights import seeded_vit_msn_weights
+
+    m = vit.VitMsnEmbedder(seeded_vit_msn_weights(1907, num_layers=2), device=0, max_batch=8)
+    batches = [[synthetic(168, 300, 700 + 8 * b + i, quality=90, subsampling=2) for i in range(8)] for b in range(3)]
+    got = [raw.clone() for raw, _ in m.embed_jpeg_stream(batches)]
+    for b, datas in enumerate(batches):
+        ref, _ = m.embed(torch.from_numpy(np.stack([pil_rgb(d) for d in datas])))
+        assert torch.equal(got[b], ref)
+    mixed = [synthetic(168, 300, 800, quality=90), synthetic(224, 224, 801, quality=90), synthetic(640, 480, 802)]
+    raw = torch.tensor(m.embed_jpeg(mixed))
+    for i, data in enumerate(mixed):
+        ref, _ = m.embed(torch.from_numpy(pil_rgb(data).copy())[None])
+        assert torch.equal(raw[i], ref[0].cpu())
+    m.close()
