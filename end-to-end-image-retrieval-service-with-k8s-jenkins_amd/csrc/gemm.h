@@ -896,9 +896,14 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     const int b = m / np, pi = m - b * np, py = pi / gp, px = pi - py * gp;
     const uint8_t *abase = a.img + (((int64_t)b * S + py * P) * S + px * P) * 3;
     const int arow_stride = S * 3;
-    // W: lane = row n0 + tid, its 64 bytes of the step
-    const uint16_t *wrow = a.W + (int64_t)(n0 + tid) * KC;
-    const int asw = ((ar >> 3) & 1) << 1, wsw = ((tid >> 3) & 1) << 1;  // chunk XOR of the fragment layout
+    // W: thread t stages 16-B chunk (t & 3) of rows (t >> 2) + 64 i, i = 0..3: four lanes
+    // cover a 64-B row, so each ds_write_b128 of a wave writes 16 rows x 64 B whole —
+    // conflict-free (one row per lane wrote 4 rows at a 64-B stride into the same banks:
+    // 2-way conflicts on every W store, 46 % of the kernel's LDS cycles, r03b PMC)
+    const int wch = tid & 3, wr0 = tid >> 2;
+    const uint16_t *wrow = a.W + (int64_t)(n0 + wr0) * KC + wch * 8;
+    const int asw = ((ar >> 3) & 1) << 1, wsw = ((wr0 >> 3) & 1) << 1;  // chunk XOR of the fragment layout
+                                                                     // (rows wr0 + 64 i share bit 3)
 
     // register staging two K-steps ahead: set R holds step kt + 2 while step kt + 1's
     // set is written to LDS, so each global load has two steps of MFMAs to land
@@ -910,7 +915,7 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
         const int ky = k0 / (3 * P), off = k0 - ky * (3 * P);
         r.av = *reinterpret_cast<const uint4 *>(abase + ky * arow_stride + off);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) r.wv[c] = *reinterpret_cast<const uint4 *>(wrow + kt * BK + 8 * c);
+        for (int i = 0; i < 4; ++i) r.wv[i] = *reinterpret_cast<const uint4 *>(wrow + (int64_t)64 * i * KC + kt * BK);
     };
     auto store = [&](int slot, int kt, const Regs &r) {
         uint8_t *As = smem + slot * SLOT;
@@ -937,7 +942,7 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
         *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah) ^ asw) << 4)) = make_uint4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<uint4 *>(As + ar * 64 + (((2 * ah + 1) ^ asw) << 4)) = make_uint4(o[4], o[5], o[6], o[7]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4 *>(Ws + tid * 64 + ((c ^ wsw) << 4)) = r.wv[c];
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(Ws + (wr0 + 64 * i) * 64 + ((wch ^ wsw) << 4)) = r.wv[i];
     };
     const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
 

@@ -603,7 +603,7 @@ __global__ __launch_bounds__(256) void jpeg_color_resize_h_kernel(const uint8_t 
                                                                  const RDesc *__restrict__ rdescs, uint8_t *__restrict__ tmp,
                                                                  uint8_t *__restrict__ out) {
     __shared__ uint8_t row[RS_WIN * 3];
-    __shared__ int span[2];
+    __shared__ int span[2];  // [1]: the end of the current window's outputs
     const Desc d = descs[blockIdx.y];
     const RDesc r = rdescs[blockIdx.y];
     const int y = blockIdx.x;
@@ -621,15 +621,19 @@ __global__ __launch_bounds__(256) void jpeg_color_resize_h_kernel(const uint8_t 
         return;
     }
     for (int xo0 = 0; xo0 < S;) {
-        if (threadIdx.x == 0) {  // outputs [xo0, xo1) whose taps fit one window from xmin(xo0)
-            const int w0 = r.hb[2 * xo0];
-            int xo1 = xo0 + 1;
-            while (xo1 < S && r.hb[2 * xo1] + r.hb[2 * xo1 + 1] <= w0 + RS_WIN) ++xo1;
-            span[0] = w0;
-            span[1] = xo1;
+        // outputs [xo0, xo1) whose taps fit one window starting at xmin(xo0): the first output
+        // past it, found by every lane testing its outputs at once (a min over the block);
+        // a row of <= RS_WIN pixels is one window
+        const int w0 = r.hb[2 * xo0];
+        int xo1 = S;
+        if (d.W - w0 > RS_WIN) {
+            if (threadIdx.x == 0) span[1] = S;
+            __syncthreads();
+            for (int xo = xo0 + 1 + (int)threadIdx.x; xo < S; xo += 256)
+                if (r.hb[2 * xo] + r.hb[2 * xo + 1] > w0 + RS_WIN) atomicMin(&span[1], xo);
+            __syncthreads();
+            xo1 = span[1];
         }
-        __syncthreads();
-        const int w0 = span[0], xo1 = span[1];
         const int w1 = min(d.W, w0 + RS_WIN);
         for (int x = w0 + (int)threadIdx.x; x < w1; x += 256) {
             int R, G, B;
