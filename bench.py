@@ -43,6 +43,7 @@ PKG = "end-to-end-image-retrieval-service-with-k8s-jenkins_amd"
 METRIC = "top-k queries/s over 1B×512 index + embed images/s; % HBM/MFMA roofline"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E spec
+PEAK_I8_TOPS = 5000.0       # MI355X dense int8 MFMA: 2x bf16 (16x16x64 in the cycles of bf16 16x16x32)
 
 
 def log(*a):
@@ -836,39 +837,65 @@ def main():
                          "bytes_per_launch": scan_bytes / max(scan_n, 1)},
         }
         # config 4 as named: a batch of 1024 queries, top-100, batched MFMA path
-        # (staged filter GEMM + exact rescoring per shard, RCCL all-gather + merge)
+        # (staged filter GEMM + exact rescoring per shard, RCCL all-gather + merge), first
+        # with the f16 filter on the stored rows, then with the int8 filter copy
         nqb, kb = args.batch_queries, 100
         gqb = torch.Generator(device=dev).manual_seed(6)
         qbatch = torch.randn((nqb, dim), device=dev, generator=gqb)
-        sidx.search(qbatch, kb, mode="mfma")
-        torch.cuda.synchronize()
-        shard.timing(True)
-        shard.gemm_timing_read()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.batch_reps):
+
+        def batched_run(tag):
             sidx.search(qbatch, kb, mode="mfma")
+            torch.cuda.synchronize()
+            shard.timing(True)
+            shard.gemm_timing_read()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.batch_reps):
+                out = sidx.search(qbatch, kb, mode="mfma")
+            torch.cuda.synchronize()
+            barrier()
+            bel = max_over_ranks(time.perf_counter() - t0)
+            g_ms, g_n, g_flops, g_fb = shard.gemm_timing_read()
+            shard.timing(False)
+            g_tf = g_flops / (g_ms / 1e3) / 1e12 if g_ms > 0 else 0.0
+            i8 = tag == "i8"
+            peak = PEAK_I8_TOPS if i8 else PEAK_BF16_TFLOPS
+            kern = ("filter_i8_kernel<4> (int8 copy of the rows: 256 queries per block, 32 per wave in registers x "
+                    "128-row tiles, 8-step LDS ring, per-row scale + residual-norm bound epilogue)" if i8 else
+                    "filter_qs_kernel<f16,8,0> (256 queries per block, 32 per wave in registers x 128-row tiles, "
+                    "8-step LDS ring, candidate epilogue)")
+            return out, {
+                "value": nqb * args.batch_reps / bel,
+                "unit": "queries/s",
+                "ms_per_batch": bel / args.batch_reps * 1e3,
+                "filter": ("int8 copy (rc_index_set_filter(RC_FILTER_I8)); candidates rescored exactly on the fp16 rows"
+                           if i8 else "fp16 stored rows"),
+                "roofline": {"kernel": kern, "bound": "mfma", "achieved": g_tf, "peak": peak,
+                             "unit": "TOP/s" if i8 else "TFLOP/s", "frac": g_tf / peak,
+                             "traffic": load_profile_traffic("filter_i8" if i8 else "filter_f16"),
+                             "avg_launch_ms": g_ms / max(g_n, 1), "launches": g_n,
+                             "ops_per_batch": g_flops / max(args.batch_reps, 1)},
+                "gemm_share_of_batch": (g_ms / args.batch_reps) / (bel / args.batch_reps * 1e3),
+                "exact_fallbacks": g_fb,
+            }
+
+        (s_f16, r_f16), native = batched_run("f16")
+        t0 = time.perf_counter()
+        shard.set_filter("i8")  # quantises the shard's rows once (int8 copy + per-row scale / bound)
         torch.cuda.synchronize()
-        barrier()
-        bel = max_over_ranks(time.perf_counter() - t0)
-        g_ms, g_n, g_flops, g_fb = shard.gemm_timing_read()
-        shard.timing(False)
-        g_tf = g_flops / (g_ms / 1e3) / 1e12 if g_ms > 0 else 0.0
+        quant_s = time.perf_counter() - t0
+        (s_i8, r_i8), best = batched_run("i8")
+        same = bool(torch.equal(r_f16, r_i8) and torch.equal(s_f16, s_i8))
+        if rank == 0:
+            log(f"bench: batched f16 {native['value']:.0f} q/s, int8 filter {best['value']:.0f} q/s, identical={same}")
         result["search"]["batched"] = {
             "workload": f"BASELINE config 4: {rows * world:,} x 512 fp16 rows ({rows:,}/GPU), batch of {nqb} queries, exact top-{kb}",
-            "value": nqb * args.batch_reps / bel,
-            "unit": "queries/s",
-            "ms_per_batch": bel / args.batch_reps * 1e3,
-            "roofline": {"kernel": ("filter_qs_kernel<f16,8,4> (256 queries per block, 64 per wave in AGPRs x 64-row tiles, 16-step LDS ring, candidate epilogue)"
-                                    if os.environ.get("RC_FILTER_QT") == "4" else
-                                    "filter_qs_kernel<f16,8,2> (256 queries per block, 32 per wave in registers x 128-row tiles, 8-step LDS ring, candidate epilogue)"),
-                         "bound": "mfma", "achieved": g_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": g_tf / PEAK_BF16_TFLOPS, "traffic": load_profile_traffic("filter_f16"),
-                         "avg_launch_ms": g_ms / max(g_n, 1), "launches": g_n,
-                         "flops_per_batch": g_flops / max(args.batch_reps, 1)},
-            "gemm_share_of_batch": (g_ms / args.batch_reps) / (bel / args.batch_reps * 1e3),
-            "exact_fallbacks": g_fb,
+            **best,
+            "identical_to_f16_filter": same,
+            "quantise_seconds": quant_s,
+            "f16_filter": native,
         }
+        shard.set_filter("native")
         sidx.close()
         del shard, sidx
         torch.cuda.empty_cache()

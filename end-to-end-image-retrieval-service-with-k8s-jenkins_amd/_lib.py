@@ -30,6 +30,8 @@ RC_TOPK_MAX = 256
 RC_SEARCH_AUTO, RC_SEARCH_SCAN, RC_SEARCH_MFMA = 0, 1, 2
 SEARCH_MODES = {"auto": RC_SEARCH_AUTO, "scan": RC_SEARCH_SCAN, "mfma": RC_SEARCH_MFMA}
 DTYPES = {"float32": RC_F32, "f32": RC_F32, "float16": RC_F16, "f16": RC_F16, "bfloat16": RC_BF16, "bf16": RC_BF16}
+RC_FILTER_NATIVE, RC_FILTER_I8 = 0, 1
+FILTERS = {"native": RC_FILTER_NATIVE, "i8": RC_FILTER_I8}
 
 
 class RetrievalCoreError(RuntimeError):
@@ -104,6 +106,9 @@ SIGNATURES = {
     "rc_topk_merge": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "rc_index_set_row_map": (C.c_int, [_vp, _i64, _i64]),
     "rc_index_grow": (C.c_int, [_vp, _i64, _vp]),
+    "rc_index_set_filter": (C.c_int, [_vp, _i32, _vp]),
+    "rc_index_get_filter": (C.c_int, [_vp, _pi32]),
+    "rc_sharded_set_filter": (C.c_int, [_vp, _i32]),
     "rc_sharded_create": (C.c_int, [_i32, _pi32, _i32, _i32, _i64, C.POINTER(_vp)]),
     "rc_sharded_destroy": (C.c_int, [_vp]),
     "rc_sharded_info": (C.c_int, [_vp, _pi32, _pi64, _pi64]),

@@ -94,6 +94,42 @@ __global__ __launch_bounds__(256) void fill_random_kernel(T *__restrict__ rows, 
     }
 }
 
+// The int8 filter copy (search_mfma.hip, filter_i8_kernel): one wave per stored row x̂,
+// sx = max|x̂| / 127, x8 = rne(x̂ / sx) clamped to [-127, 127], ex = ||x̂ - sx·x8||₂ rounded
+// up (x1.001 covers the f32 sum of squares, +1e-7 the f32 residuals), sx and ex at
+// i8_slot(row).  Rows come from slots[v] (upsert) or row0 + v (fill / import / enable).
+template <typename T>
+__global__ __launch_bounds__(256) void quantize_rows_kernel(const T *__restrict__ rows, int64_t ld,
+                                                           const int64_t *__restrict__ slots, int64_t row0, int64_t n,
+                                                           int64_t cap, int8_t *__restrict__ rows8, float *__restrict__ rsx,
+                                                           float *__restrict__ rex) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < n; v += nw) {
+        const int64_t r = slots ? slots[v] : row0 + v;
+        if (r < 0 || r >= cap) continue;  // wave-uniform
+        const T *src = rows + r * ld;
+        float mx = 0.f;
+        for (int c = lane; c < ld; c += 64) mx = fmaxf(mx, fabsf(Elem<T>::load(src, c)));
+        mx = wave_max(mx);
+        const float s = mx * (1.0f / 127.0f), is = mx > 0.f ? 127.0f / mx : 0.f;
+        float e = 0.f;
+        int8_t *dst = rows8 + r * ld;
+        for (int c = lane; c < ld; c += 64) {
+            const float x = Elem<T>::load(src, c);
+            const float q = fminf(127.f, fmaxf(-127.f, rintf(x * is)));
+            dst[c] = (int8_t)q;
+            const float d = x - s * q;
+            e = fmaf(d, d, e);
+        }
+        e = wave_sum(e);
+        if (lane == 0) {
+            rsx[i8_slot(r)] = s;
+            rex[i8_slot(r)] = sqrtf(e) * 1.001f + 1e-7f;
+        }
+    }
+}
+
 // queries [nq, dim] f32 → normalised, zero-padded [nq, ld]
 // rows >= nq (padding up to a multiple of the scan's queries-per-pass) are zero.
 __global__ __launch_bounds__(64) void normalize_queries_kernel(const float *__restrict__ q, int nq, int dim, int64_t ld,
@@ -236,6 +272,10 @@ struct rc_index {
     int64_t row_stride = 1;
     void *rows = nullptr;
     float *norms = nullptr;
+    // int8 filter copy (RC_FILTER_I8): [cap_pad][ld] x8, sx / ex [cap_pad] at i8_slot(row)
+    int filter = RC_FILTER_NATIVE;
+    int8_t *rows8 = nullptr;
+    float *rsx = nullptr, *rex = nullptr;
     // search workspace
     int ws_nq = 0, ws_k = 0, ws_nblk = 0;
     float *qn = nullptr;
@@ -278,12 +318,34 @@ void ensure_workspace(rc_index *h, int nq, int k) {
     h->ws_k = k2;
 }
 
+int64_t cap_pad(int64_t capacity) { return (capacity + INDEX_ROW_PAD - 1) / INDEX_ROW_PAD * INDEX_ROW_PAD; }
+
+// refresh the int8 filter copy of rows slots[0..n) (or row0 .. row0 + n) after a write
+template <typename T>
+void launch_quantize(rc_index *h, const int64_t *slots, int64_t row0, int64_t n, hipStream_t s) {
+    if (h->rows8 == nullptr || n == 0) return;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 256 * 32);
+    hipLaunchKernelGGL(quantize_rows_kernel<T>, dim3(grid), dim3(256), 0, s, (const T *)h->rows, h->ld, slots, row0, n,
+                       h->capacity, h->rows8, h->rsx, h->rex);
+    RC_LAUNCH_CHECK();
+}
+
+void free_filter(rc_index *h) {
+    dfree(h->rows8);
+    dfree(h->rsx);
+    dfree(h->rex);
+    h->rows8 = nullptr;
+    h->rsx = h->rex = nullptr;
+    h->filter = RC_FILTER_NATIVE;
+}
+
 template <typename T>
 void launch_upsert(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *slots, hipStream_t s) {
     const unsigned grid = (unsigned)((n + 3) / 4);
     hipLaunchKernelGGL(upsert_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, vecs, src_idx,
                        slots, n, h->capacity);
     RC_LAUNCH_CHECK();
+    launch_quantize<T>(h, slots, 0, n, s);
 }
 
 template <typename T>
@@ -301,6 +363,7 @@ void launch_fill(rc_index *h, uint64_t seed, int64_t row0, int64_t n, hipStream_
     if (grid == 0) return;
     hipLaunchKernelGGL(fill_random_kernel<T>, dim3(grid), dim3(256), 0, s, (T *)h->rows, h->norms, h->ld, h->dim, seed, row0, n);
     RC_LAUNCH_CHECK();
+    launch_quantize<T>(h, nullptr, row0, n, s);
 }
 
 void launch_scan(rc_index *h, const ScanArgs &a) {
@@ -373,6 +436,9 @@ void batched_search_exact(rc_index *h, const float *queries, int nq, int64_t n_r
                           int64_t *out_rows, hipStream_t s) {
     h->bws.ensure(nq, k, h->ld, (int)dtype_size(h->dtype));
     BatchPlan p{h->rows, h->dtype, h->dim, h->nch, h->ld, n_rows, h->row_base, h->row_stride, queries, nq, k, scores, out_rows};
+    p.rows8 = h->rows8;
+    p.rsx = h->rsx;
+    p.rex = h->rex;
     if (h->gtimer.enabled) h->gtimer.create();
     batched_search(p, h->bws, s, h->gtimer.enabled ? &h->gtimer : nullptr);
     int nblk = (int)std::min<int64_t>(h->bws.fb_blocks, std::max<int64_t>(1, (n_rows + 511) / 512));
@@ -461,6 +527,7 @@ int rc_index_destroy(rc_index *h) {
         h->timer.destroy();
         h->gtimer.destroy();
         h->bws.release();
+        free_filter(h);
         dfree(h->rows);
         dfree(h->norms);
         dfree(h->qn);
@@ -514,16 +581,33 @@ int rc_index_grow(rc_index *h, int64_t new_capacity, void *stream) {
         const int64_t new_pad = (new_capacity + INDEX_ROW_PAD - 1) / INDEX_ROW_PAD * INDEX_ROW_PAD;
         void *rows = dmalloc((size_t)new_pad * rb);
         float *norms = nullptr;
+        int8_t *rows8 = nullptr;
+        float *rsx = nullptr, *rex = nullptr;
         try {
             norms = (float *)dmalloc((size_t)new_capacity * sizeof(float));
             RC_HIP(hipMemcpyAsync(rows, h->rows, (size_t)old_pad * rb, hipMemcpyDeviceToDevice, s));
             RC_HIP(hipMemsetAsync((uint8_t *)rows + (size_t)old_pad * rb, 0, (size_t)(new_pad - old_pad) * rb, s));
             RC_HIP(hipMemcpyAsync(norms, h->norms, (size_t)h->capacity * sizeof(float), hipMemcpyDeviceToDevice, s));
             RC_HIP(hipMemsetAsync(norms + h->capacity, 0, (size_t)(new_capacity - h->capacity) * sizeof(float), s));
+            if (h->rows8) {  // the filter copy keeps its slots (i8_slot is position-stable)
+                const size_t rb8 = (size_t)h->ld;
+                rows8 = (int8_t *)dmalloc((size_t)new_pad * rb8);
+                rsx = (float *)dmalloc((size_t)new_pad * sizeof(float));
+                rex = (float *)dmalloc((size_t)new_pad * sizeof(float));
+                RC_HIP(hipMemcpyAsync(rows8, h->rows8, (size_t)old_pad * rb8, hipMemcpyDeviceToDevice, s));
+                RC_HIP(hipMemsetAsync(rows8 + (size_t)old_pad * rb8, 0, (size_t)(new_pad - old_pad) * rb8, s));
+                RC_HIP(hipMemcpyAsync(rsx, h->rsx, (size_t)old_pad * sizeof(float), hipMemcpyDeviceToDevice, s));
+                RC_HIP(hipMemsetAsync(rsx + old_pad, 0, (size_t)(new_pad - old_pad) * sizeof(float), s));
+                RC_HIP(hipMemcpyAsync(rex, h->rex, (size_t)old_pad * sizeof(float), hipMemcpyDeviceToDevice, s));
+                RC_HIP(hipMemsetAsync(rex + old_pad, 0, (size_t)(new_pad - old_pad) * sizeof(float), s));
+            }
             RC_HIP(hipStreamSynchronize(s));  // work queued earlier on other streams is the caller's to order
         } catch (...) {
             dfree(rows);
             dfree(norms);
+            dfree(rows8);
+            dfree(rsx);
+            dfree(rex);
             throw;
         }
         RC_HIP(hipDeviceSynchronize());  // no kernel may still read the old buffers
@@ -531,6 +615,14 @@ int rc_index_grow(rc_index *h, int64_t new_capacity, void *stream) {
         dfree(h->norms);
         h->rows = rows;
         h->norms = norms;
+        if (h->rows8) {
+            dfree(h->rows8);
+            dfree(h->rsx);
+            dfree(h->rex);
+            h->rows8 = rows8;
+            h->rsx = rsx;
+            h->rex = rex;
+        }
         h->capacity = new_capacity;
     });
 }
@@ -542,6 +634,46 @@ int rc_index_reserve(rc_index *h, int max_nq, int max_k) {
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceScope ds(h->device);
         ensure_workspace(h, max_nq, max_k);
+    });
+}
+
+int rc_index_set_filter(rc_index *h, int kind, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(kind == RC_FILTER_NATIVE || kind == RC_FILTER_I8, RC_ERR_INVALID, "filter must be RC_FILTER_NATIVE or RC_FILTER_I8");
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceScope ds(h->device);
+        hipStream_t s = (hipStream_t)stream;
+        if (kind == h->filter) return;
+        if (kind == RC_FILTER_NATIVE) {
+            RC_HIP(hipDeviceSynchronize());  // no search may still read the copy
+            free_filter(h);
+            return;
+        }
+        RC_REQUIRE(i8_filter_supported(h->ld), RC_ERR_UNSUPPORTED,
+                   "the int8 filter needs a row width (dim rounded up to 128) of 256 or 512");
+        const int64_t pad = cap_pad(h->capacity);
+        try {
+            h->rows8 = (int8_t *)dmalloc((size_t)pad * h->ld);
+            h->rsx = (float *)dmalloc((size_t)pad * sizeof(float));
+            h->rex = (float *)dmalloc((size_t)pad * sizeof(float));
+            RC_HIP(hipMemsetAsync(h->rows8, 0, (size_t)pad * h->ld, s));
+            RC_HIP(hipMemsetAsync(h->rsx, 0, (size_t)pad * sizeof(float), s));
+            RC_HIP(hipMemsetAsync(h->rex, 0, (size_t)pad * sizeof(float), s));
+            dispatch_dtype(h->dtype, [&](auto t) { launch_quantize<decltype(t)>(h, nullptr, 0, h->capacity, s); });
+            RC_HIP(hipStreamSynchronize(s));
+        } catch (...) {
+            free_filter(h);
+            throw;
+        }
+        h->filter = RC_FILTER_I8;
+    });
+}
+
+int rc_index_get_filter(const rc_index *h, int *kind) {
+    return guard([&] {
+        RC_REQUIRE(h && kind, RC_ERR_INVALID, "null argument");
+        *kind = h->filter;
     });
 }
 
@@ -618,6 +750,7 @@ int rc_index_import(rc_index *h, int64_t row0, int64_t n, const void *rows_in, c
         hipStream_t s = (hipStream_t)stream;
         RC_HIP(hipMemcpyAsync((uint8_t *)h->rows + (size_t)row0 * rb, rows_in, (size_t)n * rb, hipMemcpyDefault, s));
         RC_HIP(hipMemcpyAsync(h->norms + row0, norms_in, (size_t)n * sizeof(float), hipMemcpyDefault, s));
+        dispatch_dtype(h->dtype, [&](auto t) { launch_quantize<decltype(t)>(h, nullptr, row0, n, s); });
     });
 }
 
@@ -644,8 +777,9 @@ int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows
             empty_search(nq, k, scores, out_rows, s);
             return;
         }
-        const bool mfma_ok = h->dtype != RC_F32;
-        RC_REQUIRE(mode != RC_SEARCH_MFMA || mfma_ok, RC_ERR_UNSUPPORTED, "batched MFMA search needs an f16/bf16 index");
+        const bool mfma_ok = h->dtype != RC_F32 || h->rows8 != nullptr;
+        RC_REQUIRE(mode != RC_SEARCH_MFMA || mfma_ok, RC_ERR_UNSUPPORTED,
+                   "batched MFMA search needs an f16/bf16 index or the int8 filter copy");
         const bool use_mfma = mode == RC_SEARCH_MFMA ||
                               (mode == RC_SEARCH_AUTO && mfma_ok && nq >= kBatchMinQueries && n_rows >= kBatchMinRows);
         if (!use_mfma) {

@@ -114,6 +114,8 @@ struct BatchWs {
     uint32_t *cand = nullptr;   // [nq_cap][cap] candidate rows
     uint64_t *keys = nullptr;   // [nq_cap][k_cap] running top-k keys (sorted)
     int *flags = nullptr;       // [nq_cap] 1 = candidate overflow, exact fallback needed
+    float *sq = nullptr;        // [nq_cap] int8 filter: query scale (q̃ = sq · q8)
+    float *aq = nullptr;        // [nq_cap] int8 filter: coefficient of a row's residual norm in the bound
     int *ovf = nullptr;         // overflowed queries since the last timing read (device counter)
     int fb_blocks = 0;               // blocks of the fallback scan: FB_BUDGET_BYTES / (nq_cap * k_cap * 8), clamped
     uint64_t *fb_partial = nullptr;  // [fb_blocks][nq_cap][k_cap] partial keys of the exact fallback scan
@@ -135,11 +137,23 @@ struct BatchPlan {
     int k;
     float *out_scores;
     int64_t *out_rows;
+    // int8 filter copy of the rows (rc_index_set_filter(RC_FILTER_I8)), or null
+    const int8_t *rows8 = nullptr;  // [cap_pad][ld] x8, x̃ = sx · x8
+    const float *rsx = nullptr;     // [cap_pad] sx, at i8_slot(row)
+    const float *rex = nullptr;     // [cap_pad] ||x̂ - x̃||₂ (rounded up), at i8_slot(row)
 };
+
+// The int8 filter keeps a row's scale and residual norm at a tile-transposed slot:
+// within each 128-row tile, row 16·rf + li sits at 8·li + rf, so the filter lane that
+// holds rows {16·rf + li : rf} reads its 8 values as two 16-B loads.
+__host__ __device__ __forceinline__ int64_t i8_slot(int64_t row) {
+    return (row & ~int64_t(127)) + (row & 15) * 8 + ((row & 127) >> 4);
+}
+bool i8_filter_supported(int64_t ld);  // row widths filter_i8_kernel is instantiated for
 
 // Enqueue the staged filter-GEMM / rescore search on `s` (no host sync).
 void batched_search(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer);
-int batch_stage_ratio(int k, int cap);
+int batch_stage_ratio(int k, int cap, int inflation = 1);
 
 #if defined(SCAN_INSTANTIATE)
 // qn holds nq_total (a multiple of QB) query rows, zero beyond the caller's

@@ -101,6 +101,8 @@ struct FilterArgs {
     uint32_t *cnt;     // [nqb*256]
     uint32_t *cand;    // [nqb*256][cap]
     int cap;
+    // int8 filter only (filter_i8_kernel): per-row sx / ex at i8_slot(row), per-query sq / aq
+    const float *rsx = nullptr, *rex = nullptr, *sq = nullptr, *aq = nullptr;
 };
 
 // 256x256x64 tile, 512 threads = 8 waves in two groups (G0 = waves 0-3 own
@@ -470,6 +472,242 @@ __global__ __launch_bounds__(512, 1) void filter_qs_kernel(FilterArgs a) {
     }
 }
 
+// ------------------------------------------------ int8 filter (optional) --
+// With the index's int8 filter copy (rc_index_set_filter(RC_FILTER_I8)) the filter GEMM
+// runs on v_mfma_i32_16x16x64_i8 — twice the f16/bf16 MFMA rate, half the row bytes —
+// and the candidates are still rescored exactly on the stored rows (rescore_kernel).
+// A stored row x̂ is kept as x̃ = sx·x8 (x8 = rne(x̂/sx) in [-127, 127], sx = max|x̂|/127)
+// with ex >= ||x̂ - x̃||₂; a normalised query qn as q̃ = sq·q8 with eq >= ||qn - q̃||₂.
+// The integer dot D = q8·x8 is exact (|D| <= ld·127² < 2^24: exact in f32 too), and
+//   |sq·sx·D - qn·x̂| <= ||qn||·ex + eq·||x̃|| <= ex·(1.0001 + eq) + 1.01·eq
+// (||qn|| <= 1.0001, ||x̃|| <= ||x̂|| + ex, ||x̂|| <= 1.01).  A row is kept iff
+//   sq·(sx·D) + ex·aq >= thr[q],   aq = 1.0001 + eq,   thr = kth - eps,
+//   eps = 1.01·eq + 6.5e-5 (the f32 bound of the exact scores, as above) + 1e-6 (the
+// f32 rounding of the left side), so the filter never drops a row of the final top-k.
+// For unit rows in 512-d, ex and eq are ≈ 0.004-0.008: the candidate lists are a few
+// times longer than with the f16 filter, so the stages grow more slowly
+// (batch_stage_ratio's inflation).
+//
+// Queries: as prepare_queries_kernel (same qn arithmetic), plus q8 / sq / aq.
+__global__ __launch_bounds__(64) void prepare_queries_i8_kernel(const float *__restrict__ q, int nq, int dim, int64_t ld,
+                                                               float *__restrict__ qn, int8_t *__restrict__ q8,
+                                                               float *__restrict__ sq, float *__restrict__ aq,
+                                                               float *__restrict__ eps, float *__restrict__ thr) {
+    const int lane = threadIdx.x;
+    const int qi = blockIdx.x;
+    const bool valid = qi < nq;
+    const float *src = q + (int64_t)(valid ? qi : 0) * dim;
+    float ss = 0.f;
+    for (int c = lane; c < dim; c += 64) ss = valid ? fmaf(src[c], src[c], ss) : 0.f;
+    ss = wave_sum(ss);
+    const float inv = ss > 0.f ? 1.0f / sqrtf(ss) : 0.f;
+    float mx = 0.f;
+    for (int c = lane; c < ld; c += 64) {
+        const float v = (valid && c < dim) ? src[c] * inv : 0.f;
+        mx = fmaxf(mx, fabsf(v));
+        if (valid) qn[(int64_t)qi * ld + c] = v;
+    }
+    mx = wave_max(mx);
+    const float s = mx * (1.0f / 127.0f), is = mx > 0.f ? 127.0f / mx : 0.f;
+    float err = 0.f;
+    for (int c = lane; c < ld; c += 64) {
+        const float v = (valid && c < dim) ? src[c] * inv : 0.f;  // the value stored in qn above
+        const float r = fminf(127.f, fmaxf(-127.f, rintf(v * is)));
+        q8[(int64_t)qi * ld + c] = (int8_t)r;
+        const float d = v - s * r;
+        err = fmaf(d, d, err);
+    }
+    err = wave_sum(err);
+    if (lane == 0) {
+        const float eq = sqrtf(err) * 1.001f + 1e-7f;
+        sq[qi] = s;
+        aq[qi] = 1.0001f + eq;
+        eps[qi] = 1.01f * eq + 6.6e-5f;
+        thr[qi] = valid ? -INFINITY : INFINITY;
+    }
+}
+
+// Query-stationary like filter_qs_kernel (same LDS ring, buffer-descriptor DMA, 128-row
+// tiles, 8 waves x 32 queries), with the MFMA roles swapped: A = queries (registers),
+// B = index rows (LDS), so lane (li, g) of acc[rf][qt] holds queries 16·qt + 4g + j of
+// row 16·rf + li — one row per (lane, rf): its sx / ex are 8 values per lane per tile
+// (i8_slot layout), loaded with the previous tile's epilogue.  A K-step is 128 bytes
+// = 128 int8 elements, NKT = row bytes / 128 steps per tile.  Every ring step is
+// issued (a step past the block's range reads nothing: zero-size buffer descriptor), so
+// each wait counts a fixed number of younger loads: the DMA of the younger steps, plus
+// this tile's 4 scale loads while they are younger than the awaited step.
+template <int NKT>
+__global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    constexpr int QT = QS_QT, WAVES = 16 / QS_QT, RF = QS_RT / 16;
+    constexpr int STEP_BYTES = QS_RT * 128;
+    constexpr int SPS = 2, SXL = 4;
+    constexpr int PPW = 2 * RF / WAVES;
+    static_assert(RF == 8 && NKT % SPS == 0 && (QS_NS - 2 * SPS) * PPW + SXL < 64, "layout");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+
+    const int b = blockIdx.x, xcd = b & 7, jx = b >> 3;
+    const int qb = jx % a.nqb;
+    const int64_t chunk = (int64_t)(jx / a.nqb) * 8 + xcd;
+    const int64_t rt_total = (a.r_end - a.r_begin + QS_RT - 1) / QS_RT;
+    const int64_t rt0 = chunk * a.tiles_per_chunk;
+    const int64_t rt1 = min(rt_total, rt0 + a.tiles_per_chunk);
+    if (rt0 >= rt1) return;  // block-uniform
+    const int64_t ldb = a.ld;  // bytes per row
+    const int ntiles = (int)(rt1 - rt0);
+    const int nsteps = ntiles * NKT;
+    const int64_t row0 = a.r_begin + rt0 * QS_RT;  // a multiple of 128 (host check)
+    const uint8_t *Rg = (const uint8_t *)a.rows + row0 * ldb;
+
+    i32x4_t qf[QT][2 * NKT];  // bytes [64 kk + 16 g, +16) of query q0 + 16 qt + li
+    const int q0 = qb * SB_TILE + wave * 16 * QT;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int kk = 0; kk < 2 * NKT; ++kk)
+            qf[qt][kk] = *reinterpret_cast<const i32x4_t *>((const uint8_t *)a.qh + (int64_t)(q0 + qt * 16 + li) * ldb +
+                                                            kk * 64 + g * 16);
+    float thr[QT][4], sq[QT][4], aq[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = q0 + qt * 16 + 4 * g + j;
+            thr[qt][j] = a.thr[q];
+            sq[qt][j] = a.sq[q];
+            aq[qt][j] = a.aq[q];
+        }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(thr[qt][j]), "v"(sq[qt][j]), "v"(aq[qt][j]));
+#pragma unroll
+        for (int kk = 0; kk < 2 * NKT; ++kk) asm volatile("" ::"v"(qf[qt][kk]));
+    }
+
+    uint32_t loff[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int r = (wave + WAVES * i) * 8 + (lane >> 3);
+        loff[i] = (uint32_t)(r * (int)ldb + (((lane & 7) ^ ((r >> 1) & 7)) << 4));
+    }
+    auto issue = [&](int t) {
+        const bool ok = t < nsteps;
+        const int tile = t / NKT;
+        const int ks = t - tile * NKT;
+        uint8_t *base = smem + (t % QS_NS) * STEP_BYTES;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(ok ? Rg + (int64_t)tile * QS_RT * ldb + ks * 128 : Rg), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            lds_void *dst = (lds_void *)(base + (wave + WAVES * i) * 1024);
+            const uint32_t off = loff[i];
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, 0);
+        }
+    };
+    f32x4_t sxv[2], exv[2];  // rows 16 rf + li of the tile, rf = 4 h + e → sxv[h][e]
+    auto load_scales = [&](int tile) {
+        const int64_t p = row0 + (int64_t)tile * QS_RT + li * 8;
+        asm volatile("" ::: "memory");
+        sxv[0] = *reinterpret_cast<const f32x4_t *>(a.rsx + p);
+        sxv[1] = *reinterpret_cast<const f32x4_t *>(a.rsx + p + 4);
+        exv[0] = *reinterpret_cast<const f32x4_t *>(a.rex + p);
+        exv[1] = *reinterpret_cast<const f32x4_t *>(a.rex + p + 4);
+        asm volatile("" ::: "memory");
+    };
+    for (int t = 0; t < QS_NS - SPS; ++t) issue(t);
+    load_scales(0);
+
+    i32x4_t acc[RF][QT];
+    for (int tile = 0; tile < ntiles; ++tile) {
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) acc[rf][qt] = i32x4_t{0, 0, 0, 0};
+#pragma unroll
+        for (int kp = 0; kp < NKT / SPS; ++kp) {
+            const int t = tile * NKT + SPS * kp;
+            // steps t..t+SPS-1 must have landed; younger: NS - 2·SPS steps, and this tile's
+            // scale loads while they were issued after step t + SPS - 1
+            if (t + QS_NS - SPS - 1 < nsteps) {
+                if (SPS * (kp + 2) <= QS_NS)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((QS_NS - 2 * SPS) * PPW + SXL) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((QS_NS - 2 * SPS) * PPW) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int j = QS_NS - SPS; j < QS_NS; ++j) issue(t + j);
+            constexpr int RH = RF / 4, NG = SPS * 2 * RH;
+#pragma unroll
+            for (int gi = 0; gi < NG; ++gi) {
+                const int kl = gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
+                const int ks = SPS * kp + kl;
+                const uint8_t *Sr = smem + ((t + kl) % QS_NS) * STEP_BYTES + li * 128 +
+                                    (((sh * 4 + g) ^ ((li >> 1) & 7)) << 4) + rh * 4 * 2048;
+                i32x4_t cur[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cur[i] = *reinterpret_cast<const i32x4_t *>(Sr + i * 2048);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+                        acc[rh * 4 + i][qt] =
+                            __builtin_amdgcn_mfma_i32_16x16x64_i8(qf[qt][ks * 2 + sh], cur[i], acc[rh * 4 + i][qt], 0, 0, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            }
+        }
+        // ---- epilogue: keep (q, row) iff sq·(sx·D) + ex·aq >= thr[q]
+        float sx[RF], ex[RF];
+#pragma unroll
+        for (int rf = 0; rf < RF; ++rf) {
+            sx[rf] = sxv[rf >> 2][rf & 3];
+            ex[rf] = exv[rf >> 2][rf & 3];
+        }
+        float exm = ex[0];
+#pragma unroll
+        for (int rf = 1; rf < RF; ++rf) exm = fmaxf(exm, ex[rf]);
+        bool hit = false;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float m = -INFINITY;
+#pragma unroll
+                for (int rf = 0; rf < RF; ++rf) m = fmaxf(m, sx[rf] * (float)acc[rf][qt][j]);
+                hit |= fmaf(exm, aq[qt][j], sq[qt][j] * m) >= thr[qt][j];
+            }
+        if (__ballot(hit) != 0 && hit) {
+            const int64_t rbase = row0 + (int64_t)tile * QS_RT + li;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = q0 + qt * 16 + 4 * g + j;
+#pragma unroll
+                    for (int rf = 0; rf < RF; ++rf) {
+                        const int64_t row = rbase + rf * 16;
+                        const float v = fmaf(ex[rf], aq[qt][j], sq[qt][j] * (sx[rf] * (float)acc[rf][qt][j]));
+                        if (v >= thr[qt][j] && row < a.r_end) {
+                            const uint32_t pos = atomicAdd(&a.cnt[q], 1u);
+                            if ((int)pos < a.cap) a.cand[(int64_t)q * a.cap + pos] = (uint32_t)row;
+                        }
+                    }
+                }
+        }
+        load_scales(min(tile + 1, ntiles - 1));  // unconditional: the same wait counts on every path
+    }
+}
+
 // ------------------------------------------------------- exact rescoring --
 // One block per query.  Candidates are scored exactly as scan_topk_kernel
 // scores a row (16 lanes per row, 16-B chunks, f32 FMA in chunk order, DPP
@@ -604,38 +842,56 @@ void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipSt
 static const int filter_abl = std::getenv("RC_FILTER_ABL") ? std::atoi(std::getenv("RC_FILTER_ABL")) : 0;
 #endif
 
-int batch_stage_ratio(int k, int cap) {
-    const int g = cap / (5 * k / 2 + 1);
+int batch_stage_ratio(int k, int cap, int inflation) {
+    const int g = cap / (5 * k / 2 * inflation + 1);
     return std::max(2, std::min(64, g));
 }
 
-template <typename T>
-void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
+// The stages: stage 1 takes the first cap rows as candidates (thr = -inf), each later
+// stage filters the next g-times-larger row range against the running thresholds, then
+// rescore_kernel merges its candidates.  filter(c0, c1, nchunk) enqueues one filter
+// dispatch over rows [c0, c1) split into nchunk row chunks.
+template <typename T, typename F>
+void run_stages(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer, int g, int64_t row_bytes, F &&filter) {
     const int nqb = (p.nq + SB_TILE - 1) / SB_TILE;
     const int nq_pad = nqb * SB_TILE;
-    hipLaunchKernelGGL(prepare_queries_kernel<T>, dim3(nq_pad), dim3(64), 0, s, p.queries, p.nq, p.dim, p.ld, ws.qn,
-                       (T *)ws.qh, ws.eps, ws.thr);
-    RC_LAUNCH_CHECK();
     RC_HIP(hipMemsetAsync(ws.keys, 0xFF, (size_t)p.nq * p.k * sizeof(uint64_t), s));
     RC_HIP(hipMemsetAsync(ws.cnt, 0, (size_t)nq_pad * sizeof(uint32_t), s));
     RC_HIP(hipMemsetAsync(ws.flags, 0, (size_t)p.nq * sizeof(int), s));
-
-    const int g = batch_stage_ratio(p.k, ws.cap);
-    int64_t b0 = 0, b1 = std::min<int64_t>(p.n_rows, ws.cap);  // stage 1: every row is a candidate
+    int64_t b0 = 0, b1 = std::min<int64_t>(p.n_rows, ws.cap);
     // With nq > 256 the nqb query blocks that read one row chunk run side by side on one
     // XCD so that its L2 serves the second to last reader; over a long chunk their
     // progress drifts apart by more than the L2 holds (memory-side reads 2.8x the rows
     // at 125M rows).  Sub-launches of <= 2 GB of rows realign them: reads fall to 1.05x
     // and the filter runs 3-5 % faster (profiles/r02/r02_ab_results.txt).
-    const int64_t split = nqb > 1 ? std::max<int64_t>(SB_TILE, ((int64_t)1 << 31) / (p.ld * (int64_t)sizeof(T)) / SB_TILE * SB_TILE)
+    const int64_t split = nqb > 1 ? std::max<int64_t>(SB_TILE, ((int64_t)1 << 31) / row_bytes / SB_TILE * SB_TILE)
                                   : (int64_t)0;
     while (b0 < p.n_rows) {
-      for (int64_t c0 = b0; c0 < b1;) {
-        const int64_t c1 = split > 0 ? std::min(b1, c0 + split) : b1;
-        const int slot = timer ? timer->begin(s) : -1;  // per dispatch, as rocprofv3 counts them
+        for (int64_t c0 = b0; c0 < b1;) {
+            const int64_t c1 = split > 0 ? std::min(b1, c0 + split) : b1;
+            const int slot = timer ? timer->begin(s) : -1;  // per dispatch, as rocprofv3 counts them
+            const int64_t rt_total = (c1 - c0 + SB_TILE - 1) / SB_TILE;
+            int64_t nchunk = std::min<int64_t>(rt_total, std::max<int64_t>(1, (256 + nqb - 1) / nqb));
+            nchunk = (nchunk + 7) / 8 * 8;
+            filter(c0, c1, nchunk, nqb);
+            RC_LAUNCH_CHECK();
+            if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(c1 - c0) * (double)p.ld);
+            c0 = c1;
+        }
+        launch_rescore<T>(p, ws, b1 == p.n_rows ? 1 : 0, s);
+        b0 = b1;
+        b1 = std::min<int64_t>(p.n_rows, b1 * g);
+    }
+}
+
+template <typename T>
+void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
+    const int nq_pad = (p.nq + SB_TILE - 1) / SB_TILE * SB_TILE;
+    hipLaunchKernelGGL(prepare_queries_kernel<T>, dim3(nq_pad), dim3(64), 0, s, p.queries, p.nq, p.dim, p.ld, ws.qn,
+                       (T *)ws.qh, ws.eps, ws.thr);
+    RC_LAUNCH_CHECK();
+    auto filter = [&](int64_t c0, int64_t c1, int64_t nchunk, int nqb) {
         const int64_t rt_total = (c1 - c0 + SB_TILE - 1) / SB_TILE;
-        int64_t nchunk = std::min<int64_t>(rt_total, std::max<int64_t>(1, (256 + nqb - 1) / nqb));
-        nchunk = (nchunk + 7) / 8 * 8;
         const int64_t tpc = (rt_total + nchunk - 1) / nchunk;
         FilterArgs fa{p.rows, ws.qh, p.ld, (int)(p.ld / 64), c0, c1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
         const int nkt = (int)(p.ld / 64);
@@ -656,22 +912,51 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
         } else {
             hipLaunchKernelGGL(filter_gemm_kernel<T>, dim3((unsigned)(nchunk * nqb)), dim3(512), 0, s, fa);
         }
-        RC_LAUNCH_CHECK();
-        if (timer) timer->end(slot, s, 2.0 * (double)nq_pad * (double)(c1 - c0) * (double)p.ld);
-        c0 = c1;
-      }
-        launch_rescore<T>(p, ws, b1 == p.n_rows ? 1 : 0, s);
-        b0 = b1;
-        b1 = std::min<int64_t>(p.n_rows, b1 * g);
-    }
+    };
+    run_stages<T>(p, ws, s, timer, batch_stage_ratio(p.k, ws.cap), p.ld * (int64_t)sizeof(T), filter);
 }
+
+// Candidates per stage grow by exp(z·eps/σ) over the f16 filter's (≈ 3x for random unit
+// rows in 512-d at top-100 of 125M); the stage ratio assumes 3x.
+constexpr int I8_STAGE_INFLATION = 3;
+
+template <typename T>
+void run_batched_i8(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
+    const int nq_pad = (p.nq + SB_TILE - 1) / SB_TILE * SB_TILE;
+    hipLaunchKernelGGL(prepare_queries_i8_kernel, dim3(nq_pad), dim3(64), 0, s, p.queries, p.nq, p.dim, p.ld, ws.qn,
+                       (int8_t *)ws.qh, ws.sq, ws.aq, ws.eps, ws.thr);
+    RC_LAUNCH_CHECK();
+    const int nkt = (int)(p.ld / 128);
+    auto filter = [&](int64_t c0, int64_t c1, int64_t nchunk, int nqb) {
+        RC_REQUIRE(c0 % QS_RT == 0, RC_ERR_INVALID, "internal: int8 filter range not tile-aligned");
+        const int64_t tpc = ((c1 - c0 + QS_RT - 1) / QS_RT + nchunk - 1) / nchunk;
+        FilterArgs fa{p.rows8, ws.qh, p.ld, nkt, c0, c1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
+        fa.rsx = p.rsx;
+        fa.rex = p.rex;
+        fa.sq = ws.sq;
+        fa.aq = ws.aq;
+        const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * 16 / QS_QT);
+        if (nkt == 4) hipLaunchKernelGGL(filter_i8_kernel<4>, gr, bl, 0, s, fa);
+        else hipLaunchKernelGGL(filter_i8_kernel<2>, gr, bl, 0, s, fa);
+    };
+    run_stages<T>(p, ws, s, timer, batch_stage_ratio(p.k, ws.cap, I8_STAGE_INFLATION), p.ld, filter);
+}
+
+// ld 768 would hold 96 query-fragment registers per lane and spill at 2 waves per SIMD
+bool i8_filter_supported(int64_t ld) { return ld == 256 || ld == 512; }
 
 void batched_search(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
     RC_REQUIRE(p.ld % 64 == 0, RC_ERR_UNSUPPORTED, "batched search needs ld % 64 == 0");
     RC_REQUIRE(p.n_rows > 0, RC_ERR_INVALID, "batched search over an empty range");
+    if (p.rows8 != nullptr) {
+        RC_REQUIRE(i8_filter_supported(p.ld), RC_ERR_UNSUPPORTED, "int8 filter needs ld 256 or 512");
+        if (p.dtype == RC_F16) return run_batched_i8<f16_t>(p, ws, s, timer);
+        if (p.dtype == RC_BF16) return run_batched_i8<bf16_t>(p, ws, s, timer);
+        if (p.dtype == RC_F32) return run_batched_i8<float>(p, ws, s, timer);
+    }
     if (p.dtype == RC_F16) return run_batched<f16_t>(p, ws, s, timer);
     if (p.dtype == RC_BF16) return run_batched<bf16_t>(p, ws, s, timer);
-    throw Error(RC_ERR_UNSUPPORTED, "batched MFMA search needs an f16 or bf16 index");
+    throw Error(RC_ERR_UNSUPPORTED, "batched MFMA search needs an f16 or bf16 index (or the int8 filter copy)");
 }
 
 void BatchWs::ensure(int nq, int k, int64_t ld, int dtype_bytes) {
@@ -689,6 +974,8 @@ void BatchWs::ensure(int nq, int k, int64_t ld, int dtype_bytes) {
     cand = (uint32_t *)dmalloc((size_t)nq_cap * cap * sizeof(uint32_t));
     keys = (uint64_t *)dmalloc((size_t)nq_cap * k_cap * sizeof(uint64_t));
     flags = (int *)dmalloc((size_t)nq_cap * sizeof(int));
+    sq = (float *)dmalloc((size_t)nq_cap * sizeof(float));
+    aq = (float *)dmalloc((size_t)nq_cap * sizeof(float));
     ovf = (int *)dmalloc(sizeof(int));
     RC_HIP(hipMemset(ovf, 0, sizeof(int)));
     // the fallback scan's partial lists are sized by a memory budget, not by the row count:
@@ -707,6 +994,8 @@ void BatchWs::release() {
     dfree(cand);
     dfree(keys);
     dfree(flags);
+    dfree(sq);
+    dfree(aq);
     dfree(ovf);
     dfree(fb_partial);
     qn = nullptr;
@@ -715,6 +1004,7 @@ void BatchWs::release() {
     cnt = cand = nullptr;
     keys = nullptr;
     flags = ovf = nullptr;
+    sq = aq = nullptr;
     fb_partial = nullptr;
     fb_blocks = 0;
     nq_cap = k_cap = 0;

@@ -269,6 +269,14 @@ int rc_sharded_grow(rc_sharded *h, int64_t new_capacity_per_shard) {
     });
 }
 
+int rc_sharded_set_filter(rc_sharded *h, int kind) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        std::lock_guard<std::mutex> lk(h->mu);
+        for (int s = 0; s < h->n; ++s) check_status(rc_index_set_filter(h->shard[s], kind, h->st[s]));
+    });
+}
+
 int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t *rows, void *stream) {
     return guard([&] {
         RC_REQUIRE(h, RC_ERR_INVALID, "null index");

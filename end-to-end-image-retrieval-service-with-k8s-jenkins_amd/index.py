@@ -104,6 +104,20 @@ class DeviceIndex:
     def reserve(self, max_nq: int, max_k: int) -> None:
         check(self.lib.rc_index_reserve(self.handle, int(max_nq), int(max_k)))
 
+    def set_filter(self, kind: str, stream=None) -> None:
+        """Filter copy of the batched search (rc_index_set_filter): "native" (the filter GEMM
+        reads the stored rows) or "i8" (an int8 copy of every row, int8 MFMA at twice the f16
+        rate; results unchanged — candidates are rescored exactly on the stored rows)."""
+        if kind not in _lib.FILTERS:
+            raise ValueError(f"unknown filter {kind!r} (expected one of {sorted(_lib.FILTERS)})")
+        check(self.lib.rc_index_set_filter(self.handle, _lib.FILTERS[kind], stream_ptr(stream)))
+
+    @property
+    def filter(self) -> str:
+        k = _lib.C.c_int()
+        check(self.lib.rc_index_get_filter(self.handle, _lib.C.byref(k)))
+        return {v: n for n, v in _lib.FILTERS.items()}[k.value]
+
     def _vecs(self, vecs: torch.Tensor) -> torch.Tensor:
         if vecs.dim() == 1:
             vecs = vecs[None]
@@ -293,6 +307,16 @@ class ShardSet:
     def grow(self, new_capacity_per_shard: int) -> None:
         check(self.lib.rc_sharded_grow(self.handle, int(new_capacity_per_shard)))
 
+    def set_filter(self, kind: str) -> None:
+        """``DeviceIndex.set_filter`` on every shard."""
+        if kind not in _lib.FILTERS:
+            raise ValueError(f"unknown filter {kind!r} (expected one of {sorted(_lib.FILTERS)})")
+        check(self.lib.rc_sharded_set_filter(self.handle, _lib.FILTERS[kind]))
+
+    @property
+    def filter(self) -> str:
+        return self._shards[0].filter
+
     def upsert_rows(self, vecs: torch.Tensor, rows) -> None:
         """vecs f32 [n, dim] (any device; moved to the leader), rows: global rows (host)."""
         if vecs.dim() == 1:
@@ -401,9 +425,12 @@ class Index:
     """
 
     def __init__(self, name: str, dimension: int = 768, metric: str = "cosine", dtype: str = "float32",
-                 capacity: int = 1 << 20, device=None, shards: int | None = None, devices=None):
+                 capacity: int = 1 << 20, device=None, shards: int | None = None, devices=None,
+                 filter: str = "native"):
         if metric != "cosine":
             raise ValueError("only metric='cosine' is supported")
+        if filter not in _lib.FILTERS:
+            raise ValueError(f"unknown filter {filter!r} (expected one of {sorted(_lib.FILTERS)})")
         if devices is None:
             devices = [device] * int(shards or 1)
         self.name = name
@@ -412,6 +439,8 @@ class Index:
         n = len(devices)
         self._set = ShardSet(self.dimension, dtype=dtype, capacity_per_shard=max(1, -(-int(capacity) // n)),
                              devices=devices)
+        if filter != "native":
+            self._set.set_filter(filter)
         self._rows: dict[str, int] = {}
         self._ids: list[str] = []
         self._meta: dict[str, dict] = {}
@@ -675,7 +704,7 @@ class Index:
             np.save(os.path.join(path, "norms.npy"), norms)
             manifest = {"format": self.SNAPSHOT_FORMAT, "name": self.name, "dimension": self.dimension,
                         "metric": self.metric, "dtype": self._set.dtype, "ld": self._set.ld, "count": n,
-                        "capacity": self._set.capacity,
+                        "capacity": self._set.capacity, "filter": self._set.filter,
                         "ids": list(self._ids), "metadata": {i: self._meta.get(i, {}) for i in self._ids}}
             tmp = os.path.join(path, "manifest.json.tmp")
             with open(tmp, "w") as f:
@@ -684,7 +713,7 @@ class Index:
 
     @classmethod
     def load(cls, path: str, capacity: int | None = None, device=None, shards: int | None = None,
-             devices=None) -> "Index":
+             devices=None, filter: str | None = None) -> "Index":
         import numpy as np
 
         with open(os.path.join(path, "manifest.json")) as f:
@@ -694,7 +723,7 @@ class Index:
         n = int(man["count"])
         idx = cls(man["name"], dimension=man["dimension"], metric=man["metric"], dtype=man["dtype"],
                   capacity=max(int(capacity or man.get("capacity", 0)), n, 1), device=device, shards=shards,
-                  devices=devices)
+                  devices=devices, filter=filter or man.get("filter", "native"))
         if idx._set.ld != man["ld"]:
             raise ValueError("snapshot row layout does not match this build")
         rows = np.load(os.path.join(path, "rows.npy"), allow_pickle=False)

@@ -52,7 +52,7 @@ def get_index(index_name: str, dimension: int | None = None, dtype: str | None =
         if idx is None:
             idx = Index(index_name, dimension=dimension or Config.INPUT_RESOLUTION, metric="cosine",
                         dtype=dtype or Config.INDEX_DTYPE, capacity=capacity or Config.INDEX_CAPACITY,
-                        devices=devices if devices is not None else index_devices())
+                        devices=devices if devices is not None else index_devices(), filter=Config.INDEX_FILTER)
             _indexes[index_name] = idx
             logger.info("Created in-HBM index: %s", index_name)
         return idx

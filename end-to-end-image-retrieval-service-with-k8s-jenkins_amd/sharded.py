@@ -29,7 +29,8 @@ import torch.distributed as dist
 
 class ShardedIndex:
     def __init__(self, dim: int, dtype: str = "float16", capacity_per_rank: int = 1 << 20, group=None,
-                 device=None, backend_factory: Callable | None = None, merge_fn: Callable | None = None):
+                 device=None, backend_factory: Callable | None = None, merge_fn: Callable | None = None,
+                 filter: str = "native"):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -48,6 +49,8 @@ class ShardedIndex:
                                                   row_base=self.rank, row_stride=self.world)
             merge_fn = merge_fn or topk_merge
         self.local = backend_factory()
+        if filter != "native":  # the batched search's int8 filter copy (DeviceIndex.set_filter)
+            self.local.set_filter(filter)
         self.merge = merge_fn
         self.n_rows = 0  # global rows [0, n_rows) hold data (the same value on every rank)
         self.written = 0  # local rows [0, written) of this rank's shard hold data (high-water mark)

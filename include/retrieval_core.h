@@ -144,6 +144,22 @@ int rc_index_search(rc_index *h, const float *queries, int nq, int64_t n_rows, i
 int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows, int k,
                        float *scores, int64_t *out_rows, int mode, void *stream);
 
+/* Filter copy for the batched search (no reference counterpart: Pinecone's query
+ * internals; results are unchanged, only the speed of RC_SEARCH_MFMA):
+ *   RC_FILTER_NATIVE — the filter GEMM reads the stored rows (f16/bf16 MFMA);
+ *   RC_FILTER_I8     — the index also keeps an int8 copy of every row (per-row
+ *                      scale and residual norm, ld + 8 bytes per row, maintained
+ *                      by upsert / fill / import / grow); the filter GEMM runs on
+ *                      int8 MFMA at twice the f16 rate with a per-(query, row) error
+ *                      bound, and candidates are rescored exactly on the stored rows.
+ *                      Row widths (dim rounded up to 128) 256 or 512; makes
+ *                      RC_SEARCH_MFMA available on f32 indexes too.
+ * Enabling quantises every row (synchronous on `stream`). */
+#define RC_FILTER_NATIVE 0
+#define RC_FILTER_I8 1
+int rc_index_set_filter(rc_index *h, int kind, void *stream);
+int rc_index_get_filter(const rc_index *h, int *kind);
+
 /* Synthetic rows for benchmarks (no reference counterpart): rows
  * [row0, row0+n) get uniform[-1,1) values from a counter-based hash of
  * (seed, row, col), normalised and cast like an upsert. */
@@ -188,6 +204,8 @@ int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, 
  * leader-device [nq, k], identical to one rc_index holding the same rows. */
 int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
                       int64_t *out_rows, int mode, void *stream);
+/* rc_index_set_filter on every shard. */
+int rc_sharded_set_filter(rc_sharded *h, int kind);
 
 /* ------------------------------------------------------------------------
  * ViT-MSN image embedding.  Replaces the /embed compute path —
