@@ -25,7 +25,7 @@ class Config:
     # build-side knobs
     INDEX_DTYPE = os.getenv("RC_INDEX_DTYPE", "float32")
     INDEX_CAPACITY = int(os.getenv("RC_INDEX_CAPACITY", str(1 << 20)))  # initial rows; grows on demand
-    # batched-search filter copy: "native" or "i8" (int8 copy of the rows; dims up to 512)
+    # batched-search filter copy: "native" or "i8" (int8 copy of the rows; dims up to 768)
     INDEX_FILTER = os.getenv("RC_INDEX_FILTER", "native")
     # index shards: RC_INDEX_DEVICES = "all" (one shard per visible GPU) or a comma list
     # of device ordinals ("0,1,2,3"); otherwise RC_INDEX_SHARDS shards on the current GPU

@@ -651,7 +651,7 @@ int rc_index_set_filter(rc_index *h, int kind, void *stream) {
             return;
         }
         RC_REQUIRE(i8_filter_supported(h->ld), RC_ERR_UNSUPPORTED,
-                   "the int8 filter needs a row width (dim rounded up to 128) of 256 or 512");
+                   "the int8 filter needs a row width (dim rounded up to 128) of 256, 512 or 768");
         const int64_t pad = cap_pad(h->capacity);
         try {
             h->rows8 = (int8_t *)dmalloc((size_t)pad * h->ld);

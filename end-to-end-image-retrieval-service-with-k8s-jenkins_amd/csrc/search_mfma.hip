@@ -536,14 +536,16 @@ __global__ __launch_bounds__(64) void prepare_queries_i8_kernel(const float *__r
 // issued (a step past the block's range reads nothing: zero-size buffer descriptor), so
 // each wait counts a fixed number of younger loads: the DMA of the younger steps, plus
 // this tile's 4 scale loads while they are younger than the awaited step.
-template <int NKT>
+// RT = rows per tile: 128, or 64 at ld 768 (NKT 6), where the 96 query-fragment registers
+// leave room for only half the accumulators.
+template <int NKT, int RT>
 __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     typedef int i32x4_t __attribute__((ext_vector_type(4)));
-    constexpr int QT = QS_QT, WAVES = 16 / QS_QT, RF = QS_RT / 16;
-    constexpr int STEP_BYTES = QS_RT * 128;
-    constexpr int SPS = 2, SXL = 4;
+    constexpr int QT = QS_QT, WAVES = 16 / QS_QT, RF = RT / 16, RH = RF / 4;
+    constexpr int STEP_BYTES = RT * 128;
+    constexpr int SPS = 2, SXL = 2 * RH;
     constexpr int PPW = 2 * RF / WAVES;
-    static_assert(RF == 8 && NKT % SPS == 0 && (QS_NS - 2 * SPS) * PPW + SXL < 64, "layout");
+    static_assert((RT == 128 || RT == 64) && NKT % SPS == 0 && (QS_NS - 2 * SPS) * PPW + SXL < 64, "layout");
     __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -553,14 +555,14 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     const int b = blockIdx.x, xcd = b & 7, jx = b >> 3;
     const int qb = jx % a.nqb;
     const int64_t chunk = (int64_t)(jx / a.nqb) * 8 + xcd;
-    const int64_t rt_total = (a.r_end - a.r_begin + QS_RT - 1) / QS_RT;
+    const int64_t rt_total = (a.r_end - a.r_begin + RT - 1) / RT;
     const int64_t rt0 = chunk * a.tiles_per_chunk;
     const int64_t rt1 = min(rt_total, rt0 + a.tiles_per_chunk);
     if (rt0 >= rt1) return;  // block-uniform
     const int64_t ldb = a.ld;  // bytes per row
     const int ntiles = (int)(rt1 - rt0);
     const int nsteps = ntiles * NKT;
-    const int64_t row0 = a.r_begin + rt0 * QS_RT;  // a multiple of 128 (host check)
+    const int64_t row0 = a.r_begin + rt0 * RT;  // a multiple of RT (host check)
     const uint8_t *Rg = (const uint8_t *)a.rows + row0 * ldb;
 
     i32x4_t qf[QT][2 * NKT];  // bytes [64 kk + 16 g, +16) of query q0 + 16 qt + li
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
         const int ks = t - tile * NKT;
         uint8_t *base = smem + (t % QS_NS) * STEP_BYTES;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(ok ? Rg + (int64_t)tile * QS_RT * ldb + ks * 128 : Rg), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
+            (void *)(ok ? Rg + (int64_t)tile * RT * ldb + ks * 128 : Rg), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
             lds_void *dst = (lds_void *)(base + (wave + WAVES * i) * 1024);
@@ -609,14 +611,15 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, 0);
         }
     };
-    f32x4_t sxv[2], exv[2];  // rows 16 rf + li of the tile, rf = 4 h + e → sxv[h][e]
+    f32x4_t sxv[RH], exv[RH];  // rows 16 rf + li of the tile, rf = 4 h + e → sxv[h][e]
     auto load_scales = [&](int tile) {
-        const int64_t p = row0 + (int64_t)tile * QS_RT + li * 8;
+        const int64_t tb = row0 + (int64_t)tile * RT;  // i8_slot(tb + 16 rf + li) = p + rf
+        const int64_t p = (tb & ~int64_t(127)) + li * 8 + ((tb & 127) >> 4);
         asm volatile("" ::: "memory");
-        sxv[0] = *reinterpret_cast<const f32x4_t *>(a.rsx + p);
-        sxv[1] = *reinterpret_cast<const f32x4_t *>(a.rsx + p + 4);
-        exv[0] = *reinterpret_cast<const f32x4_t *>(a.rex + p);
-        exv[1] = *reinterpret_cast<const f32x4_t *>(a.rex + p + 4);
+#pragma unroll
+        for (int h = 0; h < RH; ++h) sxv[h] = *reinterpret_cast<const f32x4_t *>(a.rsx + p + 4 * h);
+#pragma unroll
+        for (int h = 0; h < RH; ++h) exv[h] = *reinterpret_cast<const f32x4_t *>(a.rex + p + 4 * h);
         asm volatile("" ::: "memory");
     };
     for (int t = 0; t < QS_NS - SPS; ++t) issue(t);
@@ -646,7 +649,7 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int j = QS_NS - SPS; j < QS_NS; ++j) issue(t + j);
-            constexpr int RH = RF / 4, NG = SPS * 2 * RH;
+            constexpr int NG = SPS * 2 * RH;
 #pragma unroll
             for (int gi = 0; gi < NG; ++gi) {
                 const int kl = gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
@@ -687,7 +690,7 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
                 hit |= fmaf(exm, aq[qt][j], sq[qt][j] * m) >= thr[qt][j];
             }
         if (__ballot(hit) != 0 && hit) {
-            const int64_t rbase = row0 + (int64_t)tile * QS_RT + li;
+            const int64_t rbase = row0 + (int64_t)tile * RT + li;
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
@@ -928,28 +931,29 @@ void run_batched_i8(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer 
     RC_LAUNCH_CHECK();
     const int nkt = (int)(p.ld / 128);
     auto filter = [&](int64_t c0, int64_t c1, int64_t nchunk, int nqb) {
-        RC_REQUIRE(c0 % QS_RT == 0, RC_ERR_INVALID, "internal: int8 filter range not tile-aligned");
-        const int64_t tpc = ((c1 - c0 + QS_RT - 1) / QS_RT + nchunk - 1) / nchunk;
+        const int rt = nkt == 6 ? 64 : 128;
+        RC_REQUIRE(c0 % rt == 0, RC_ERR_INVALID, "internal: int8 filter range not tile-aligned");
+        const int64_t tpc = ((c1 - c0 + rt - 1) / rt + nchunk - 1) / nchunk;
         FilterArgs fa{p.rows8, ws.qh, p.ld, nkt, c0, c1, tpc, nqb, ws.thr, ws.cnt, ws.cand, ws.cap};
         fa.rsx = p.rsx;
         fa.rex = p.rex;
         fa.sq = ws.sq;
         fa.aq = ws.aq;
         const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * 16 / QS_QT);
-        if (nkt == 4) hipLaunchKernelGGL(filter_i8_kernel<4>, gr, bl, 0, s, fa);
-        else hipLaunchKernelGGL(filter_i8_kernel<2>, gr, bl, 0, s, fa);
+        if (nkt == 4) hipLaunchKernelGGL((filter_i8_kernel<4, 128>), gr, bl, 0, s, fa);
+        else if (nkt == 6) hipLaunchKernelGGL((filter_i8_kernel<6, 64>), gr, bl, 0, s, fa);
+        else hipLaunchKernelGGL((filter_i8_kernel<2, 128>), gr, bl, 0, s, fa);
     };
     run_stages<T>(p, ws, s, timer, batch_stage_ratio(p.k, ws.cap, I8_STAGE_INFLATION), p.ld, filter);
 }
 
-// ld 768 would hold 96 query-fragment registers per lane and spill at 2 waves per SIMD
-bool i8_filter_supported(int64_t ld) { return ld == 256 || ld == 512; }
+bool i8_filter_supported(int64_t ld) { return ld == 256 || ld == 512 || ld == 768; }
 
 void batched_search(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer) {
     RC_REQUIRE(p.ld % 64 == 0, RC_ERR_UNSUPPORTED, "batched search needs ld % 64 == 0");
     RC_REQUIRE(p.n_rows > 0, RC_ERR_INVALID, "batched search over an empty range");
     if (p.rows8 != nullptr) {
-        RC_REQUIRE(i8_filter_supported(p.ld), RC_ERR_UNSUPPORTED, "int8 filter needs ld 256 or 512");
+        RC_REQUIRE(i8_filter_supported(p.ld), RC_ERR_UNSUPPORTED, "int8 filter needs ld 256, 512 or 768");
         if (p.dtype == RC_F16) return run_batched_i8<f16_t>(p, ws, s, timer);
         if (p.dtype == RC_BF16) return run_batched_i8<bf16_t>(p, ws, s, timer);
         if (p.dtype == RC_F32) return run_batched_i8<float>(p, ws, s, timer);

@@ -152,7 +152,7 @@ int rc_index_search_ex(rc_index *h, const float *queries, int nq, int64_t n_rows
  *                      by upsert / fill / import / grow); the filter GEMM runs on
  *                      int8 MFMA at twice the f16 rate with a per-(query, row) error
  *                      bound, and candidates are rescored exactly on the stored rows.
- *                      Row widths (dim rounded up to 128) 256 or 512; makes
+ *                      Row widths (dim rounded up to 128) 256, 512 or 768; makes
  *                      RC_SEARCH_MFMA available on f32 indexes too.
  * Enabling quantises every row (synchronous on `stream`). */
 #define RC_FILTER_NATIVE 0

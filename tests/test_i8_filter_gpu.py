@@ -36,7 +36,7 @@ def _same(dev, Q, k, n):
 
 
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
-@pytest.mark.parametrize("dim", [512, 200])
+@pytest.mark.parametrize("dim", [512, 200, 768])
 @pytest.mark.parametrize("n,k,nq", [(200, 5, 3), (5000, 10, 1), (70_000, 100, 20), (70_000, 256, 9), (300_000, 10, 300)])
 def test_i8_filter_matches_scan(idxmod, cuda, dtype, dim, n, k, nq):
     import torch
@@ -83,7 +83,7 @@ def test_i8_copy_follows_every_write(idxmod, cuda):
     rows, norms = src.export_rows(0, 1000)
     dev.import_rows(0, rows, norms)
     q2 = src.stored_rows(torch.tensor([0, 500, 999]))
-    _, r = _same(dev, torch.cat([q2, Q]), 20, 100_000)
+    _, r = _same(dev, torch.cat([q2.cpu(), Q]), 20, 100_000)
     assert r[:3, 0].cpu().tolist() == [0, 500, 999]
     # off and on again: same results
     dev.set_filter("native")
@@ -160,7 +160,7 @@ def test_i8_sublaunches_and_query_blocks(idxmod, cuda):
 
 
 def test_i8_unsupported_width_and_bad_kind(idxmod, cuda):
-    dev = idxmod.DeviceIndex(768, dtype="float16", capacity=1000, device=cuda)
+    dev = idxmod.DeviceIndex(1000, dtype="float16", capacity=1000, device=cuda)  # ld 1024
     with pytest.raises(ValueError):
         dev.set_filter("i8")
     with pytest.raises(ValueError):
