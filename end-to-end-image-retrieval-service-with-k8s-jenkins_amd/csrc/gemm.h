@@ -71,77 +71,109 @@ __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
     __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4 *>(dst));
 }
 
-// Copy-out of the f32 epilogues (residual add / patch scatter + position): the
-// block's NT threads move NT / 64 · ROWS_PER_WAVE staged f32 rows (1-KB rows of 256
-// columns, 16-B chunk XOR (row & 63) in `smem`; output rows r0 .., columns n0 ..
-// n0 + 256), one row per wave per step, in passes of PASS rows: PASS residual /
-// position loads back to back, then the adds, the LN statistics of those rows
-// (branch-free, so their wave reductions interleave) and the stores.  HL: the
-// residual stream is the bf16 pair (a.ln_x, a.res_lo) (vit_kernels.h, "Residual
-// stream as bf16 pairs"); otherwise f32 a.out_f32, plus the bf16 copy and statistics
-// when a.ln_x is set.
-template <int EPI, int NT, int ROWS_PER_WAVE, int PASS = 8>
-__device__ __forceinline__ void resid_copy_out(const GemmArgs &a, const uint8_t *smem, int tid, int r0, int n0) {
+// f32 epilogues (residual add / patch scatter + position embedding, optionally the bf16
+// copy and LayerNorm partials), straight from the accumulators — no LDS, no barrier.
+// One wave, NR output rows per lane (rows[r]: lane li's row of row slot r, the same for
+// its four 16-lane groups g), each as two 32-column chunks c of the wave's 64 columns
+// [colw, colw + 64): A[r][c][h] = columns colw + 32c + 16h + 4g + 0..3 (the tiled kernels'
+// swapped-operand accumulator layout).  One v_permlane16_swap per accumulator register
+// pair gives lane g the 8 consecutive columns colw + 32c + ln_slice_col(g) — 16-B loads and
+// stores, and exactly the canonical LayerNorm slice of the lane (LN_PARTS), so the block
+// partial is two more swaps (ln_block_reduce_rows).  bq: the bias of those 8 columns.
+// Values: x = (acc + bias) + residual (or + position), the skinny kernel's order.  HL: the
+// residual stream is the bf16 pair (a.ln_x, a.res_lo); otherwise f32 a.out_f32, plus the
+// bf16 copy in a.ln_x and the partials when a.ln_x is set.  All lanes run the swaps; rows
+// >= M load a clamped row and store nothing.
+template <int EPI, int NR>
+__device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4 (&A)[NR][2][2], const int (&rows)[NR],
+                                                  int colw, int g, const float4 (&bq)[2][2]) {
     constexpr bool HL = epi_hl(EPI);
-    const int lane = tid & 63;
     const bool stats = HL ? a.ln_stats != nullptr : a.ln_x != nullptr;
+    const int cl = ln_slice_col(g, 0);
+    // every source load of the NR rows first (16 B each), then the arithmetic and stores
+    uint4 sh[NR][2], sl[NR][2];
+    float4 sf[NR][2][2];
 #pragma unroll
-    for (int p8 = 0; p8 < ROWS_PER_WAVE; p8 += PASS) {
-        float4 add[PASS];
-        uint4 addp[PASS];
+    for (int r = 0; r < NR; ++r) {
+        const int rr = rows[r] < a.M ? rows[r] : a.M - 1;
 #pragma unroll
-        for (int j = 0; j < PASS; ++j) {
-            const int id = (p8 + j) * NT + tid;
-            const int rl = id >> 6, ch = id & 63;
-            const int row = r0 + rl;
-            const int rr = row < a.M ? row : (r0 < a.M ? r0 : 0);  // clamp: keep the load in bounds, result unused
+        for (int c = 0; c < 2; ++c) {
+            const int col = colw + 32 * c + cl;
             if constexpr (epi_resid(EPI)) {
-                const int64_t off = (int64_t)rr * a.N + n0 + ch * 4;
-                if constexpr (HL) addp[j] = hl_load(a.ln_x + off, a.res_lo + off);
-                else add[j] = *reinterpret_cast<const float4 *>(a.out_f32 + off);
+                const int64_t off = (int64_t)rr * a.N + col;
+                if constexpr (HL) {
+                    sh[r][c] = *reinterpret_cast<const uint4 *>(a.ln_x + off);
+                    sl[r][c] = *reinterpret_cast<const uint4 *>(a.res_lo + off);
+                } else {
+                    sf[r][c][0] = *reinterpret_cast<const float4 *>(a.out_f32 + off);
+                    sf[r][c][1] = *reinterpret_cast<const float4 *>(a.out_f32 + off + 4);
+                }
             } else {
                 const int p = rr % (a.tokens - 1);
-                add[j] = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + n0 + ch * 4);
+                const float *pr = a.pos + (int64_t)(1 + p) * a.N + col;
+                sf[r][c][0] = *reinterpret_cast<const float4 *>(pr);
+                sf[r][c][1] = *reinterpret_cast<const float4 *>(pr + 4);
             }
         }
-        float4 o[PASS];
-        uint4 op[PASS];
+    }
 #pragma unroll
-        for (int j = 0; j < PASS; ++j) {
-            const int rl = ((p8 + j) * NT + tid) >> 6, ch = tid & 63;
-            const float4 v = *reinterpret_cast<const float4 *>(smem + rl * 1024 + ((ch ^ (rl & 63)) << 4));
-            float4 r;
-            if constexpr (EPI == EPI_RESID_HL) r = hl_value(addp[j]);
-            else r = add[j];
-            o[j] = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
-            if constexpr (HL) op[j] = hl_split(o[j]);
+    for (int r = 0; r < NR; ++r) {
+        const int row = rows[r];
+        int64_t orow = row;
+        if constexpr (epi_patch(EPI)) {
+            const int np = a.tokens - 1;
+            const int img = row / np, p = row - img * np;
+            orow = (int64_t)img * a.tokens + 1 + p;
         }
-        float2 st[PASS];
-        if (stats) {  // LayerNorm fold producer
+        const bool ok = row < a.M;
+        float xs[16];
 #pragma unroll
-            for (int j = 0; j < PASS; ++j) st[j] = ln_row_stats(HL ? hl_value(op[j]) : o[j]);
-        }
+        for (int c = 0; c < 2; ++c) {
+            float v[8];
 #pragma unroll
-        for (int j = 0; j < PASS; ++j) {
-            const int id = (p8 + j) * NT + tid;
-            const int rl = id >> 6, ch = id & 63;  // one row per wave: the branches below are uniform
-            const int row = r0 + rl;
-            if (row < a.M) {
-                int64_t orow = row;
-                if constexpr (epi_patch(EPI)) {
-                    const int np = a.tokens - 1;
-                    const int img = row / np, p = row - img * np;
-                    orow = (int64_t)img * a.tokens + 1 + p;
-                }
-                float *srow = a.ln_stats + (orow * LN_TILES + n0 / 256) * 2;
-                if constexpr (HL) {
-                    hl_store(op[j], a.ln_x + orow * a.N + n0 + ch * 4, a.res_lo + orow * a.N + n0 + ch * 4);
-                    if (stats && lane == 0) *reinterpret_cast<float2 *>(srow) = st[j];
-                } else {
-                    *reinterpret_cast<float4 *>(a.out_f32 + orow * a.N + n0 + ch * 4) = o[j];
-                    if (stats) ln_row_store(o[j], st[j], a.ln_x + orow * a.N + n0, srow, lane);
-                }
+            for (int j = 0; j < 4; ++j) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(A[r][c][0][j]),
+                                                                 __float_as_uint(A[r][c][1][j]), false, false);
+                v[j] = __uint_as_float(sw[0]);
+                v[4 + j] = __uint_as_float(sw[1]);
             }
+            const float b[8] = {bq[c][0].x, bq[c][0].y, bq[c][0].z, bq[c][0].w,
+                                bq[c][1].x, bq[c][1].y, bq[c][1].z, bq[c][1].w};
+            float add[8];
+            if constexpr (EPI == EPI_RESID_HL) {
+                hl8_value(sh[r][c], sl[r][c], add);
+            } else {
+                const float4 s0 = sf[r][c][0], s1 = sf[r][c][1];
+                add[0] = s0.x, add[1] = s0.y, add[2] = s0.z, add[3] = s0.w;
+                add[4] = s1.x, add[5] = s1.y, add[6] = s1.z, add[7] = s1.w;
+            }
+            float x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = (v[k] + b[k]) + add[k];
+            const int64_t off = orow * a.N + colw + 32 * c + cl;
+            if constexpr (HL) {
+                uint4 h, l;
+                float xv[8];
+                hl8_split(x, h, l, xv);
+                if (ok) {
+                    *reinterpret_cast<uint4 *>(a.ln_x + off) = h;
+                    *reinterpret_cast<uint4 *>(a.res_lo + off) = l;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
+            } else {
+                if (ok) {
+                    *reinterpret_cast<float4 *>(a.out_f32 + off) = make_float4(x[0], x[1], x[2], x[3]);
+                    *reinterpret_cast<float4 *>(a.out_f32 + off + 4) = make_float4(x[4], x[5], x[6], x[7]);
+                    if (stats) *reinterpret_cast<uint4 *>(a.ln_x + off) = bf16x8_pack(x);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) xs[8 * c + k] = x[k];
+            }
+        }
+        if (stats) {  // LayerNorm fold producer: this row's partial of the wave's 64-column block
+            const float2 st = ln_block_reduce_rows(ln_slice_stats(xs));
+            if (ok && g == 0) *reinterpret_cast<float2 *>(a.ln_stats + orow * LN_STRIDE + 2 * (colw >> 6)) = st;
         }
     }
 }
@@ -151,10 +183,10 @@ __device__ __forceinline__ void resid_copy_out(const GemmArgs &a, const uint8_t 
 // wc*64 + nq*32 + ni*16 + 4g + j).  smem: the ring (>= 128 KB, every read and DMA of the
 // K loop retired by its final barrier); ln_off: the LayerNorm-fold row scales (EPI_*_LN);
 // biasr: the bf16 epilogues' bias, loaded before the K loop.
-template <int EPI, int ABL>
+template <int EPI, int ABL, int NR = 4>
 __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2][4][2], uint8_t *smem, int ln_off,
-                                            int m0, int n0, const float4 (&biasr)[2][2]) {
-    const int tid = threadIdx.x, lane = tid & 63;
+                                            int m0, int n0, const float4 (&biasr)[2][2], int tid) {
+    const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wave >> 2, wc = wave & 3;
     const int g = lane >> 4, li = lane & 15;
@@ -294,39 +326,32 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
         }
         return;
     }
-    // f32 epilogues (residual add / patch scatter): the 256x256 f32 tile is 256 KB,
-    // so each group's 128 rows are staged in turn (1-KB rows, 16-B chunk XOR
-    // (row & 63)) and copied out by all 512 threads as whole 1-KB row segments:
-    // 16-B residual/pos loads issued back to back, then 16-B stores.
+    // f32 epilogues (residual add): straight from the accumulators, 4 rows per lane at a time
+    float4 bq[2][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (grp == h) {
-#pragma unroll
-            for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                for (int ni = 0; ni < 2; ++ni) {
-                    const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * g;
-                    const float4 bias = *reinterpret_cast<const float4 *>(a.bias + n0 + cl);
-#pragma unroll
-                    for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-                        for (int mi = 0; mi < 4; ++mi) {
-                            const int rl = mq * 64 + mi * 16 + li;  // row within the half
-                            const f32x4 v4 = acc[mq][nq][mi][ni];
-                            const int off = rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4);
-                            *reinterpret_cast<float4 *>(smem + off) =
-                                make_float4(v4[0] + bias.x, v4[1] + bias.y, v4[2] + bias.z, v4[3] + bias.w);
-                        }
-                }
-        }
-        __syncthreads();
-        // 16 rows per wave in two passes of 8 (registers: the other group's accumulators
-        // may still be live): 8 residual loads back to back, then the adds, the LN statistics
-        // of the 8 rows (branch-free, so their wave reductions interleave), and the stores
-        // (bf16 pairs: passes of 4 rows; 8 would spill beside the other group's accumulators)
-        resid_copy_out<EPI, 512, 16, epi_hl(EPI) ? 4 : 8>(a, smem, tid, m0 + h * 128, n0);
-        if (h == 0) __syncthreads();  // group 1 overwrites the staging rows next
+    for (int c = 0; c < 2; ++c) {
+        const float *bp = a.bias + n0 + wc * 64 + 32 * c + ln_slice_col(g, 0);
+        bq[c][0] = *reinterpret_cast<const float4 *>(bp);
+        bq[c][1] = *reinterpret_cast<const float4 *>(bp + 4);
     }
+    static_assert(NR == 1 || NR == 2 || NR == 4, "rows per lane per epilogue pass");
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int m4 = 0; m4 < 4; m4 += NR) {
+            f32x4 A[NR][2][2];
+            int rows[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int mi = m4 + r;
+                rows[r] = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) A[r][c][h] = acc[mq][c][mi][h];
+            }
+            f32_rows_epilogue<EPI, NR>(a, A, rows, n0 + wc * 64, g, bq);
+        }
 }
 
 // ----------------------------------------------------------- ping-pong GEMM --
@@ -349,33 +374,59 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
 // NKT: K / 64 fixed at compile time for the model's shapes (12: QKV / O-proj / fc1,
 // 48: fc2), 0 = from a.K.  It also names the launch: O-proj (EPI 6, NKT 12) and fc2
 // (EPI 6, NKT 48) share an epilogue but are separate rows in a kernel trace.
-template <int EPI, int ABL = 0, int NKT = 0>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
-    constexpr int BM = 256, BN = 256, BK = 64;
-    constexpr int A_BYTES = BM * BK * 2, STAGE = 2 * A_BYTES;  // A tile then W tile, 32 KB each
-    // LayerNorm-fold consumers keep the tile rows' (rstd, -rstd*mu) behind the ring (one
-    // __shared__ array: a second one would make hipcc drain the LDS-DMA queue every K-step)
-    constexpr int LN_LDS = epi_ln(EPI) ? BM * 8 : 0;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + LN_LDS];
+constexpr int PP_BM = 256, PP_BK = 64, PP_STAGE = 2 * PP_BM * PP_BK * 2;  // A tile then W tile, 32 KB each
 
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    const int g = lane >> 4, li = lane & 15;
+// Diagnostic builds (tools/build_diag.sh) only: s_memrealtime stamps of a workgroup's phases
+// into g_rc_stamps (set by rc_diag_set_stamps; tools/gemm_timeline.py reads them).  The
+// product build compiles RC_STAMP to nothing.
+#if defined(RC_GEMM_ABLATION)
+static __device__ uint64_t *g_rc_stamps = nullptr;
+#define RC_STAMP(idx, val)                                                 \
+    do {                                                                    \
+        if (g_rc_stamps != nullptr && threadIdx.x == 0) g_rc_stamps[idx] = (val); \
+    } while (0)
+#else
+#define RC_STAMP(idx, val) \
+    do {                   \
+    } while (0)
+#endif
+#define RC_NOW() __builtin_amdgcn_s_memrealtime()
 
-    const int ntn = a.N / BN;
-    const int nwg = gridDim.x, orig = blockIdx.x;
+// XCD-aware bijective remap of blockIdx.x: blocks b, b + 8, ... share an XCD and get a
+// contiguous run of ids
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    int tm = tile / ntn, tn = tile % ntn;
-    if (a.group_m > 0) {  // groups of group_m row tiles, column-major inside a group
-        const int ntm = (a.M + BM - 1) / BM;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+}
+// tile id -> (row tile, column tile): row-major, or groups of group_m row tiles walked
+// column-major inside a group
+__device__ __forceinline__ void pp_tile_coords(const GemmArgs &a, int tile, int &tm, int &tn) {
+    const int ntn = a.N / PP_BM;
+    tm = tile / ntn;
+    tn = tile % ntn;
+    if (a.group_m > 0) {
+        const int ntm = (a.M + PP_BM - 1) / PP_BM;
         const int gt = a.group_m * ntn, gi = tile / gt, in = tile - gi * gt;
         const int gm = min(a.group_m, ntm - gi * a.group_m);
         tm = gi * a.group_m + in % gm;
         tn = in / gm;
     }
-    const int m0 = tm * BM, n0 = tn * BN;
+}
+
+// Prologue + K loop of one 256x256 tile over the K-steps [kb, ke) (64 deep each), adding
+// into acc (which the caller zeroes, or loads with a partial sum of the K-steps before kb:
+// the MFMA chain then continues exactly as if it had run from 0).  The ping-pong schedule
+// described above gemm_pp_kernel.  smem: the 2-stage ring (2 * PP_STAGE) then, for the
+// LayerNorm-fold consumers, the tile rows' (rstd, -rstd*mu) at 2 * PP_STAGE.  On return
+// every wave has passed the loop's last barrier (the ring is free for the epilogue).
+template <int EPI, int ABL>
+__device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m0, int n0, int kb, int ke,
+                                         f32x4 (&acc)[2][2][4][2], int tid, int64_t sb = -1) {
+    constexpr int BM = PP_BM, BK = PP_BK, A_BYTES = BM * BK * 2, STAGE = PP_STAGE;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
     const int K = a.K;
     const uint16_t *Ag = a.A + (int64_t)m0 * K;
     const uint16_t *Wg = a.W + (int64_t)n0 * K;
@@ -398,49 +449,26 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-
-    f32x4 acc[2][2][4][2];
-#pragma unroll
-    for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-        for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-            for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // bf16 epilogues: bias of this lane's 16 output columns, loaded before the K
-    // loop so its latency hides under the prologue wait instead of stalling the
-    // epilogue (the f32 epilogues keep their own load: 16 more live VGPRs there spill)
-    float4 biasr[2][2];
-    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-                biasr[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
-    }
-
-    const int nk = NKT > 0 ? NKT : K / BK;
     auto kofs = [](int kt) { return kt * BK; };
-    stage4(0, kofs(0), 0);
-    stage4(0, kofs(0), 4);
+    stage4(0, kofs(kb), 0);
+    stage4(0, kofs(kb), 4);
     if constexpr (epi_ln(EPI)) {  // LayerNorm fold: this tile's row scales, under the first DMA
         if (tid < BM)
             *reinterpret_cast<float2 *>(smem + 2 * STAGE + tid * 8) =
-                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * (2 * LN_TILES), a.ln_eps);
+                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * LN_STRIDE, a.ln_eps);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
+    if (sb >= 0) RC_STAMP(sb, RC_NOW());
     if (grp == 1) bar();  // stagger: G1 one segment behind
 
     bf16x8 af[4][2], wf[2][2];  // [mi][s], [ni][s]
 #pragma nounroll
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
+    for (int kt = kb; kt < ke; ++kt) {
+        const int cur = (kt - kb) & 1;
         const uint8_t *As = smem + cur * STAGE;
         const uint8_t *Ws = As + A_BYTES;
-        const bool more = kt + 1 < nk;
+        const bool more = kt + 1 < ke;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int mq = p >> 1;                 // quadrant rows
@@ -486,6 +514,50 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         }
     }
     if (grp == 0) bar();  // balance the stagger barrier
+    if (sb >= 0) RC_STAMP(sb + 1, RC_NOW());
+}
+
+// bf16 epilogues: bias of this lane's 16 output columns, loaded before the K loop so its
+// latency hides under the prologue wait (the other epilogues load their own)
+template <int EPI>
+__device__ __forceinline__ void pp_bias_regs(const GemmArgs &a, int n0, float4 (&biasr)[2][2], int tid) {
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        const int lane = tid & 63, g = lane >> 4;
+        const int wc = __builtin_amdgcn_readfirstlane(tid >> 6) & 3;
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                biasr[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
+    }
+}
+
+template <int EPI, int ABL = 0, int NKT = 0>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+    // LayerNorm-fold consumers keep the tile rows' (rstd, -rstd*mu) behind the ring (one
+    // __shared__ array: a second one would make hipcc drain the LDS-DMA queue every K-step)
+    constexpr int LN_LDS = epi_ln(EPI) ? PP_BM * 8 : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + LN_LDS];
+    int tm, tn;
+    pp_tile_coords(a, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * PP_BM, n0 = tn * PP_BM;
+
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+        for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+            for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int64_t sb = (int64_t)blockIdx.x * 64;
+    RC_STAMP(sb, RC_NOW());
+    RC_STAMP(sb + 4, (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) | ((uint64_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32));
+    RC_STAMP(sb + 5, (uint64_t)(m0 / PP_BM) | ((uint64_t)(n0 / PP_BM) << 32));
+    float4 biasr[2][2];
+    pp_bias_regs<EPI>(a, n0, biasr, threadIdx.x);
+    pp_kloop<EPI, ABL>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, threadIdx.x, sb + 1);
     if constexpr ((ABL & 4) != 0) {
 #pragma unroll
         for (int a0 = 0; a0 < 2; ++a0)
@@ -497,8 +569,167 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                     for (int a3 = 0; a3 < 2; ++a3) asm volatile("" ::"v"(acc[a0][a1][a2][a3]));
         return;
     }
+    pp_epilogue<EPI, ABL>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, threadIdx.x);
+    RC_STAMP(sb + 3, RC_NOW());
+}
 
-    pp_epilogue<EPI, ABL>(a, acc, smem, 2 * STAGE, m0, n0, biasr);
+// ----------------------------------------------------------- stream-K GEMM --
+// The ping-pong tile and K loop as a persistent kernel over an even split of the
+// tiles x K-steps "units" (stream-K): virtual workgroup v (XCD-contiguous, xcd_remap)
+// owns units [U·v/G, U·(v+1)/G), U = tiles · nk, at least nk of them (G <= tiles).  Two
+// things the one-tile-per-workgroup grid cannot do: (1) no partial last round (the N =
+// 768 GEMMs have 2.31 rounds of 256 tiles: the third runs 31 % full), and (2) the
+// epilogues — HBM-bound bursts of residual reads and stores (O-proj, fc2) or store bursts
+// (QKV, fc1) — fall at different times on different CUs instead of all at once, so they
+// overlap other CUs' MFMA main loops.
+// A tile split between workgroups v (ends its range inside it) and v + 1 (starts inside
+// it) stays bit-identical to the unsplit tile: v + 1 runs the chain-FIRST K-steps
+// [0, nk - c) at its start and stores the f32 accumulators (ws slot v + 1, lane-linear
+// 256 KB) with an agent-scope release + flag = epoch; v, at the end of its range, polls the
+// flag, acquires, loads the partial into its accumulators and continues the MFMA chain over
+// [nk - c, nk) — the same chain, in the same K order, as gemm_pp_kernel and the skinny
+// kernel.  The flag was set ~(units per workgroup − nk) K-steps earlier, so the poll
+// normally succeeds at once; if it does not within SK_WAIT_TICKS (v + 1 not resident), v
+// recomputes the whole tile itself (same bits), so no launch can deadlock on residency.
+// a.sk_epoch must differ from every earlier launch on the same flags (the host counts).
+// Hand-off (MI355X_MICROARCH.md, "Valid forms", first table row): the partial is stored
+// write-through (sc1) by every wave, each wave waits vmcnt(0), a workgroup barrier, then
+// one lane's sc1 flag store; the consumer's lane 0 polls with sc1 loads, the workgroup
+// barrier follows, and every load of the partial is an sc1 load — no L2 write-back or
+// invalidate (an agent release here wrote back the XCD's whole dirty L2 per hand-off).
+constexpr int SK_SC1 = 16;         // buffer-instruction cache policy bit sc1 (gfx940+ CPol::SC1)
+constexpr int SK_EPI_ROWS = 2;       // f32 epilogue rows per pass (4 spills beside the persistent loop's state)
+constexpr int SK_WAIT_TICKS = 4000;  // s_memrealtime ticks (100 MHz): 40 us
+
+// Bands (a.sk_band = B > 1, B = the column tiles of a row, N = 256·B): the split unit is a
+// row tile's K-steps, and B workgroups of one XCD (consecutive virtual ids) walk the same
+// row tiles in lockstep, one column tile each, so the A K-slab each reads is the one its
+// band partners read at the same time (one L2 fill serves B workgroups — the sharing the
+// one-tile grid gets from its row-major order and plain stream-K loses).  Bands, not
+// workgroups, then take even shares of the units; the grid is 8 XCDs x (bands per XCD) x B.
+template <int EPI, int NKT = 0>
+__global__ __launch_bounds__(512, 1) void gemm_sk_kernel(GemmArgs a) {
+    constexpr int LN_LDS = epi_ln(EPI) ? PP_BM * 8 : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + LN_LDS + 16];
+    const int tid = threadIdx.x;
+    const int nk = NKT > 0 ? NKT : a.K / PP_BK;
+    const int ntm = (a.M + PP_BM - 1) / PP_BM, ntn = a.N / PP_BM;
+    const int G = gridDim.x, v = xcd_remap(blockIdx.x, G);
+    const int B = a.sk_band > 1 ? a.sk_band : 1;
+    // band member (column tile in band mode) and band index; band b's workgroups are the
+    // B consecutive virtual ids b·B .. b·B + B - 1 (one XCD when G / 8 is a multiple of B)
+    const int member = v % B, band = v / B, NB = G / B;
+    const int64_t U = (int64_t)(B > 1 ? ntm : ntm * ntn) * nk;
+    const int64_t u1 = U * (band + 1) / NB;
+    int *okflag = reinterpret_cast<int *>(smem + 2 * PP_STAGE + LN_LDS);
+    // partial-sum slots as buffer resources: lane-linear f32x4 i of lane tid at byte
+    // i * 8192 + tid * 16 (SGPR offsets, no per-access VGPR address); slot = virtual id,
+    // the producer of a tail's partial is the same member of the next band (id v + B)
+    const __amdgpu_buffer_rsrc_t ws_mine = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.sk_ws + (int64_t)v * (PP_BM * PP_BM)), (short)0, PP_BM * PP_BM * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ws_next = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.sk_ws + (int64_t)(v + B) * (PP_BM * PP_BM)), (short)0, PP_BM * PP_BM * 4, 0x00020000);
+    if (band >= NB) return;  // (G a multiple of B: never)
+    bool first = true;
+    int seg = 0;
+    RC_STAMP((int64_t)blockIdx.x * 64 + 63, (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                                               ((uint64_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32));
+    for (int64_t u = U * band / NB; u < u1;) {
+        // a per-segment copy of the thread index: keeps hipcc from hoisting every per-lane
+        // address of the K loop and the epilogue out of the segment loop (they spilled)
+        int ltid = tid;
+        asm volatile("" : "+v"(ltid));
+        const int T = (int)(u / nk), j = (int)(u - (int64_t)T * nk);
+        const int64_t tile_end = (int64_t)(T + 1) * nk, seg_end = tile_end < u1 ? tile_end : u1;
+        // kind 0: whole tile; 1: head of this range inside T (chain-first K-steps, partial
+        // out); 2: tail of this range inside T (partial of v + 1 in, then the last K-steps)
+        const int kind = j > 0 ? 1 : (seg_end < tile_end ? 2 : 0);
+        int kb = 0, ke = nk;
+        if (kind == 1) ke = nk - j;
+        if (kind == 2) kb = nk - (int)(seg_end - (int64_t)T * nk);
+        int tm, tn;
+        if (B > 1) {
+            tm = T;
+            tn = member;
+        } else {
+            pp_tile_coords(a, T, tm, tn);
+        }
+        const int m0 = tm * PP_BM, n0 = tn * PP_BM;
+        if (!first) __builtin_amdgcn_s_barrier();  // the last epilogue's LDS reads are done
+        first = false;
+        const int64_t sb = seg < 7 ? (int64_t)blockIdx.x * 64 + seg * 8 : -1;
+        ++seg;
+        if (sb >= 0) {
+            RC_STAMP(sb, RC_NOW());
+            RC_STAMP(sb + 4, (uint64_t)T | ((uint64_t)kind << 32));
+            RC_STAMP(sb + 5, (uint64_t)kb | ((uint64_t)ke << 32));
+        }
+
+        f32x4 acc[2][2][4][2];
+#pragma unroll
+        for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+            for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+                for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                    for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (kind == 2) {
+            if (tid == 0) {
+                const int *flag = a.sk_flags + v + B;
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                int ok = 1;
+                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.sk_epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)SK_WAIT_TICKS) {
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                *okflag = ok;
+            }
+            __syncthreads();
+            if (*okflag) {
+#pragma unroll
+                for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+                    for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+                        for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                            for (int a3 = 0; a3 < 2; ++a3)
+                                acc[a0][a1][a2][a3] = __builtin_bit_cast(
+                                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               ws_next, ltid * 16, ((((a0 * 2 + a1) * 4 + a2) * 2 + a3) * 8192), SK_SC1));
+            } else {
+                kb = 0;  // v + 1 never published: run the whole chain here
+            }
+        }
+        float4 biasr[2][2];
+        pp_bias_regs<EPI>(a, n0, biasr, ltid);
+        pp_kloop<EPI, 0>(a, smem, m0, n0, kb, ke, acc, ltid, sb >= 0 ? sb + 1 : -1);
+        if (kind == 1) {
+            typedef int i32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+                for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+                    for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+                        for (int a3 = 0; a3 < 2; ++a3)
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[a0][a1][a2][a3]), ws_mine,
+                                                                       ltid * 16,
+                                                                       ((((a0 * 2 + a1) * 4 + a2) * 2 + a3) * 8192), SK_SC1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(a.sk_flags + v, a.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            pp_epilogue<EPI, 0, SK_EPI_ROWS>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, ltid);
+        }
+        if (sb >= 0) RC_STAMP(sb + 3, RC_NOW());
+        u = seg_end;
+    }
 }
 
 // --------------------------------------------------------------- ring GEMM --
@@ -608,7 +839,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
     if constexpr (epi_ln(EPI)) {
         if (tid < BM)
             *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) =
-                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * (2 * LN_TILES), a.ln_eps);
+                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * LN_STRIDE, a.ln_eps);
     }
     if (nk >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -662,22 +893,23 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
         }
     }
     if (grp == 0) bar();  // balance the stagger barrier
-    pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr);
+    pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr, threadIdx.x);
 }
 
 // Epilogue of a 128 x 256 tile held as acc[mi][ni] by 4 waves (wave w: columns
 // [64w, 64w + 64)): acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + w*64 + ni*16 + 4g + j].
-// Stages through `smem` (>= 64 KB; the caller's main loop must be done with it).
+// The bf16 epilogues stage through `smem` (>= 64 KB; the caller's main loop must be done
+// with it); the f32 ones store from the accumulators.
 template <int EPI>
 __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4], uint8_t *smem, int m0, int n0) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
-    float4 bias[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
-    __syncthreads();  // every wave's last fragment reads are done: the ring is free
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        float4 bias[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
+        __syncthreads();  // every wave's last fragment reads are done: the ring is free
         // 128 x 256 bf16 tile staged in LDS (512-B rows, 16-B chunk XOR (row & 31)),
         // stored as whole 512-B row segments, 16 B per lane.
 #pragma unroll
@@ -710,28 +942,27 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
         }
         return;
     }
-    // f32 epilogues: two halves of 64 rows (64 KB each: 1-KB rows, 16-B chunk XOR
-    // (row & 63)), copied out as whole 1-KB row segments with the residual /
-    // position loads issued back to back before the adds and stores.
+    // f32 epilogues: straight from the accumulators (f32_rows_epilogue), 4 rows per lane at a time
+    float4 bq[2][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int c = 0; c < 2; ++c) {
+        const float *bp = a.bias + n0 + wave * 64 + 32 * c + ln_slice_col(g, 0);
+        bq[c][0] = *reinterpret_cast<const float4 *>(bp);
+        bq[c][1] = *reinterpret_cast<const float4 *>(bp + 4);
+    }
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            const int cl = wave * 64 + ni * 16 + 4 * g;
+    for (int h4 = 0; h4 < 2; ++h4) {
+        f32x4 A[4][2][2];
+        int rows[4];
 #pragma unroll
-            for (int mq = 0; mq < 4; ++mq) {
-                const int rl = mq * 16 + li;
-                const f32x4 v4 = acc[h * 4 + mq][ni];
-                *reinterpret_cast<float4 *>(smem + rl * 1024 + (((cl >> 2) ^ (rl & 63)) << 4)) =
-                    make_float4(v4[0] + bias[ni].x, v4[1] + bias[ni].y, v4[2] + bias[ni].z, v4[3] + bias[ni].w);
-            }
+        for (int r = 0; r < 4; ++r) {
+            rows[r] = m0 + (h4 * 4 + r) * 16 + li;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) A[r][c][h] = acc[h4 * 4 + r][2 * c + h];
         }
-        __syncthreads();
-        // 16 rows per wave in two passes of 8: 8 residual loads back to back, then the adds,
-        // the LN statistics of the 8 rows (branch-free, so their wave reductions interleave),
-        // and the stores
-        resid_copy_out<EPI, 256, 16>(a, smem, tid, m0 + h * 64, n0);
-        if (h == 0) __syncthreads();  // the second half overwrites the staging rows
+        f32_rows_epilogue<EPI, 4>(a, A, rows, n0 + wave * 64, g, bq);
     }
 }
 
@@ -1018,7 +1249,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
     }
     if (row >= a.M) return;
     float2 lrs;  // LayerNorm fold: this row's (rstd, -rstd*mu), as gemm_pp_kernel computes it
-    if constexpr (epi_ln(EPI)) lrs = ln_row_scale(a.ln_stats + (int64_t)row * (2 * LN_TILES), a.ln_eps);
+    if constexpr (epi_ln(EPI)) lrs = ln_row_scale(a.ln_stats + (int64_t)row * LN_STRIDE, a.ln_eps);
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
         const int c = n0 + ni * 16 + 4 * g;
@@ -1125,25 +1356,36 @@ inline void launch_skinny_splitk_resid(const GemmArgs &a, float *part, hipStream
     RC_LAUNCH_CHECK();
 }
 
-// LayerNorm-fold producer pass for rows a skinny GEMM wrote (M <= 256): one wave per
-// (row, 256-column tile), the same lane -> column map and reductions as the tiled
-// kernels' epilogues (ln_emit_row), so the partials are bit-identical for any M.
-// lo != null: the rows are the bf16 pairs (ln_x, lo); only the statistics are written.
+// LayerNorm-fold producer pass for rows a skinny GEMM wrote (M <= 256): four lanes per
+// (row, 64-column block), one canonical slice each (vit_kernels.h, LN_PARTS) and the same
+// reduction tree as the tiled epilogues, so the partials are bit-identical for any M.
+// lo != null: the rows are the bf16 pairs (ln_x, lo), only the partials are written;
+// otherwise x is the f32 stream and ln_x receives its bf16 copy.
 __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ x, uint16_t *__restrict__ ln_x,
                                                      const uint16_t *__restrict__ lo, float *__restrict__ ln_stats, int M) {
-    const int lane = threadIdx.x & 63;
-    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (item >= M * LN_TILES) return;  // wave-uniform
-    const int row = item / LN_TILES, t = item - row * LN_TILES;
-    const int64_t off = (int64_t)row * 256 * LN_TILES + t * 256;
-    float *srow = ln_stats + ((int64_t)row * LN_TILES + t) * 2;
-    if (lo != nullptr) {
-        const float2 st = ln_row_stats(hl_value(hl_load(ln_x + off + 4 * lane, lo + off + 4 * lane)));
-        if (lane == 0) *reinterpret_cast<float2 *>(srow) = st;
-        return;
+    constexpr int H = 64 * LN_PARTS;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int item = t >> 2, g = t & 3;
+    const bool ok = item < M * LN_PARTS;  // every lane joins the shuffles; only valid items store
+    const int it = ok ? item : 0;
+    const int row = it / LN_PARTS, blk = it - row * LN_PARTS;
+    float xs[16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int64_t off = (int64_t)row * H + blk * 64 + ln_slice_col(g, c);
+        float v[8];
+        if (lo != nullptr) {
+            hl8_value(*reinterpret_cast<const uint4 *>(ln_x + off), *reinterpret_cast<const uint4 *>(lo + off), v);
+        } else {
+            const float4 a = *reinterpret_cast<const float4 *>(x + off), b = *reinterpret_cast<const float4 *>(x + off + 4);
+            v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+            if (ok) *reinterpret_cast<uint4 *>(ln_x + off) = bf16x8_pack(v);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xs[8 * c + k] = v[k];
     }
-    const float4 v = reinterpret_cast<const float4 *>(x + off)[lane];
-    ln_emit_row(v, ln_x + off, srow, lane, true);
+    const float2 st = ln_block_reduce_quad(ln_slice_stats(xs), g);
+    if (ok && g == 0) *reinterpret_cast<float2 *>(ln_stats + (int64_t)row * LN_STRIDE + 2 * blk) = st;
 }
 
 // Kernel choice: 4 = ping-pong 256x256, 8 = two-workgroup 128x256, 9 = skinny
@@ -1152,7 +1394,9 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 // (Rounds 1-2 also measured a 128x128 4-wave kernel, a 256x256 / 128x256 single-
 // barrier kernel, a persistent kernel, Stream-K and a deferred-store persistent
 // kernel: each lost on every shape and was removed.)
-enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9 };
+enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_STREAMK = 7, GEMM_W2 = 8,
+                   GEMM_SKINNY = 9 };
+constexpr int SK_MAX_GRID = 512;  // partial-sum slots / flags a stream-K workspace provides
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
@@ -1203,7 +1447,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
+        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_STREAMK ||
+                    pick == GEMM_SKINNY) && a.ln_c &&
                        a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
     }
     switch (pick) {
@@ -1240,10 +1485,35 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
             if (a.ln_x != nullptr && a.ln_stats != nullptr) {  // LayerNorm-fold producer: the partials in a second pass
                 RC_LAUNCH_CHECK();
-                RC_REQUIRE(a.N == 256 * LN_TILES, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
-                hipLaunchKernelGGL(ln_emit_kernel, dim3((a.M * LN_TILES + 3) / 4), dim3(256), 0, s, a.out_f32, a.ln_x,
+                RC_REQUIRE(a.N == 64 * LN_PARTS, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
+                hipLaunchKernelGGL(ln_emit_kernel, dim3((a.M * LN_PARTS + 63) / 64), dim3(256), 0, s, a.out_f32, a.ln_x,
                                    a.res_lo, a.ln_stats, a.M);
             }
+            break;
+        }
+        case GEMM_STREAMK: {
+            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
+            RC_REQUIRE(a.sk_ws && a.sk_flags && a.sk_grid >= 1 && a.sk_grid <= SK_MAX_GRID, RC_ERR_INVALID,
+                       "stream-K GEMM needs a workspace (sk_ws, sk_flags, sk_grid <= SK_MAX_GRID)");
+            a.group_m = gemm_group_m(a);
+            // band mode for short rows (N <= 1024: 2-4 column tiles); every band's or
+            // workgroup's range must span >= one tile of K-steps: grid <= tiles (bands <= row tiles)
+            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
+            int grid;
+            if (ntn >= 2 && ntn <= 4 && a.sk_band != 1) {
+                a.sk_band = ntn;
+                int bands = std::max(1, a.sk_grid / ntn);
+                if (bands >= 8) bands = bands / 8 * 8;  // whole XCD blocks of bands
+                bands = std::min(bands, ntm);
+                grid = bands * ntn;
+            } else {
+                a.sk_band = 1;
+                grid = std::min(a.sk_grid, ntm * ntn);
+            }
+            const dim3 gr(grid), bl(512);
+            if (a.K == 768) hipLaunchKernelGGL((gemm_sk_kernel<EPI, 12>), gr, bl, 0, s, a);
+            else if (a.K == 3072) hipLaunchKernelGGL((gemm_sk_kernel<EPI, 48>), gr, bl, 0, s, a);
+            else hipLaunchKernelGGL((gemm_sk_kernel<EPI>), gr, bl, 0, s, a);
             break;
         }
         case GEMM_PINGPONG: {

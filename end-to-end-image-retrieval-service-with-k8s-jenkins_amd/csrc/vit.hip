@@ -9,7 +9,7 @@
 //             biases / LayerNorm params / cls / pos — f32
 //   workspace (sized for max_batch images, rows padded to the GEMM tile):
 //             residual stream: under the LayerNorm fold the bf16 pair ln = RNE(x),
-//             res_lo = RNE(x − ln) [Mp][H] with ln_stats f32 [Mp][3][2]; without it
+//             res_lo = RNE(x − ln) [Mp][H] with ln_stats f32 [Mp][LN_PARTS][2]; without it
 //             hidden f32 [Mp][H] and ln bf16 [Mp][H] = LayerNorm output; qkv bf16
 //             [Mp][3H], attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
 #include <algorithm>
@@ -78,7 +78,7 @@ struct rc_model {
     uint16_t *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
     uint16_t *res_lo = nullptr;  // LayerNorm fold: low halves of the residual stream's bf16 pairs
-    float *ln_stats = nullptr;     // [Mp][3][2] LayerNorm-fold partials (per 256-column tile: mean, M2)
+    float *ln_stats = nullptr;     // [Mp][LN_PARTS][2] LayerNorm-fold partials (per 64-column block: mean, M2)
     bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
     bool cls_only_last = true;     // rc_model_set_last_layer
@@ -89,6 +89,12 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // diagnostic builds: RC_GEMM_VARIANT (ablation variants)
+    // stream-K projection GEMMs (gemm_sk_kernel): per batch part a partial-sum workspace and
+    // flags, the launch epoch, and the part whose encode is being issued (host-sequential)
+    float *sk_ws[4] = {};
+    int *sk_flags[4] = {};
+    int sk_epoch[4] = {};
+    int sk_grid = 0, cur_part = 0, active_parts = 1;
     int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -342,12 +348,43 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
 }
 
 // role: T_QKV / T_OPROJ / T_FC1 / T_FC2 (its own timer besides T_GEMM), or -1
+// stream-K workspace of one batch part: partial-sum slots and flags for sk_grid workgroups
+void ensure_streamk(rc_model *m) {
+    if (m->sk_grid > 0) return;
+    int cus = 0;
+    RC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->device));
+    m->sk_grid = std::max(8, std::min(cus, SK_MAX_GRID));
+    for (int p = 0; p < kMaxParts; ++p) {
+        m->sk_ws[p] = (float *)m->alloc((size_t)m->sk_grid * 256 * 256 * 4);
+        m->sk_flags[p] = (int *)m->alloc((size_t)m->sk_grid * 4);
+        RC_HIP(hipMemset(m->sk_flags[p], 0, (size_t)m->sk_grid * 4));
+    }
+}
+
 template <int EPI>
-void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
+void gemm(rc_model *m, const GemmArgs &a_in, hipStream_t s, int role = -1) {
+    GemmArgs a = a_in;
+    int variant = m->gemm_variant;
+    // stream-K: 7 = the short-row projections (O-proj, fc2: N = 768) as bands, the wide ones
+    // (QKV, fc1) on the ping-pong kernel; 17 = every projection (A/B)
+    if (variant == GEMM_STREAMK + 10) variant = GEMM_STREAMK;
+    else if (variant == GEMM_STREAMK && a.N > 1024) variant = GEMM_PINGPONG;
+    if (variant == GEMM_STREAMK) {
+        if (a.M > 256 && a.N % 256 == 0 && m->sk_grid > 0) {
+            const int p = m->cur_part;
+            a.sk_ws = m->sk_ws[p];
+            a.sk_flags = m->sk_flags[p];
+            a.sk_epoch = ++m->sk_epoch[p];
+            // concurrent parts share the CUs: each part's grid takes its share
+            a.sk_grid = std::max(8, m->sk_grid / std::max(1, m->active_parts));
+        } else {
+            variant = GEMM_AUTO;
+        }
+    }
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = role >= 0 ? m->timers[role].begin(s) : -1;
-    launch_gemm<EPI>(a, m->gemm_variant, s);
+    launch_gemm<EPI>(a, variant, s);
     if (role >= 0) m->timers[role].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
@@ -382,7 +419,7 @@ void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *
     // CLS rows alone, from their bf16 rows and statistics gathered compact (same arithmetic
     // as the full QKV GEMM: the skinny / tiled kernels give a row the same bits at any M)
     const bool q_cls = m->ln_fold && hi != nullptr;
-    float *cst = m->cls_stats + (int64_t)i0 * 2 * LN_TILES;
+    float *cst = m->cls_stats + (int64_t)i0 * LN_STRIDE;
     uint16_t *qc = m->cls_mlp + (int64_t)i0 * c.mlp;  // [n][H] compact queries (fc1 overwrites it later)
     hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, hi, lo, T, hc, q_cls ? lc : nullptr,
                        st_rows, cst);
@@ -402,7 +439,7 @@ void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *
     m->timers[T_ATTN].end(ta, s, 4.0 * items * (double)T * (H / c.heads));
     GemmArgs o{ac, L.w_o, L.b_o, n, H, H, nullptr, hc, nullptr, 1};
     if (m->ln_fold) {  // LN2 folded into fc1, as in the other layers
-        float *st = m->cls_stats + (int64_t)i0 * 2 * LN_TILES;
+        float *st = m->cls_stats + (int64_t)i0 * LN_STRIDE;
         o.ln_x = lc;
         o.ln_stats = st;
         gemm<EPI_RESID_F32>(m, o, s);
@@ -443,7 +480,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
     // their epilogues.  The same arithmetic at every batch size (skinny GEMMs for
     // M <= 256 included), so an image's embedding does not depend on its batch.
     const bool fold = m->ln_fold;
-    float *st = m->ln_stats + r0 * 2 * LN_TILES;
+    float *st = m->ln_stats + r0 * LN_STRIDE;
     uint16_t *lo = fold ? m->res_lo + r0 * H : nullptr;  // the residual stream is the pair (ln, lo)
     auto produce = [&](GemmArgs a, bool emit) {
         if (fold) {
@@ -540,7 +577,9 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
     // bursts overlap another part's MFMA main loops
     int parts = std::max(1, std::min(m->split, kMaxParts));
     while (parts > 1 && n < parts * m->split_min) --parts;
+    m->active_parts = parts;
     if (parts == 1) {
+        m->cur_part = 0;
         encode(m, src, 0, n, raw, normed, s);
         return;
     }
@@ -548,6 +587,7 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
     for (int p = 1; p < parts; ++p) RC_HIP(hipStreamWaitEvent(m->sp[p], m->ev_fork, 0));
     for (int p = 0; p < parts; ++p) {
         const int i0 = (int)((int64_t)n * p / parts), i1 = (int)((int64_t)n * (p + 1) / parts);
+        m->cur_part = p;
         encode(m, src, i0, i1 - i0, raw, normed, p == 0 ? s : m->sp[p]);
     }
     for (int p = 1; p < parts; ++p) {
@@ -581,8 +621,8 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             // + one tile: the second half of a split batch reads whole tiles past its last row
             m->Mp = round_up(B * m->tokens, gemm_row_pad()) + gemm_row_pad();
             m->hidden = (float *)m->alloc((size_t)m->Mp * H * 4);
-            m->ln_stats = (float *)m->alloc((size_t)m->Mp * 2 * LN_TILES * 4);
-            RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * 2 * LN_TILES * 4));  // pad rows: finite scales
+            m->ln_stats = (float *)m->alloc((size_t)m->Mp * LN_STRIDE * 4);
+            RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * LN_STRIDE * 4));  // pad rows: finite scales
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->res_lo = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->qkv = (uint16_t *)m->alloc((size_t)m->Mp * 3 * H * 2);
@@ -591,9 +631,9 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->resized = (uint8_t *)m->alloc((size_t)B * cfg->image_size * cfg->image_size * 3);
             const int Cp = B + gemm_row_pad();  // compact CLS streams (+ the rows a tile reads past n)
             m->cls_hidden = (float *)m->alloc((size_t)Cp * H * 4);
-            m->cls_stats = (float *)m->alloc((size_t)Cp * 2 * LN_TILES * 4);
+            m->cls_stats = (float *)m->alloc((size_t)Cp * LN_STRIDE * 4);
             m->cls_part = (float *)m->alloc((size_t)SKINNY_KS * Cp * H * 4);
-            RC_HIP(hipMemset(m->cls_stats, 0, (size_t)Cp * 2 * LN_TILES * 4));
+            RC_HIP(hipMemset(m->cls_stats, 0, (size_t)Cp * LN_STRIDE * 4));
             m->cls_ln = (uint16_t *)m->alloc((size_t)Cp * H * 2);
             m->cls_attn = (uint16_t *)m->alloc((size_t)Cp * H * 2);
             m->cls_mlp = (uint16_t *)m->alloc((size_t)Cp * cfg->mlp * 2);
@@ -812,9 +852,12 @@ int rc_model_set_parts(rc_model *m, int parts) {
 int rc_model_set_gemm_variant(rc_model *m, int variant) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
-        RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING4 || variant == GEMM_RING3,
-                   RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 or 6 (ring)");
+        RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING4 || variant == GEMM_RING3 ||
+                       variant == GEMM_STREAMK || variant == GEMM_STREAMK + 10,
+                   RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 or 6 (ring), 7 (stream-K)");
         std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        if (variant == GEMM_STREAMK || variant == GEMM_STREAMK + 10) ensure_streamk(m);
         m->gemm_variant = variant;
     });
 }
@@ -846,12 +889,41 @@ int rc_model_timing_reset(rc_model *m) {
 
 }  // extern "C"
 
+#if defined(RC_GEMM_ABLATION)
+// diagnostic builds: device buffer (>= 64 stamps per workgroup of the largest grid) for the
+// GEMM kernels' phase stamps, or null to stop stamping
+extern "C" int rc_diag_set_stamps(void *dev) {
+    return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rc_stamps), &dev, sizeof(dev))); });
+}
+#endif
+
 extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N,
                             int K, void *out, const float *pos, int tokens, void *stream) {
     return guard([&] {
         RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
         GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
         hipStream_t s = (hipStream_t)stream;
+        if (variant == GEMM_STREAMK) {  // the test hook's own stream-K workspace (one per process, current device)
+            static std::mutex mu;
+            static float *ws = nullptr;
+            static int *flags = nullptr, epoch = 0, grid = 0;
+            std::lock_guard<std::mutex> lk(mu);
+            if (!ws) {
+                int dev = 0, cus = 0;
+                RC_HIP(hipGetDevice(&dev));
+                RC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+                grid = std::max(8, std::min(cus, SK_MAX_GRID));
+                ws = (float *)dmalloc((size_t)grid * 256 * 256 * 4);
+                flags = (int *)dmalloc((size_t)grid * 4);
+                RC_HIP(hipMemset(flags, 0, (size_t)grid * 4));
+            }
+            a.sk_ws = ws;
+            a.sk_flags = flags;
+            a.sk_epoch = ++epoch;
+            // fewer workgroups than tiles (3/4), so even small test shapes split tiles
+            const int ntiles = ((M + 255) / 256) * (N / 256);
+            a.sk_grid = std::max(1, std::min(grid, ntiles * 3 / 4));
+        }
         switch (epi) {
             case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s); break;
             case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s); break;

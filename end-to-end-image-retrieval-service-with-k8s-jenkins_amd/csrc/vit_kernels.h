@@ -49,10 +49,10 @@ struct GemmArgs {
     int group_m = 0;                 // ping-pong tile order: 0 = row-major, G = groups of G row tiles
     int ldc = 0;                     // bf16 outputs: row stride in elements (0 = N)
     // LayerNorm folded across a GEMM pair (see "LayerNorm fold" below):
-    //   producer (f32 epilogues): ln_x != null → also write bf16(x) rows and per-(row, 256-column
-    //     tile) partial statistics (mean, M2) into ln_stats[row][N / 256][2]
+    //   producer (f32 epilogues): ln_x != null → also write bf16(x) rows and per-(row, 64-column
+    //     block) partial statistics (mean, M2) into ln_stats[row][LN_PARTS][2]
     //   consumer (bf16 epilogues): ln_c != null → A is bf16(x), W = W∘γ, bias = b + W·β, and the
-    //     epilogue applies rstd·(acc − μ·c) + bias with μ, rstd from ln_stats[row][3][2]
+    //     epilogue applies rstd·(acc − μ·c) + bias with μ, rstd from ln_stats[row][LN_PARTS][2]
     uint16_t *ln_x = nullptr;
     float *ln_stats = nullptr;
     //   EPI_RESID_HL / EPI_PATCH_HL: the residual stream is the bf16 pair (ln_x, res_lo) instead
@@ -68,21 +68,40 @@ struct GemmArgs {
     const uint8_t *img = nullptr;  // [images][S][S][3]
     float pre_a[3] = {}, pre_b[3] = {};
     int img_size = 0;              // S
+    // stream-K schedule (gemm_sk_kernel): partial-sum slots [grid][256·256] f32, one flag per
+    // slot, the launch's epoch (differs from every earlier launch on these flags), grid size
+    float *sk_ws = nullptr;
+    int *sk_flags = nullptr;
+    int sk_epoch = 0;
+    int sk_grid = 0;
+    int sk_band = 0;  // 0: bands of a row's column tiles when N <= 1024, 1: plain stream-K
 };
 
 // ------------------------------------------------------------ LayerNorm fold
 // modeling_vit_msn.py:258-259 LayerNorm(768, eps) then nn.Linear:
 //   LN(x)·Wᵀ + b = rstd·(x·W′ᵀ − μ·c) + b′,  W′ = W·diag(γ),  c_n = Σ_k W′[n][k],  b′ = b + W·β.
 // The residual stream's producer epilogue (patch GEMM, O-proj, fc2, cls_init)
-// writes bf16(x) next to the f32 x plus, per 256-column tile of each row, the
-// tile mean and M2 = Σ (x − tile mean)²; the consumer GEMM (QKV, fc1) combines
-// the three tiles by Chan's formula (exact in exact arithmetic, no E[x²] − μ²
+// writes bf16(x) next to the f32 x plus, per 64-column block of each row, the
+// block mean and M2 = Σ (x − block mean)²; the consumer GEMM (QKV, fc1) combines
+// the twelve blocks by Chan's formula (exact in exact arithmetic, no E[x²] − μ²
 // cancellation) and applies the correction in its epilogue.  What this removes:
 // the standalone LayerNorm pass (f32 read + bf16 write of the whole stream, 24
 // launches per batch).  Accuracy: bf16(x) carries the same relative error as
 // bf16(LN(x)) while |μ| ≲ σ per token; c is summed from the bf16 W′ the MFMAs
 // use, so the μ·c term cancels exactly what the MFMAs add for the mean.
-constexpr int LN_TILES = 3;  // 768 columns / 256
+//
+// Partials (round 3): per row, LN_PARTS = 12 blocks of 64 columns, each (mean, M2) —
+// the 64 columns one wave of a tiled GEMM holds per row, so the producer epilogues reduce
+// inside the wave (two permlane swaps) and never across waves.  Canonical order, which
+// every producer (tiled epilogues, ln_emit_kernel, cls_init_kernel) reproduces bit for
+// bit: "slice" g = 0..3 of a block holds the 16 columns 32c + 16(g & 1) + 8(g >> 1) + k
+// (c = 0, 1; k = 0..7 — after one v_permlane16_swap, the 8 consecutive columns a lane of
+// the accumulator layout holds per 32-column chunk); ln_slice_stats gives its (mean, M2),
+// then ln_combine(g0, g1), ln_combine(g2, g3) and ln_combine(g01, g23) (Chan, equal
+// counts).  The consumer combines the 12 block partials in ln_row_scale.
+constexpr int LN_PARTS = 12;            // 768 columns / 64
+constexpr int LN_STRIDE = 2 * LN_PARTS;  // floats of partials per row
+__device__ __forceinline__ int ln_slice_col(int g, int c) { return 32 * c + 16 * (g & 1) + 8 * (g >> 1); }
 
 // ------------------------------------------- Residual stream as bf16 pairs
 // Under the LayerNorm fold the residual stream x is kept as two bf16 arrays, hi =
@@ -118,41 +137,105 @@ __device__ __forceinline__ void hl_store(uint4 p, uint16_t *hi, uint16_t *lo) {
     *reinterpret_cast<uint2 *>(lo) = make_uint2(p.z, p.w);
 }
 
-// Chan combination of the LN_TILES partials of one row → (rstd, −rstd·μ)
-__device__ __forceinline__ float2 ln_row_scale(const float *__restrict__ st, float eps) {
-    float m[LN_TILES], M2 = 0.f, mu = 0.f;
+// 8 bf16 (one 16-B load) <-> 8 f32
+__device__ __forceinline__ void bf16x8_unpack(uint4 u, float (&f)[8]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-    for (int t = 0; t < LN_TILES; ++t) {
-        m[t] = st[2 * t];
-        M2 += st[2 * t + 1];
-        mu += m[t];
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = __uint_as_float(w[i] << 16);
+        f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
-    mu *= 1.0f / LN_TILES;
+}
+__device__ __forceinline__ uint4 bf16x8_pack(const float (&f)[8]) {
+    return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+// the pair (hi, lo) of 8 consecutive elements -> x' = f32(hi) + f32(lo) (hl_value's arithmetic)
+__device__ __forceinline__ void hl8_value(uint4 hi, uint4 lo, float (&x)[8]) {
+    float h[8], l[8];
+    bf16x8_unpack(hi, h);
+    bf16x8_unpack(lo, l);
 #pragma unroll
-    for (int t = 0; t < LN_TILES; ++t) M2 = fmaf(256.0f * (m[t] - mu), m[t] - mu, M2);
-    const float rstd = 1.0f / sqrtf(M2 * (1.0f / (256 * LN_TILES)) + eps);
-    return make_float2(rstd, -rstd * mu);
+    for (int k = 0; k < 8; ++k) x[k] = h[k] + l[k];
+}
+// hl_split of 8 elements; xv receives the value the pair stands for (hl_value of the result)
+__device__ __forceinline__ void hl8_split(const float (&x)[8], uint4 &hi, uint4 &lo, float (&xv)[8]) {
+    hi = bf16x8_pack(x);
+    float hf[8], d[8];
+    bf16x8_unpack(hi, hf);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = x[k] - hf[k];
+    lo = bf16x8_pack(d);
+    float lf[8];
+    bf16x8_unpack(lo, lf);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xv[k] = hf[k] + lf[k];
 }
 
-// Producer side, one wave holding one row's 256-column segment as float4 v per
-// lane: the tile's (mean, M2) (wave-collective) and the stores of bf16(v) and
-// the statistics.  The tiled epilogues compute the statistics of all their rows
-// first, branch-free, so the wave reductions of different rows interleave.
-__device__ __forceinline__ float2 ln_row_stats(const float4 v) {
-    const float s = wave_sum((v.x + v.y) + (v.z + v.w));
-    const float mt = s * (1.0f / 256);
-    const float d0 = v.x - mt, d1 = v.y - mt, d2 = v.z - mt, d3 = v.w - mt;
-    return make_float2(mt, wave_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3)));
+// (mean, M2) of one canonical 16-column slice (x[8c + k] = column 32c + slice offset + k).
+// Written with explicit fmaf and no multiply-add left to the compiler's contraction, so
+// every kernel that inlines it rounds identically.
+__device__ __forceinline__ float ln_sum8(const float *x) {
+    return ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
 }
-__device__ __forceinline__ void ln_row_store(const float4 v, float2 st, uint16_t *__restrict__ xrow,
-                                             float *__restrict__ strow, int lane) {
-    reinterpret_cast<uint2 *>(xrow)[lane] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
-    if (lane == 0) *reinterpret_cast<float2 *>(strow) = st;
+__device__ __forceinline__ float ln_sq8(const float *x, float m) {
+    float d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = x[k] - m;
+    const float t0 = fmaf(d[0], d[0], d[1] * d[1]), t1 = fmaf(d[2], d[2], d[3] * d[3]);
+    const float t2 = fmaf(d[4], d[4], d[5] * d[5]), t3 = fmaf(d[6], d[6], d[7] * d[7]);
+    return (t0 + t1) + (t2 + t3);
 }
-__device__ __forceinline__ void ln_emit_row(const float4 v, uint16_t *__restrict__ xrow, float *__restrict__ strow,
-                                            int lane, bool store) {
-    const float2 st = ln_row_stats(v);
-    if (store) ln_row_store(v, st, xrow, strow, lane);
+__device__ __forceinline__ float2 ln_slice_stats(const float (&x)[16]) {
+    const float m = (ln_sum8(x) + ln_sum8(x + 8)) * 0.0625f;
+    return make_float2(m, ln_sq8(x, m) + ln_sq8(x + 8, m));
+}
+// Chan's combination of two equal-count partials (n columns each): a is the lower slice
+// (or pair of slices), b the upper; w = n / 2 (= n·n / 2n)
+__device__ __forceinline__ float2 ln_combine(float2 a, float2 b, float w) {
+    const float d = a.x - b.x;
+    return make_float2((a.x + b.x) * 0.5f, fmaf(d * d, w, a.y + b.y));
+}
+// The block partial from the four slices held by lanes l, l ^ 16, l ^ 32, l ^ 48 (slice
+// g = lane >> 4: the accumulator layout of the tiled GEMMs).  Every lane gets the result.
+__device__ __forceinline__ float2 ln_block_reduce_rows(float2 s) {
+    // rows (16-lane groups) 0 <-> 1 and 2 <-> 3: [0] = the even row's value, [1] = the odd row's
+    const auto px = __builtin_amdgcn_permlane16_swap(__float_as_uint(s.x), __float_as_uint(s.x), false, false);
+    const auto py = __builtin_amdgcn_permlane16_swap(__float_as_uint(s.y), __float_as_uint(s.y), false, false);
+    s = ln_combine(make_float2(__uint_as_float(px[0]), __uint_as_float(py[0])),
+                   make_float2(__uint_as_float(px[1]), __uint_as_float(py[1])), 8.0f);
+    // rows {0, 1} <-> {2, 3}: [0] = the lower half's value, [1] = the upper half's
+    const auto qx = __builtin_amdgcn_permlane32_swap(__float_as_uint(s.x), __float_as_uint(s.x), false, false);
+    const auto qy = __builtin_amdgcn_permlane32_swap(__float_as_uint(s.y), __float_as_uint(s.y), false, false);
+    return ln_combine(make_float2(__uint_as_float(qx[0]), __uint_as_float(qy[0])),
+                      make_float2(__uint_as_float(qx[1]), __uint_as_float(qy[1])), 16.0f);
+}
+// The same reduction with slice g = lane & 3 (the emitter kernels: 4 lanes per block)
+__device__ __forceinline__ float2 ln_block_reduce_quad(float2 s, int g) {
+    float2 o = make_float2(__shfl_xor(s.x, 1), __shfl_xor(s.y, 1));
+    s = (g & 1) ? ln_combine(o, s, 8.0f) : ln_combine(s, o, 8.0f);
+    o = make_float2(__shfl_xor(s.x, 2), __shfl_xor(s.y, 2));
+    return (g & 2) ? ln_combine(o, s, 16.0f) : ln_combine(s, o, 16.0f);
+}
+
+// Chan combination of the LN_PARTS block partials of one row → (rstd, −rstd·μ)
+__device__ __forceinline__ float2 ln_row_scale(const float *__restrict__ st, float eps) {
+    float m[LN_PARTS], q[LN_PARTS];
+#pragma unroll
+    for (int t = 0; t < LN_PARTS / 2; ++t) {
+        const float4 v = reinterpret_cast<const float4 *>(st)[t];
+        m[2 * t] = v.x;
+        q[2 * t] = v.y;
+        m[2 * t + 1] = v.z;
+        q[2 * t + 1] = v.w;
+    }
+    static_assert(LN_PARTS == 12, "the combination tree below is written for 12 partials");
+    const float sm = (((m[0] + m[1]) + (m[2] + m[3])) + ((m[4] + m[5]) + (m[6] + m[7]))) + ((m[8] + m[9]) + (m[10] + m[11]));
+    float M2 = (((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]))) + ((q[8] + q[9]) + (q[10] + q[11]));
+    const float mu = sm * (1.0f / LN_PARTS);
+#pragma unroll
+    for (int t = 0; t < LN_PARTS; ++t) M2 = fmaf(64.0f * (m[t] - mu), m[t] - mu, M2);
+    const float rstd = 1.0f / sqrtf(fmaf(M2, 1.0f / (64 * LN_PARTS), eps));
+    return make_float2(rstd, -rstd * mu);
 }
 
 // One wave per row of H = 256*NV f32 values → bf16 LayerNorm output.
@@ -246,33 +329,46 @@ __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__
 }
 
 // hidden[img*tokens + 0] = cls + pos[0]; with ln_x: also its bf16 copy and LN partials
-// (the LayerNorm fold's producer for the CLS rows; H = 768, one wave per 256 columns);
-// with lo: the row as the bf16 pair (ln_x, lo) and no f32 row
+// (the LayerNorm fold's producer for the CLS rows; H = 768: 48 lanes, one canonical
+// slice each, see LN_PARTS); with lo: the row as the bf16 pair (ln_x, lo) and no f32 row
 __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidden, int tokens, int H,
                                                       const float *__restrict__ cls, const float *__restrict__ pos,
                                                       uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats,
                                                       uint16_t *__restrict__ lo) {
     const int img = blockIdx.x;
     const int64_t row = (int64_t)img * tokens;
-    if (lo != nullptr) {
-        if (threadIdx.x < 64 * LN_TILES) {
-            const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            const int c = t * 256 + lane * 4;
-            const uint4 p = hl_split(make_float4(cls[c] + pos[c], cls[c + 1] + pos[c + 1], cls[c + 2] + pos[c + 2],
-                                                 cls[c + 3] + pos[c + 3]));
-            hl_store(p, ln_x + row * H + c, lo + row * H + c);
-            const float2 st = ln_row_stats(hl_value(p));
-            if (lane == 0) *reinterpret_cast<float2 *>(ln_stats + (row * LN_TILES + t) * 2) = st;
+    if (lo == nullptr) {
+        for (int c = threadIdx.x; c < H; c += 256) hidden[row * H + c] = cls[c] + pos[c];
+        if (ln_x == nullptr) return;
+    }
+    if (threadIdx.x >= 64) return;  // one wave: lanes 0-47 = (block, slice), 48-63 only join the shuffles
+    const int t = threadIdx.x, g = t & 3, ok = t < 4 * LN_PARTS;
+    const int blk = ok ? t >> 2 : 0;
+    float xs[16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int col = blk * 64 + ln_slice_col(g, c);
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = cls[col + k] + pos[col + k];
+        if (lo != nullptr) {
+            uint4 h, l;
+            float xv[8];
+            hl8_split(x, h, l, xv);
+            if (ok) {
+                *reinterpret_cast<uint4 *>(ln_x + row * H + col) = h;
+                *reinterpret_cast<uint4 *>(lo + row * H + col) = l;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
+        } else {
+            if (ok) *reinterpret_cast<uint4 *>(ln_x + row * H + col) = bf16x8_pack(x);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) xs[8 * c + k] = x[k];
         }
-        return;
     }
-    for (int c = threadIdx.x; c < H; c += 256) hidden[row * H + c] = cls[c] + pos[c];
-    if (ln_x != nullptr && threadIdx.x < 64 * LN_TILES) {
-        const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const int c = t * 256 + lane * 4;
-        const float4 v = make_float4(cls[c] + pos[c], cls[c + 1] + pos[c + 1], cls[c + 2] + pos[c + 2], cls[c + 3] + pos[c + 3]);
-        ln_emit_row(v, ln_x + row * H + t * 256, ln_stats + (row * LN_TILES + t) * 2, lane, true);
-    }
+    const float2 st = ln_block_reduce_quad(ln_slice_stats(xs), g);
+    if (ok && g == 0) *reinterpret_cast<float2 *>(ln_stats + row * LN_STRIDE + 2 * blk) = st;
 }
 
 // Self-attention v2 for one (image, head), tokens <= 208, head dim 64.
@@ -447,8 +543,8 @@ __global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict
     const int64_t r0 = (int64_t)img * tokens * H;
     if (hc_ln != nullptr) {
         reinterpret_cast<uint2 *>(hc_ln + (int64_t)img * H)[threadIdx.x] = reinterpret_cast<const uint2 *>(hi + r0)[threadIdx.x];
-        if (threadIdx.x < 2 * LN_TILES)
-            hc_st[img * 2 * LN_TILES + threadIdx.x] = st[(int64_t)img * tokens * 2 * LN_TILES + threadIdx.x];
+        if (threadIdx.x < LN_STRIDE)
+            hc_st[img * LN_STRIDE + threadIdx.x] = st[(int64_t)img * tokens * LN_STRIDE + threadIdx.x];
     }
     reinterpret_cast<float4 *>(hc + (int64_t)img * H)[threadIdx.x] =
         hi ? hl_value(hl_load(hi + r0 + 4 * threadIdx.x, lo + r0 + 4 * threadIdx.x))
