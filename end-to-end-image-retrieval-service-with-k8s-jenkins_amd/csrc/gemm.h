@@ -573,165 +573,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     RC_STAMP(sb + 3, RC_NOW());
 }
 
-// ----------------------------------------------------------- stream-K GEMM --
-// The ping-pong tile and K loop as a persistent kernel over an even split of the
-// tiles x K-steps "units" (stream-K): virtual workgroup v (XCD-contiguous, xcd_remap)
-// owns units [U·v/G, U·(v+1)/G), U = tiles · nk, at least nk of them (G <= tiles).  Two
-// things the one-tile-per-workgroup grid cannot do: (1) no partial last round (the N =
-// 768 GEMMs have 2.31 rounds of 256 tiles: the third runs 31 % full), and (2) the
-// epilogues — HBM-bound bursts of residual reads and stores (O-proj, fc2) or store bursts
-// (QKV, fc1) — fall at different times on different CUs instead of all at once, so they
-// overlap other CUs' MFMA main loops.
-// A tile split between workgroups v (ends its range inside it) and v + 1 (starts inside
-// it) stays bit-identical to the unsplit tile: v + 1 runs the chain-FIRST K-steps
-// [0, nk - c) at its start and stores the f32 accumulators (ws slot v + 1, lane-linear
-// 256 KB) with an agent-scope release + flag = epoch; v, at the end of its range, polls the
-// flag, acquires, loads the partial into its accumulators and continues the MFMA chain over
-// [nk - c, nk) — the same chain, in the same K order, as gemm_pp_kernel and the skinny
-// kernel.  The flag was set ~(units per workgroup − nk) K-steps earlier, so the poll
-// normally succeeds at once; if it does not within SK_WAIT_TICKS (v + 1 not resident), v
-// recomputes the whole tile itself (same bits), so no launch can deadlock on residency.
-// a.sk_epoch must differ from every earlier launch on the same flags (the host counts).
-// Hand-off (MI355X_MICROARCH.md, "Valid forms", first table row): the partial is stored
-// write-through (sc1) by every wave, each wave waits vmcnt(0), a workgroup barrier, then
-// one lane's sc1 flag store; the consumer's lane 0 polls with sc1 loads, the workgroup
-// barrier follows, and every load of the partial is an sc1 load — no L2 write-back or
-// invalidate (an agent release here wrote back the XCD's whole dirty L2 per hand-off).
-constexpr int SK_SC1 = 16;         // buffer-instruction cache policy bit sc1 (gfx940+ CPol::SC1)
-constexpr int SK_EPI_ROWS = 2;       // f32 epilogue rows per pass (4 spills beside the persistent loop's state)
-constexpr int SK_WAIT_TICKS = 4000;  // s_memrealtime ticks (100 MHz): 40 us
-
-// Bands (a.sk_band = B > 1, B = the column tiles of a row, N = 256·B): the split unit is a
-// row tile's K-steps, and B workgroups of one XCD (consecutive virtual ids) walk the same
-// row tiles in lockstep, one column tile each, so the A K-slab each reads is the one its
-// band partners read at the same time (one L2 fill serves B workgroups — the sharing the
-// one-tile grid gets from its row-major order and plain stream-K loses).  Bands, not
-// workgroups, then take even shares of the units; the grid is 8 XCDs x (bands per XCD) x B.
-template <int EPI, int NKT = 0>
-__global__ __launch_bounds__(512, 1) void gemm_sk_kernel(GemmArgs a) {
-    constexpr int LN_LDS = epi_ln(EPI) ? PP_BM * 8 : 0;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + LN_LDS + 16];
-    const int tid = threadIdx.x;
-    const int nk = NKT > 0 ? NKT : a.K / PP_BK;
-    const int ntm = (a.M + PP_BM - 1) / PP_BM, ntn = a.N / PP_BM;
-    const int G = gridDim.x, v = xcd_remap(blockIdx.x, G);
-    const int B = a.sk_band > 1 ? a.sk_band : 1;
-    // band member (column tile in band mode) and band index; band b's workgroups are the
-    // B consecutive virtual ids b·B .. b·B + B - 1 (one XCD when G / 8 is a multiple of B)
-    const int member = v % B, band = v / B, NB = G / B;
-    const int64_t U = (int64_t)(B > 1 ? ntm : ntm * ntn) * nk;
-    const int64_t u1 = U * (band + 1) / NB;
-    int *okflag = reinterpret_cast<int *>(smem + 2 * PP_STAGE + LN_LDS);
-    // partial-sum slots as buffer resources: lane-linear f32x4 i of lane tid at byte
-    // i * 8192 + tid * 16 (SGPR offsets, no per-access VGPR address); slot = virtual id,
-    // the producer of a tail's partial is the same member of the next band (id v + B)
-    const __amdgpu_buffer_rsrc_t ws_mine = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(a.sk_ws + (int64_t)v * (PP_BM * PP_BM)), (short)0, PP_BM * PP_BM * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ws_next = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(a.sk_ws + (int64_t)(v + B) * (PP_BM * PP_BM)), (short)0, PP_BM * PP_BM * 4, 0x00020000);
-    if (band >= NB) return;  // (G a multiple of B: never)
-    bool first = true;
-    int seg = 0;
-    RC_STAMP((int64_t)blockIdx.x * 64 + 63, (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
-                                               ((uint64_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32));
-    for (int64_t u = U * band / NB; u < u1;) {
-        // a per-segment copy of the thread index: keeps hipcc from hoisting every per-lane
-        // address of the K loop and the epilogue out of the segment loop (they spilled)
-        int ltid = tid;
-        asm volatile("" : "+v"(ltid));
-        const int T = (int)(u / nk), j = (int)(u - (int64_t)T * nk);
-        const int64_t tile_end = (int64_t)(T + 1) * nk, seg_end = tile_end < u1 ? tile_end : u1;
-        // kind 0: whole tile; 1: head of this range inside T (chain-first K-steps, partial
-        // out); 2: tail of this range inside T (partial of v + 1 in, then the last K-steps)
-        const int kind = j > 0 ? 1 : (seg_end < tile_end ? 2 : 0);
-        int kb = 0, ke = nk;
-        if (kind == 1) ke = nk - j;
-        if (kind == 2) kb = nk - (int)(seg_end - (int64_t)T * nk);
-        int tm, tn;
-        if (B > 1) {
-            tm = T;
-            tn = member;
-        } else {
-            pp_tile_coords(a, T, tm, tn);
-        }
-        const int m0 = tm * PP_BM, n0 = tn * PP_BM;
-        if (!first) __builtin_amdgcn_s_barrier();  // the last epilogue's LDS reads are done
-        first = false;
-        const int64_t sb = seg < 7 ? (int64_t)blockIdx.x * 64 + seg * 8 : -1;
-        ++seg;
-        if (sb >= 0) {
-            RC_STAMP(sb, RC_NOW());
-            RC_STAMP(sb + 4, (uint64_t)T | ((uint64_t)kind << 32));
-            RC_STAMP(sb + 5, (uint64_t)kb | ((uint64_t)ke << 32));
-        }
-
-        f32x4 acc[2][2][4][2];
-#pragma unroll
-        for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-            for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-                for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                    for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (kind == 2) {
-            if (tid == 0) {
-                const int *flag = a.sk_flags + v + B;
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                int ok = 1;
-                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.sk_epoch) {
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)SK_WAIT_TICKS) {
-                        ok = 0;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                *okflag = ok;
-            }
-            __syncthreads();
-            if (*okflag) {
-#pragma unroll
-                for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-                    for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-                        for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                            for (int a3 = 0; a3 < 2; ++a3)
-                                acc[a0][a1][a2][a3] = __builtin_bit_cast(
-                                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               ws_next, ltid * 16, ((((a0 * 2 + a1) * 4 + a2) * 2 + a3) * 8192), SK_SC1));
-            } else {
-                kb = 0;  // v + 1 never published: run the whole chain here
-            }
-        }
-        float4 biasr[2][2];
-        pp_bias_regs<EPI>(a, n0, biasr, ltid);
-        pp_kloop<EPI, 0>(a, smem, m0, n0, kb, ke, acc, ltid, sb >= 0 ? sb + 1 : -1);
-        if (kind == 1) {
-            typedef int i32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-            for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-                for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-                    for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                        for (int a3 = 0; a3 < 2; ++a3)
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[a0][a1][a2][a3]), ws_mine,
-                                                                       ltid * 16,
-                                                                       ((((a0 * 2 + a1) * 4 + a2) * 2 + a3) * 8192), SK_SC1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(a.sk_flags + v, a.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            pp_epilogue<EPI, 0, SK_EPI_ROWS>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, ltid);
-        }
-        if (sb >= 0) RC_STAMP(sb + 3, RC_NOW());
-        u = seg_end;
-    }
-}
-
 // --------------------------------------------------------------- ring GEMM --
 // The ping-pong tile (256x256, 8 waves in two staggered groups, the same wave ->
 // output map and epilogue) with a deeper DMA pipeline.  gemm_pp_kernel keeps one
@@ -1394,9 +1235,7 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 // (Rounds 1-2 also measured a 128x128 4-wave kernel, a 256x256 / 128x256 single-
 // barrier kernel, a persistent kernel, Stream-K and a deferred-store persistent
 // kernel: each lost on every shape and was removed.)
-enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_STREAMK = 7, GEMM_W2 = 8,
-                   GEMM_SKINNY = 9 };
-constexpr int SK_MAX_GRID = 512;  // partial-sum slots / flags a stream-K workspace provides
+enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9 };
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
@@ -1406,10 +1245,12 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool p
     // position read + write): the two-workgroup kernel overlaps that epilogue
     // with the co-resident workgroup's MFMAs (O-proj 96 -> 89 us at batch 256,
     // tools/gemm_calib.py).  Everything else streams K at 128 flop/B: ping-pong.
-    // With the residual stream as bf16 pairs the O-proj epilogue moves 8 B per element
-    // instead of 10 and the ping-pong kernel wins there too (+0.5-1.1 % images/s at
-    // parts = 2, profiles/r02/r02_ab_results.txt).
-    if (a.N <= 768 && a.K <= 768 && !pair_epilogue) return GEMM_W2;
+    // Round 3: with every f32 epilogue storing straight from the accumulators (no LDS staging,
+    // no barrier) the two-workgroup kernel also wins O-proj on the bf16-pair stream: 141 ->
+    // 125 us per launch, -0.6 % step time at parts = 2 (profiles/r03/r03d_part_lag_w2_ab.log;
+    // fc2, K = 3072, stays on the ping-pong kernel: 305 -> 326 us there).
+    (void)pair_epilogue;
+    if (a.N <= 768 && a.K <= 768) return GEMM_W2;
     return GEMM_PINGPONG;
 }
 
@@ -1447,8 +1288,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_STREAMK ||
-                    pick == GEMM_SKINNY) && a.ln_c &&
+        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
                        a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
     }
     switch (pick) {
@@ -1489,31 +1329,6 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 hipLaunchKernelGGL(ln_emit_kernel, dim3((a.M * LN_PARTS + 63) / 64), dim3(256), 0, s, a.out_f32, a.ln_x,
                                    a.res_lo, a.ln_stats, a.M);
             }
-            break;
-        }
-        case GEMM_STREAMK: {
-            RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-            RC_REQUIRE(a.sk_ws && a.sk_flags && a.sk_grid >= 1 && a.sk_grid <= SK_MAX_GRID, RC_ERR_INVALID,
-                       "stream-K GEMM needs a workspace (sk_ws, sk_flags, sk_grid <= SK_MAX_GRID)");
-            a.group_m = gemm_group_m(a);
-            // band mode for short rows (N <= 1024: 2-4 column tiles); every band's or
-            // workgroup's range must span >= one tile of K-steps: grid <= tiles (bands <= row tiles)
-            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
-            int grid;
-            if (ntn >= 2 && ntn <= 4 && a.sk_band != 1) {
-                a.sk_band = ntn;
-                int bands = std::max(1, a.sk_grid / ntn);
-                if (bands >= 8) bands = bands / 8 * 8;  // whole XCD blocks of bands
-                bands = std::min(bands, ntm);
-                grid = bands * ntn;
-            } else {
-                a.sk_band = 1;
-                grid = std::min(a.sk_grid, ntm * ntn);
-            }
-            const dim3 gr(grid), bl(512);
-            if (a.K == 768) hipLaunchKernelGGL((gemm_sk_kernel<EPI, 12>), gr, bl, 0, s, a);
-            else if (a.K == 3072) hipLaunchKernelGGL((gemm_sk_kernel<EPI, 48>), gr, bl, 0, s, a);
-            else hipLaunchKernelGGL((gemm_sk_kernel<EPI>), gr, bl, 0, s, a);
             break;
         }
         case GEMM_PINGPONG: {

@@ -89,12 +89,6 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // diagnostic builds: RC_GEMM_VARIANT (ablation variants)
-    // stream-K projection GEMMs (gemm_sk_kernel): per batch part a partial-sum workspace and
-    // flags, the launch epoch, and the part whose encode is being issued (host-sequential)
-    float *sk_ws[4] = {};
-    int *sk_flags[4] = {};
-    int sk_epoch[4] = {};
-    int sk_grid = 0, cur_part = 0, active_parts = 1;
     int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -348,43 +342,12 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
 }
 
 // role: T_QKV / T_OPROJ / T_FC1 / T_FC2 (its own timer besides T_GEMM), or -1
-// stream-K workspace of one batch part: partial-sum slots and flags for sk_grid workgroups
-void ensure_streamk(rc_model *m) {
-    if (m->sk_grid > 0) return;
-    int cus = 0;
-    RC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->device));
-    m->sk_grid = std::max(8, std::min(cus, SK_MAX_GRID));
-    for (int p = 0; p < kMaxParts; ++p) {
-        m->sk_ws[p] = (float *)m->alloc((size_t)m->sk_grid * 256 * 256 * 4);
-        m->sk_flags[p] = (int *)m->alloc((size_t)m->sk_grid * 4);
-        RC_HIP(hipMemset(m->sk_flags[p], 0, (size_t)m->sk_grid * 4));
-    }
-}
-
 template <int EPI>
-void gemm(rc_model *m, const GemmArgs &a_in, hipStream_t s, int role = -1) {
-    GemmArgs a = a_in;
-    int variant = m->gemm_variant;
-    // stream-K: 7 = the short-row projections (O-proj, fc2: N = 768) as bands, the wide ones
-    // (QKV, fc1) on the ping-pong kernel; 17 = every projection (A/B)
-    if (variant == GEMM_STREAMK + 10) variant = GEMM_STREAMK;
-    else if (variant == GEMM_STREAMK && a.N > 1024) variant = GEMM_PINGPONG;
-    if (variant == GEMM_STREAMK) {
-        if (a.M > 256 && a.N % 256 == 0 && m->sk_grid > 0) {
-            const int p = m->cur_part;
-            a.sk_ws = m->sk_ws[p];
-            a.sk_flags = m->sk_flags[p];
-            a.sk_epoch = ++m->sk_epoch[p];
-            // concurrent parts share the CUs: each part's grid takes its share
-            a.sk_grid = std::max(8, m->sk_grid / std::max(1, m->active_parts));
-        } else {
-            variant = GEMM_AUTO;
-        }
-    }
+void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = role >= 0 ? m->timers[role].begin(s) : -1;
-    launch_gemm<EPI>(a, variant, s);
+    launch_gemm<EPI>(a, m->gemm_variant, s);
     if (role >= 0) m->timers[role].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
@@ -577,9 +540,7 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
     // bursts overlap another part's MFMA main loops
     int parts = std::max(1, std::min(m->split, kMaxParts));
     while (parts > 1 && n < parts * m->split_min) --parts;
-    m->active_parts = parts;
     if (parts == 1) {
-        m->cur_part = 0;
         encode(m, src, 0, n, raw, normed, s);
         return;
     }
@@ -587,7 +548,6 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
     for (int p = 1; p < parts; ++p) RC_HIP(hipStreamWaitEvent(m->sp[p], m->ev_fork, 0));
     for (int p = 0; p < parts; ++p) {
         const int i0 = (int)((int64_t)n * p / parts), i1 = (int)((int64_t)n * (p + 1) / parts);
-        m->cur_part = p;
         encode(m, src, i0, i1 - i0, raw, normed, p == 0 ? s : m->sp[p]);
     }
     for (int p = 1; p < parts; ++p) {
@@ -852,12 +812,9 @@ int rc_model_set_parts(rc_model *m, int parts) {
 int rc_model_set_gemm_variant(rc_model *m, int variant) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
-        RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING4 || variant == GEMM_RING3 ||
-                       variant == GEMM_STREAMK || variant == GEMM_STREAMK + 10,
-                   RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 or 6 (ring), 7 (stream-K)");
+        RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING4 || variant == GEMM_RING3,
+                   RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 or 6 (ring)");
         std::lock_guard<std::mutex> lk(m->mu);
-        DeviceScope ds(m->device);
-        if (variant == GEMM_STREAMK || variant == GEMM_STREAMK + 10) ensure_streamk(m);
         m->gemm_variant = variant;
     });
 }
@@ -903,27 +860,6 @@ extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint1
         RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
         GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
         hipStream_t s = (hipStream_t)stream;
-        if (variant == GEMM_STREAMK) {  // the test hook's own stream-K workspace (one per process, current device)
-            static std::mutex mu;
-            static float *ws = nullptr;
-            static int *flags = nullptr, epoch = 0, grid = 0;
-            std::lock_guard<std::mutex> lk(mu);
-            if (!ws) {
-                int dev = 0, cus = 0;
-                RC_HIP(hipGetDevice(&dev));
-                RC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-                grid = std::max(8, std::min(cus, SK_MAX_GRID));
-                ws = (float *)dmalloc((size_t)grid * 256 * 256 * 4);
-                flags = (int *)dmalloc((size_t)grid * 4);
-                RC_HIP(hipMemset(flags, 0, (size_t)grid * 4));
-            }
-            a.sk_ws = ws;
-            a.sk_flags = flags;
-            a.sk_epoch = ++epoch;
-            // fewer workgroups than tiles (3/4), so even small test shapes split tiles
-            const int ntiles = ((M + 255) / 256) * (N / 256);
-            a.sk_grid = std::max(1, std::min(grid, ntiles * 3 / 4));
-        }
         switch (epi) {
             case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s); break;
             case EPI_GELU_BF16: launch_gemm<EPI_GELU_BF16>(a, variant, s); break;

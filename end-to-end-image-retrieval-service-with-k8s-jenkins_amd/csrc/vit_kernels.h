@@ -68,13 +68,6 @@ struct GemmArgs {
     const uint8_t *img = nullptr;  // [images][S][S][3]
     float pre_a[3] = {}, pre_b[3] = {};
     int img_size = 0;              // S
-    // stream-K schedule (gemm_sk_kernel): partial-sum slots [grid][256·256] f32, one flag per
-    // slot, the launch's epoch (differs from every earlier launch on these flags), grid size
-    float *sk_ws = nullptr;
-    int *sk_flags = nullptr;
-    int sk_epoch = 0;
-    int sk_grid = 0;
-    int sk_band = 0;  // 0: bands of a row's column tiles when N <= 1024, 1: plain stream-K
 };
 
 // ------------------------------------------------------------ LayerNorm fold

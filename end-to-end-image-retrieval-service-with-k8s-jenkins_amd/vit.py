@@ -361,7 +361,7 @@ class VitMsnEmbedder:
         check(self.lib.rc_model_set_last_layer(self._h, int(bool(cls_only))))
 
     def set_gemm_variant(self, variant: int) -> None:
-        """Full-batch projection GEMM kernel: 0 auto, 4 ping-pong, 5 / 6 ring, 7 stream-K (A/B; same bits)."""
+        """Full-batch projection GEMM kernel: 0 auto, 4 ping-pong, 5 / 6 ring (A/B; same bits)."""
         check(self.lib.rc_model_set_gemm_variant(self._h, int(variant)))
 
     def timing_reset(self) -> None:

@@ -24,7 +24,7 @@ def run(epi, variant, A, W, bias, M, out, pos=None, tokens=0):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [4, 5, 6, 8])
 @pytest.mark.parametrize("M,N,K", [(300, 768, 768), (1000, 2304, 768), (513, 3072, 768), (257, 768, 3072), (64, 256, 64)])
 @pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
 def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
@@ -80,27 +80,3 @@ def test_patch_epilogue_scatter(cuda, variant):
     assert torch.allclose(got[:, 1:], ref, atol=1e-4, rtol=1e-4)
     assert bool((got[:, 0] == -3.0).all())  # CLS rows are not the GEMM's
 
-
-@pytest.mark.parametrize("M,N,K", [(300, 768, 768), (1000, 2304, 768), (2000, 768, 3072), (513, 3072, 768)])
-@pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
-def test_streamk_gemm_bit_identical_to_pingpong(cuda, M, N, K, epi):
-    """Stream-K (variant 7: tiles split between workgroups, the later one continuing the MFMA chain from
-    the earlier one's partial sums) gives the ping-pong kernel's bits exactly."""
-    import torch
-
-    g = torch.Generator(device=cuda).manual_seed(3 * M + N + K)
-    Mp = (M + 255) // 256 * 256
-    A = (torch.randn(Mp, K, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
-    W = (torch.randn(N, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
-    bias = torch.randn(N, device=cuda, generator=g) * 0.1
-    if epi == EPI_RESID:
-        resid = torch.randn(Mp, N, device=cuda, generator=g)
-        outs = [resid.clone(), resid.clone()]
-    else:
-        outs = [torch.zeros((Mp, N), device=cuda).to(torch.bfloat16) for _ in range(2)]
-    for rep in range(2):  # a second launch on the same workspace (the flags' epoch moves on)
-        if epi == EPI_RESID:
-            outs = [resid.clone(), resid.clone()]
-        run(epi, 4, A, W, bias, M, outs[0])
-        run(epi, 7, A, W, bias, M, outs[1])
-        assert torch.equal(outs[0][:M], outs[1][:M])

@@ -23,7 +23,7 @@ raw.rc_diag_set_stamps.argtypes = [C.c_void_p]
 dev = torch.device("cuda", 0)
 M = 256 * 197
 shapes = {"oproj": (768, 768, 2), "fc2": (768, 3072, 2), "qkv": (2304, 768, 0), "fc1": (3072, 768, 1)}
-variants = [int(v) for v in os.environ.get("VARIANTS", "4,7").split(",")]
+variants = [int(v) for v in os.environ.get("VARIANTS", "4").split(",")]
 sel = os.environ.get("SHAPES", "oproj,fc2").split(",")
 stamps = torch.zeros(4096 * 64, dtype=torch.int64, device=dev)
 TICK_US = 0.01
