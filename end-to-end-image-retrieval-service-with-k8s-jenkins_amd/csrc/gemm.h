@@ -91,7 +91,8 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
     const bool stats = HL ? a.ln_stats != nullptr : a.ln_x != nullptr;
     const int cl = ln_slice_col(g, 0);
     // every source load of the NR rows first (16 B each), then the arithmetic and stores
-    uint4 sh[NR][2], sl[NR][2];
+    uint4 sh[NR][2];
+    uint2 sl[NR][2];
     float4 sf[NR][2][2];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -103,7 +104,7 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
                 const int64_t off = (int64_t)rr * a.N + col;
                 if constexpr (HL) {
                     sh[r][c] = *reinterpret_cast<const uint4 *>(a.ln_x + off);
-                    sl[r][c] = *reinterpret_cast<const uint4 *>(a.res_lo + off);
+                    sl[r][c] = *reinterpret_cast<const uint2 *>(a.res_lo + off);
                 } else {
                     sf[r][c][0] = *reinterpret_cast<const float4 *>(a.out_f32 + off);
                     sf[r][c][1] = *reinterpret_cast<const float4 *>(a.out_f32 + off + 4);
@@ -152,12 +153,13 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
             for (int k = 0; k < 8; ++k) x[k] = (v[k] + b[k]) + add[k];
             const int64_t off = orow * a.N + colw + 32 * c + cl;
             if constexpr (HL) {
-                uint4 h, l;
+                uint4 h;
+                uint2 l;
                 float xv[8];
                 hl8_split(x, h, l, xv);
                 if (ok) {
                     *reinterpret_cast<uint4 *>(a.ln_x + off) = h;
-                    *reinterpret_cast<uint4 *>(a.res_lo + off) = l;
+                    *reinterpret_cast<uint2 *>(a.res_lo + off) = l;
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
@@ -1203,7 +1205,7 @@ inline void launch_skinny_splitk_resid(const GemmArgs &a, float *part, hipStream
 // lo != null: the rows are the bf16 pairs (ln_x, lo), only the partials are written;
 // otherwise x is the f32 stream and ln_x receives its bf16 copy.
 __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ x, uint16_t *__restrict__ ln_x,
-                                                     const uint16_t *__restrict__ lo, float *__restrict__ ln_stats, int M) {
+                                                     const uint8_t *__restrict__ lo, float *__restrict__ ln_stats, int M) {
     constexpr int H = 64 * LN_PARTS;
     const int t = blockIdx.x * 256 + threadIdx.x;
     const int item = t >> 2, g = t & 3;
@@ -1216,7 +1218,7 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
         const int64_t off = (int64_t)row * H + blk * 64 + ln_slice_col(g, c);
         float v[8];
         if (lo != nullptr) {
-            hl8_value(*reinterpret_cast<const uint4 *>(ln_x + off), *reinterpret_cast<const uint4 *>(lo + off), v);
+            hl8_value(*reinterpret_cast<const uint4 *>(ln_x + off), *reinterpret_cast<const uint2 *>(lo + off), v);
         } else {
             const float4 a = *reinterpret_cast<const float4 *>(x + off), b = *reinterpret_cast<const float4 *>(x + off + 4);
             v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;

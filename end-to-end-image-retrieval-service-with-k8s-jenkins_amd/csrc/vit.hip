@@ -9,7 +9,7 @@
 //             biases / LayerNorm params / cls / pos — f32
 //   workspace (sized for max_batch images, rows padded to the GEMM tile):
 //             residual stream: under the LayerNorm fold the bf16 pair ln = RNE(x),
-//             res_lo = RNE(x − ln) [Mp][H] with ln_stats f32 [Mp][LN_PARTS][2]; without it
+//             res_lo = the low byte of x around ln [Mp][H] u8 with ln_stats f32 [Mp][LN_PARTS][2]; without it
 //             hidden f32 [Mp][H] and ln bf16 [Mp][H] = LayerNorm output; qkv bf16
 //             [Mp][3H], attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
 #include <algorithm>
@@ -77,7 +77,7 @@ struct rc_model {
     int Mp = 0;
     uint16_t *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
-    uint16_t *res_lo = nullptr;  // LayerNorm fold: low halves of the residual stream's bf16 pairs
+    uint8_t *res_lo = nullptr;   // LayerNorm fold: the residual stream's low bytes (vit_kernels.h)
     float *ln_stats = nullptr;     // [Mp][LN_PARTS][2] LayerNorm-fold partials (per 64-column block: mean, M2)
     bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
@@ -372,7 +372,7 @@ void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint
 // full-batch ones (a GEMM row's result does not depend on M), so a CLS row gets
 // the same arithmetic as in the full layer except attention's summation order.
 void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *qkv, const float *hidden,
-                    const uint16_t *hi, const uint16_t *lo, const float *st_rows, float scale, hipStream_t s) {
+                    const uint16_t *hi, const uint8_t *lo, const float *st_rows, float scale, hipStream_t s) {
     const auto &c = m->cfg;
     const int H = c.hidden, T = m->tokens;
     float *hc = m->cls_hidden + (int64_t)i0 * H;
@@ -444,7 +444,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
     // M <= 256 included), so an image's embedding does not depend on its batch.
     const bool fold = m->ln_fold;
     float *st = m->ln_stats + r0 * LN_STRIDE;
-    uint16_t *lo = fold ? m->res_lo + r0 * H : nullptr;  // the residual stream is the pair (ln, lo)
+    uint8_t *lo = fold ? m->res_lo + r0 * H : nullptr;  // the residual stream is the pair (ln, lo)
     auto produce = [&](GemmArgs a, bool emit) {
         if (fold) {
             a.ln_x = ln;
@@ -584,7 +584,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->ln_stats = (float *)m->alloc((size_t)m->Mp * LN_STRIDE * 4);
             RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * LN_STRIDE * 4));  // pad rows: finite scales
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
-            m->res_lo = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
+            m->res_lo = (uint8_t *)m->alloc((size_t)m->Mp * H);
             m->qkv = (uint16_t *)m->alloc((size_t)m->Mp * 3 * H * 2);
             m->attn = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->mlp = (uint16_t *)m->alloc((size_t)m->Mp * cfg->mlp * 2);
@@ -604,7 +604,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             // pad rows are read by the GEMM tiles: keep them finite (zero) forever
             RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
             RC_HIP(hipMemset(m->ln, 0, (size_t)m->Mp * H * 2));
-            RC_HIP(hipMemset(m->res_lo, 0, (size_t)m->Mp * H * 2));
+            RC_HIP(hipMemset(m->res_lo, 0, (size_t)m->Mp * H));
             RC_HIP(hipMemset(m->qkv, 0, (size_t)m->Mp * 3 * H * 2));
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));

@@ -55,10 +55,10 @@ struct GemmArgs {
     //     epilogue applies rstd·(acc − μ·c) + bias with μ, rstd from ln_stats[row][LN_PARTS][2]
     uint16_t *ln_x = nullptr;
     float *ln_stats = nullptr;
-    //   EPI_RESID_HL / EPI_PATCH_HL: the residual stream is the bf16 pair (ln_x, res_lo) instead
+    //   EPI_RESID_HL / EPI_PATCH_HL: the residual stream is the pair (ln_x, res_lo) instead
     //     of out_f32 (see "Residual stream as bf16 pairs"): the residual is read from and the
     //     result written to the pair; the statistics only when ln_stats != null
-    uint16_t *res_lo = nullptr;
+    uint8_t *res_lo = nullptr;
     const float *ln_c = nullptr;
     float ln_eps = 1e-6f;
     // implicit-GEMM patch embedding (patch_gemm_kernel): A[m][k] is read from the u8
@@ -97,37 +97,55 @@ constexpr int LN_STRIDE = 2 * LN_PARTS;  // floats of partials per row
 __device__ __forceinline__ int ln_slice_col(int g, int c) { return 32 * c + 16 * (g & 1) + 8 * (g >> 1); }
 
 // ------------------------------------------- Residual stream as bf16 pairs
-// Under the LayerNorm fold the residual stream x is kept as two bf16 arrays, hi =
-// RNE(x) — exactly the bf16(x) the QKV / fc1 GEMMs read as A — and lo = RNE(x − hi),
-// instead of an f32 array plus that bf16 copy: the producers (patch GEMM, O-proj,
-// fc2, cls_init) write 4 B per element instead of 6 and the residual epilogues read
-// the same 4 B.  The value is x′ = f32(hi) + f32(lo), ~17 significant bits (|x − x′|
-// ≤ 2⁻¹⁸|x|, against the 2⁻⁹ of the bf16 GEMM operands); every reader forms x′ with
-// hl_value's arithmetic, and the producers compute the LN statistics from that same
-// x′, so the skinny (ln_emit_kernel) and tiled paths stay bit-identical.
+// Under the LayerNorm fold the residual stream x is kept as hi = RNE_bf16(x) — exactly the
+// bf16(x) the QKV / fc1 GEMMs read as A — plus a one-byte low part: the residual x − hi,
+// which RNE bounds by half an ulp of hi, as q = rint((x − hi) / s) with s = ulp(hi) / 256
+// (|q| <= 127).  The value is x′ = hi + q·s (exact in f32), 16 significant bits (|x − x′|
+// <= ulp(hi) / 512 <= 2⁻¹⁶|x|, against the 2⁻⁹ of the bf16 GEMM operands).  Producers
+// (patch GEMM, O-proj, fc2, cls_init) write 3 B per element and the residual epilogues read
+// 3 B (round 2 kept lo as a second bf16: 4 B each way).  Every reader forms x′ with hl_value's
+// arithmetic, and the producers compute the LN statistics from that same x′, so the skinny
+// (ln_emit_kernel) and tiled paths stay bit-identical.
 __device__ __forceinline__ float4 bf16x4_f32(uint2 u) {
     return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                        __uint_as_float(u.y & 0xffff0000u));
 }
 __device__ __forceinline__ uint2 pack_bf16x4(float4 v) { return make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)); }
-// (hi.x, hi.y, lo.x, lo.y) of four consecutive elements
+// s = ulp(h) / 256 = 2^(E − 142) for h's biased exponent E, and 1 / s (both 0 below E = 16)
+__device__ __forceinline__ float hl_step(float h) {
+    const uint32_t e = __float_as_uint(h) & 0x7f800000u;
+    return e > (15u << 23) ? __uint_as_float(e - (15u << 23)) : 0.f;
+}
+__device__ __forceinline__ float hl_inv_step(float h) {
+    const uint32_t e = __float_as_uint(h) & 0x7f800000u;
+    return e > (15u << 23) ? __uint_as_float((269u << 23) - e) : 0.f;
+}
+// the low byte of x around h = RNE_bf16(x), and the value a (h, byte) pair stands for
+__device__ __forceinline__ uint32_t hl_code(float x, float h) {
+    const int q = (int)rintf((x - h) * hl_inv_step(h));
+    return (uint32_t)(q < -127 ? -127 : (q > 127 ? 127 : q)) & 0xffu;
+}
+__device__ __forceinline__ float hl_decode(float h, uint32_t byte) {
+    return fmaf((float)(int)(int8_t)(uint8_t)byte, hl_step(h), h);
+}
+// four consecutive elements: (hi.x, hi.y, the four lo bytes, unused)
 __device__ __forceinline__ uint4 hl_split(float4 x) {
     const uint2 h = pack_bf16x4(x);
     const float4 hf = bf16x4_f32(h);
-    const uint2 l = pack_bf16x4(make_float4(x.x - hf.x, x.y - hf.y, x.z - hf.z, x.w - hf.w));
-    return make_uint4(h.x, h.y, l.x, l.y);
+    const uint32_t lo = hl_code(x.x, hf.x) | (hl_code(x.y, hf.y) << 8) | (hl_code(x.z, hf.z) << 16) | (hl_code(x.w, hf.w) << 24);
+    return make_uint4(h.x, h.y, lo, 0u);
 }
 __device__ __forceinline__ float4 hl_value(uint4 p) {
-    const float4 h = bf16x4_f32(make_uint2(p.x, p.y)), l = bf16x4_f32(make_uint2(p.z, p.w));
-    return make_float4(h.x + l.x, h.y + l.y, h.z + l.z, h.w + l.w);
+    const float4 h = bf16x4_f32(make_uint2(p.x, p.y));
+    return make_float4(hl_decode(h.x, p.z), hl_decode(h.y, p.z >> 8), hl_decode(h.z, p.z >> 16), hl_decode(h.w, p.z >> 24));
 }
-__device__ __forceinline__ uint4 hl_load(const uint16_t *hi, const uint16_t *lo) {
-    const uint2 h = *reinterpret_cast<const uint2 *>(hi), l = *reinterpret_cast<const uint2 *>(lo);
-    return make_uint4(h.x, h.y, l.x, l.y);
+__device__ __forceinline__ uint4 hl_load(const uint16_t *hi, const uint8_t *lo) {
+    const uint2 h = *reinterpret_cast<const uint2 *>(hi);
+    return make_uint4(h.x, h.y, *reinterpret_cast<const uint32_t *>(lo), 0u);
 }
-__device__ __forceinline__ void hl_store(uint4 p, uint16_t *hi, uint16_t *lo) {
+__device__ __forceinline__ void hl_store(uint4 p, uint16_t *hi, uint8_t *lo) {
     *reinterpret_cast<uint2 *>(hi) = make_uint2(p.x, p.y);
-    *reinterpret_cast<uint2 *>(lo) = make_uint2(p.z, p.w);
+    *reinterpret_cast<uint32_t *>(lo) = p.z;
 }
 
 // 8 bf16 (one 16-B load) <-> 8 f32
@@ -142,26 +160,24 @@ __device__ __forceinline__ void bf16x8_unpack(uint4 u, float (&f)[8]) {
 __device__ __forceinline__ uint4 bf16x8_pack(const float (&f)[8]) {
     return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
 }
-// the pair (hi, lo) of 8 consecutive elements -> x' = f32(hi) + f32(lo) (hl_value's arithmetic)
-__device__ __forceinline__ void hl8_value(uint4 hi, uint4 lo, float (&x)[8]) {
-    float h[8], l[8];
+// the pair of 8 consecutive elements (16 B of hi, 8 B of lo bytes) -> x′ (hl_value's arithmetic)
+__device__ __forceinline__ void hl8_value(uint4 hi, uint2 lo, float (&x)[8]) {
+    float h[8];
     bf16x8_unpack(hi, h);
-    bf16x8_unpack(lo, l);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = h[k] + l[k];
+    for (int k = 0; k < 8; ++k) x[k] = hl_decode(h[k], (k < 4 ? lo.x : lo.y) >> (8 * (k & 3)));
 }
 // hl_split of 8 elements; xv receives the value the pair stands for (hl_value of the result)
-__device__ __forceinline__ void hl8_split(const float (&x)[8], uint4 &hi, uint4 &lo, float (&xv)[8]) {
+__device__ __forceinline__ void hl8_split(const float (&x)[8], uint4 &hi, uint2 &lo, float (&xv)[8]) {
     hi = bf16x8_pack(x);
-    float hf[8], d[8];
+    float hf[8];
     bf16x8_unpack(hi, hf);
+    uint32_t c[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = x[k] - hf[k];
-    lo = bf16x8_pack(d);
-    float lf[8];
-    bf16x8_unpack(lo, lf);
+    for (int k = 0; k < 8; ++k) c[k] = hl_code(x[k], hf[k]);
+    lo = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24), c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
 #pragma unroll
-    for (int k = 0; k < 8; ++k) xv[k] = hf[k] + lf[k];
+    for (int k = 0; k < 8; ++k) xv[k] = hl_decode(hf[k], c[k]);
 }
 
 // (mean, M2) of one canonical 16-column slice (x[8c + k] = column 32c + slice offset + k).
@@ -274,7 +290,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
 template <int NV>
 // hi != null: the rows are the bf16 pairs (hi, lo) instead of `hidden`.
 __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
-                                                      const uint16_t *__restrict__ lo, int tokens,
+                                                      const uint8_t *__restrict__ lo, int tokens,
                                                       const float *__restrict__ g, const float *__restrict__ b,
                                                       float eps, float *__restrict__ raw, float *__restrict__ normed) {
     constexpr int H = 256 * NV;
@@ -327,7 +343,7 @@ __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__
 __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidden, int tokens, int H,
                                                       const float *__restrict__ cls, const float *__restrict__ pos,
                                                       uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats,
-                                                      uint16_t *__restrict__ lo) {
+                                                      uint8_t *__restrict__ lo) {
     const int img = blockIdx.x;
     const int64_t row = (int64_t)img * tokens;
     if (lo == nullptr) {
@@ -345,12 +361,13 @@ __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidde
 #pragma unroll
         for (int k = 0; k < 8; ++k) x[k] = cls[col + k] + pos[col + k];
         if (lo != nullptr) {
-            uint4 h, l;
+            uint4 h;
+            uint2 l;
             float xv[8];
             hl8_split(x, h, l, xv);
             if (ok) {
                 *reinterpret_cast<uint4 *>(ln_x + row * H + col) = h;
-                *reinterpret_cast<uint4 *>(lo + row * H + col) = l;
+                *reinterpret_cast<uint2 *>(lo + row * H + col) = l;
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
@@ -528,7 +545,7 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
 // With hc_ln: also the CLS rows' bf16 hi and LN statistics, compact (the A operand and
 // row scales of the last layer's CLS-only Q GEMM).
 __global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
-                                                        const uint16_t *__restrict__ lo, int tokens, float *__restrict__ hc,
+                                                        const uint8_t *__restrict__ lo, int tokens, float *__restrict__ hc,
                                                         uint16_t *__restrict__ hc_ln, const float *__restrict__ st,
                                                         float *__restrict__ hc_st) {
     constexpr int H = 768;
