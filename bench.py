@@ -529,7 +529,7 @@ def main():
     # takes the most time per step; `gemms` lists all four.
     M = B * 197
     shapes = {"qkv": (M, 2304, 768, "gemm_pp_kernel<4,0,12> (QKV, LayerNorm 1 folded in)"),
-              "oproj": (M, 768, 768, "gemm_pp_kernel<6,0,12> (O-proj + residual + LN-2 statistics)"),
+              "oproj": (M, 768, 768, "gemm_w2_kernel<6,0> (O-proj + residual + LN-2 statistics; two workgroups per CU)"),
               "fc1": (M, 3072, 768, "gemm_pp_kernel<5,0,12> (fc1 + GELU, LayerNorm 2 folded in)"),
               "fc2": (M, 768, 3072, "gemm_pp_kernel<6,0,48> (fc2 + residual + LN-1 statistics)")}
     model.set_parts(1)

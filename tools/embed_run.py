@@ -11,7 +11,7 @@ vit = importlib.import_module("end-to-end-image-retrieval-service-with-k8s-jenki
 B = int(os.environ.get("BATCH", "256"))
 dev = torch.device("cuda", 0)
 m = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=0, max_batch=B)
-m.set_gemm_variant(int(os.environ.get("VARIANT", "4")))
+m.set_gemm_variant(int(os.environ.get("VARIANT", "0")))
 m.set_parts(int(os.environ.get("PARTS", "1")))
 g = torch.Generator(device=dev).manual_seed(1)
 imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)

@@ -12,7 +12,8 @@ duration, and derived numbers:
 usage: python tools/pmc_summary.py DIR [--json OUT] [--latest profiles/pmc_latest.json]
 
 --latest writes the per-launch HBM traffic of the kernels bench.py prices
-(keys fc1, scan_f16, filter_f16), averaged over that kernel's launches.
+(keys qkv, oproj, fc1, fc2, attention, patch, scan_f16, filter_f16, filter_i8),
+averaged over that kernel's launches; --merge keeps entries this run did not launch.
 """
 import csv
 import glob
@@ -75,11 +76,18 @@ def main():
     if "--latest" in sys.argv:
         # the model's projections (LayerNorm folded, bf16-pair residual stream): EPI 4 QKV,
         # 5 fc1, 6 O-proj (NKT 12) / fc2 (NKT 48)
+        # (round 3: O-proj on the two-workgroup kernel; the int8 filter copy)
         keys = {"fc1": ("gemm_pp_kernel<5, 0, 12>",), "qkv": ("gemm_pp_kernel<4, 0, 12>",),
-                "oproj": ("gemm_pp_kernel<6, 0, 12>",), "fc2": ("gemm_pp_kernel<6, 0, 48>",),
+                "oproj": ("gemm_w2_kernel<6, 0>", "gemm_pp_kernel<6, 0, 12>"), "fc2": ("gemm_pp_kernel<6, 0, 48>",),
+                "attention": ("attention_v2_kernel<197>",), "patch": ("patch_gemm_kernel<16, 7>",),
                 "scan_f16": ("scan_topk_kernel<f16_t, 4, 1, 128>",),
-                "filter_f16": ("filter_qs_kernel<f16_t, 8, 0>",)}
+                "filter_f16": ("filter_qs_kernel<f16_t, 8, 0>",), "filter_i8": ("filter_i8_kernel<4, 128>",)}
         latest = {}
+        if "--merge" in sys.argv:  # keep the entries of kernels this run did not launch
+            try:
+                latest = json.load(open(sys.argv[sys.argv.index("--latest") + 1]))
+            except (OSError, ValueError):
+                latest = {}
         for key, knames in keys.items():
             kname = next((k for k in knames if any(r["kernel"] == k for r in out.values())), knames[0])
             recs = [r for r in out.values() if r["kernel"] == kname]
