@@ -976,8 +976,12 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     // 2-way conflicts on every W store, 46 % of the kernel's LDS cycles, r03b PMC)
     const int wch = tid & 3, wr0 = tid >> 2;
     const uint16_t *wrow = a.W + (int64_t)(n0 + wr0) * KC + wch * 8;
-    const int asw = ((ar >> 3) & 1) << 1, wsw = ((wr0 >> 3) & 1) << 1;  // chunk XOR of the fragment layout
-                                                                     // (rows wr0 + 64 i share bit 3)
+    // chunk XOR of row r: bit 3 of r -> chunk bit 1, bit 1 of r -> chunk bit 0.  The fragment reads
+    // (ds_read_b128, rows li of 16-row blocks) stay conflict-free, and so do the A stores: a
+    // ds_write_b128 lane group of 8 covers rows ar..ar+3, whose 64-B rows alias mod 128 B in
+    // pairs (0/2, 1/3) without the bit-1 term (2-way on every A store, r03e PMC)
+    auto swz = [](int r) { return (((r >> 3) & 1) << 1) | ((r >> 1) & 1); };
+    const int asw = swz(ar), wsw = swz(wr0);  // rows wr0 + 64 i share bits 1 and 3
 
     // register staging two K-steps ahead: set R holds step kt + 2 while step kt + 1's
     // set is written to LDS, so each global load has two steps of MFMAs to land
@@ -1018,7 +1022,7 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(Ws + (wr0 + 64 * i) * 64 + ((wch ^ wsw) << 4)) = r.wv[i];
     };
-    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+    const int fchunk = (g ^ swz(li)) << 4;
 
     f32x4 acc[8][4];
 #pragma unroll

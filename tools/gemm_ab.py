@@ -3,7 +3,7 @@
 For each round and each variant: rc_model_set_gemm_variant, then (a) `steps` timed embeds of a
 batch-256 at the bench's --parts (whole-step wall time) and (b) per-GEMM HIP-event timings on
 the unsplit batch.  Prints one JSON line per round and a summary (median over rounds).
-    python tools/gemm_ab.py [VARIANTS=4,5,6] [ROUNDS=5] [STEPS=10]
+    python tools/gemm_ab.py [VARIANTS=4,5,6] [ROUNDS=5] [STEPS=10] [ROLES=qkv,oproj,fc1,fc2]
 """
 import importlib
 import json
@@ -27,7 +27,7 @@ g = torch.Generator(device=dev).manual_seed(1)
 imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
 raw = torch.empty((B, 768), device=dev)
 nrm = torch.empty((B, 768), device=dev)
-roles = ["qkv", "oproj", "fc1", "fc2"]
+roles = os.environ.get("ROLES", "qkv,oproj,fc1,fc2").split(",")
 res = {v: {"step_ms": [], **{r: [] for r in roles}} for v in variants}
 ref = None
 for r in range(rounds):
