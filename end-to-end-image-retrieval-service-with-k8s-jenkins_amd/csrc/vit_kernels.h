@@ -111,19 +111,28 @@ __device__ __forceinline__ float4 bf16x4_f32(uint2 u) {
                        __uint_as_float(u.y & 0xffff0000u));
 }
 __device__ __forceinline__ uint2 pack_bf16x4(float4 v) { return make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)); }
-// s = ulp(h) / 256 = 2^(E − 142) for h's biased exponent E, and 1 / s (both 0 below E = 16)
+// s = ulp(h) / 256 = 2^(E − 142) for h's biased exponent E (0 below E = 16: one saturating
+// subtract of the exponent field), and 1 / s = 2^(142 − E).  Below E = 16 (|h| < 2^-111) the
+// inverse is a meaningless finite number: the byte it yields is never used, since s = 0 there.
 __device__ __forceinline__ float hl_step(float h) {
     const uint32_t e = __float_as_uint(h) & 0x7f800000u;
-    return e > (15u << 23) ? __uint_as_float(e - (15u << 23)) : 0.f;
+    return __uint_as_float(__builtin_elementwise_sub_sat(e, 15u << 23));
 }
 __device__ __forceinline__ float hl_inv_step(float h) {
     const uint32_t e = __float_as_uint(h) & 0x7f800000u;
-    return e > (15u << 23) ? __uint_as_float((269u << 23) - e) : 0.f;
+    return __uint_as_float((269u << 23) - e);
+}
+// q = rint((x − h) / s) clamped to [−127, 127], as a float (exact)
+__device__ __forceinline__ float hl_qf(float x, float h) {
+    return fminf(fmaxf(rintf((x - h) * hl_inv_step(h)), -127.f), 127.f);
 }
 // the low byte of x around h = RNE_bf16(x), and the value a (h, byte) pair stands for
-__device__ __forceinline__ uint32_t hl_code(float x, float h) {
-    const int q = (int)rintf((x - h) * hl_inv_step(h));
-    return (uint32_t)(q < -127 ? -127 : (q > 127 ? 127 : q)) & 0xffu;
+__device__ __forceinline__ uint32_t hl_code(float x, float h) { return (uint32_t)(int)hl_qf(x, h) & 0xffu; }
+// the low bytes of four codes (as ints) packed little-endian: three v_perm_b32
+__device__ __forceinline__ uint32_t hl_pack4(int c0, int c1, int c2, int c3) {
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)c1, (uint32_t)c0, 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)c3, (uint32_t)c2, 0x0c0c0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 __device__ __forceinline__ float hl_decode(float h, uint32_t byte) {
     return fmaf((float)(int)(int8_t)(uint8_t)byte, hl_step(h), h);
@@ -132,7 +141,7 @@ __device__ __forceinline__ float hl_decode(float h, uint32_t byte) {
 __device__ __forceinline__ uint4 hl_split(float4 x) {
     const uint2 h = pack_bf16x4(x);
     const float4 hf = bf16x4_f32(h);
-    const uint32_t lo = hl_code(x.x, hf.x) | (hl_code(x.y, hf.y) << 8) | (hl_code(x.z, hf.z) << 16) | (hl_code(x.w, hf.w) << 24);
+    const uint32_t lo = hl_pack4((int)hl_qf(x.x, hf.x), (int)hl_qf(x.y, hf.y), (int)hl_qf(x.z, hf.z), (int)hl_qf(x.w, hf.w));
     return make_uint4(h.x, h.y, lo, 0u);
 }
 __device__ __forceinline__ float4 hl_value(uint4 p) {
@@ -172,12 +181,14 @@ __device__ __forceinline__ void hl8_split(const float (&x)[8], uint4 &hi, uint2 
     hi = bf16x8_pack(x);
     float hf[8];
     bf16x8_unpack(hi, hf);
-    uint32_t c[8];
+    int c[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = hl_code(x[k], hf[k]);
-    lo = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24), c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) xv[k] = hl_decode(hf[k], c[k]);
+    for (int k = 0; k < 8; ++k) {  // the decode reuses q as a float: hl_decode's value, no byte round trip
+        const float qf = hl_qf(x[k], hf[k]);
+        c[k] = (int)qf;
+        xv[k] = fmaf(qf, hl_step(hf[k]), hf[k]);
+    }
+    lo = make_uint2(hl_pack4(c[0], c[1], c[2], c[3]), hl_pack4(c[4], c[5], c[6], c[7]));
 }
 
 // (mean, M2) of one canonical 16-column slice (x[8c + k] = column 32c + slice offset + k).
