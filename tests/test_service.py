@@ -1,0 +1,121 @@
+"""The one-process service (``…_amd/service.py``): every route of the reference's three pods
+over one in-HBM index.
+
+Reference deployment: ingest (``ingesting/main.py:37,172``) and retriever
+(``retriever/main.py:36,173``) are two processes that open the SAME Pinecone index by
+name.  The in-HBM index is process-local, so the drop-in serves both from one app; the
+GPU test pushes through it and then searches through it.  ``/embed`` is also pinned by
+value: the service loaded from a seed-1907 safetensors checkpoint returns the golden
+vector (reference ``tests/test_embedding.py:32-38`` checks only the length).
+"""
+import io
+import os
+
+import numpy as np
+import pytest
+from fastapi.testclient import TestClient
+
+from conftest import GOLDEN, import_pkg
+
+
+@pytest.fixture(scope="module")
+def svc():
+    return TestClient(import_pkg("service").app)
+
+
+@pytest.fixture(scope="module")
+def fixture_jpeg():
+    with open(os.path.join(GOLDEN, "test_image.jpeg"), "rb") as f:
+        return f.read()
+
+
+def test_service_serves_every_route(svc):
+    paths = {getattr(r, "path", None) for r in import_pkg("service").app.router.routes}
+    for p in ("/", "/healthz", "/embed", "/embed_batch", "/push_image", "/push_images", "/search_image"):
+        assert p in paths, p
+    assert svc.get("/healthz").json() == {"status": "healthy"}
+    assert svc.get("/").json() == {"message": "Welcome to the Image Retrieval API. Visit /docs to test."}
+
+
+def test_service_validation_contract(svc):
+    """The per-route 400 / 422 responses of the three reference services (GPU-free)."""
+    assert svc.post("/embed").status_code == 422
+    assert svc.post("/push_image").status_code == 422
+    assert svc.post("/search_image").status_code == 422
+    bad = ("a.jpg", b"This is not an image.", "image/jpeg")
+    r = svc.post("/embed", files={"file": bad})
+    assert r.status_code == 400 and r.json()["detail"] == "Uploaded file is not a valid image."
+    r = svc.post("/push_image", files={"file": bad})
+    assert r.status_code == 400 and r.json()["detail"] == "Invalid image file"
+    r = svc.post("/push_image", files={"file": ("a.gif", b"GIF89a", "image/gif")})
+    assert r.status_code == 400 and r.json()["detail"] == "Only .jpg/.jpeg/.png allowed"
+    r = svc.post("/search_image", files={"file": bad})
+    assert r.status_code == 400 and r.json()["detail"] == "Uploaded file is not a valid image."
+
+
+def test_service_embeds_in_process():
+    s = import_pkg("service")
+    utils = import_pkg("ingesting.utils")
+    assert import_pkg("ingesting.main").get_feature_vector is utils.embed_locally
+    assert import_pkg("retriever.main").get_feature_vector is utils.embed_locally
+    assert s.index is not None
+
+
+def _jpeg(seed, w=224, h=224):
+    from PIL import Image
+
+    arr = np.random.default_rng(seed).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(arr).save(b, format="JPEG", quality=85)
+    return b.getvalue()
+
+
+@pytest.mark.gpu
+def test_service_push_then_search_one_index(svc, fixture_jpeg, cuda, monkeypatch):
+    """push through the service, search through the service: the pushed image's URL is first,
+    and both routes saw the one index."""
+    cfg = import_pkg("config").Config
+    monkeypatch.setattr(cfg, "INDEX_NAME", "one-process-service")
+    r = svc.post("/push_image", files={"file": ("fixture.jpeg", fixture_jpeg, "image/jpeg")})
+    assert r.status_code == 200
+    first = r.json()
+    others = [("files", (f"o{i}.jpg", _jpeg(100 + i, 300 - 8 * i, 168 + 4 * i), "image/jpeg")) for i in range(7)]
+    r = svc.post("/push_images", files=others)
+    assert r.status_code == 200 and len(r.json()) == 7
+    batch = r.json()
+    ix = import_pkg("service").index()
+    assert len(ix) == 8
+    r = svc.post("/search_image", files={"file": ("q.jpeg", fixture_jpeg, "image/jpeg")})
+    assert r.status_code == 200
+    urls = r.json()
+    assert len(urls) == cfg.TOP_K
+    assert urls[0] == first["signed_url"] and urls[0].endswith(first["gcs_path"])
+    # an image of the batched push also finds itself first
+    r = svc.post("/search_image", files={"file": others[3][1]})
+    assert r.status_code == 200 and r.json()[0] == batch[3]["signed_url"]
+    ix.close()
+    import_pkg("ingesting.utils")._indexes.pop("one-process-service", None)
+
+
+@pytest.mark.gpu
+def test_embed_route_by_value_seed1907_checkpoint(svc, fixture_jpeg, cuda, tmp_path, monkeypatch):
+    """POST /embed on the reference's fixture with the service loaded from a seed-1907
+    safetensors checkpoint is within 1e-3 cosine of the transformers golden (fp32 tier)."""
+    from safetensors.numpy import save_file
+
+    from oracle.weights import seeded_vit_msn_weights
+
+    save_file({k: np.ascontiguousarray(v) for k, v in seeded_vit_msn_weights(1907).items()},
+              str(tmp_path / "model.safetensors"))
+    emb = import_pkg("embedding.main")
+    monkeypatch.setattr(emb.Config, "MODEL_PATH", str(tmp_path))
+    emb.reset_embedder()
+    try:
+        r = svc.post("/embed", files={"file": ("test_image.jpeg", fixture_jpeg, "image/jpeg")})
+        assert r.status_code == 200
+        got = np.asarray(r.json(), dtype=np.float64)
+        ref = np.load(os.path.join(GOLDEN, "test_image_embedding_seed1907.npy")).astype(np.float64).reshape(-1)
+        cos = got @ ref / (np.linalg.norm(got) * np.linalg.norm(ref))
+        assert got.shape == (768,) and 1.0 - cos < 1e-3, 1.0 - cos
+    finally:
+        emb.reset_embedder()

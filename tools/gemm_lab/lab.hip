@@ -1,0 +1,301 @@
+// GEMM lab (diagnostic, never loaded by the product): main-loop structures for the
+// ViT-MSN batch-256 projection shapes, C[M][N] = A[M][K] . W[N][K]^T, bf16 in, f32
+// accumulate, bf16 out (no bias / epilogue work: this isolates the K loop).
+//
+//  variant 0: the product's ping-pong schedule (gemm.h gemm_pp_kernel), 256x256x64, 8 waves
+//  variant 1: 0 with in-LDS s_memtime stamps at every barrier (waves 0 and 4, blocks 0-7)
+//  variant 2: ping-pong, W fragments kept in registers for the whole K-step (24 LDS reads
+//             per wave per K-step instead of 32)
+//  variant 3: 4 waves, one per SIMD, 128x128 outputs per wave, one barrier per K-step,
+//             the next K-tile's LDS-DMA interleaved with this one's MFMAs
+//  variant 4: 0 with the LDS-DMA as buffer loads (one lane offset, scalar row offsets)
+// Every variant accumulates each output over K in the same order (chunks of 32, k
+// ascending), so their results are bit-identical.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+struct LabArgs {
+    const uint16_t *A, *W;
+    uint16_t *C;
+    int M, N, K;
+    uint64_t *stamps;  // variant 1: [16 (block, group)][512]
+};
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    bf16x2 v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+}
+// tile id -> (row tile, column tile); groups of 8 row tiles (column-major inside) when N/256 >= 6
+__device__ __forceinline__ void tile_coords(const LabArgs &a, int BM, int BN, int tile, int &tm, int &tn) {
+    const int ntn = a.N / BN, ntm = (a.M + BM - 1) / BM;
+    tm = tile / ntn;
+    tn = tile % ntn;
+    if (ntn >= 6) {
+        const int G = 8, gt = G * ntn, gi = tile / gt, in = tile - gi * gt;
+        const int gm = min(G, ntm - gi * G);
+        tm = gi * G + in % gm;
+        tn = in / gm;
+    }
+}
+
+__device__ __forceinline__ void bar() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// ------------------------------------------------------------------ ping-pong
+constexpr int PP_STAGE = 2 * 256 * 64 * 2;  // A tile then W tile, 32 KB each
+
+template <int VAR>
+__global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
+    constexpr bool STAMP = VAR == 1, WKEEP = VAR == 2, BUF = VAR == 4;
+    constexpr int A_BYTES = 256 * 64 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + (STAMP ? 8192 : 0)];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 64;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+    const bool stamper = STAMP && lane == 0 && (wave & 3) == 0 && blockIdx.x < 8;
+    int ns = 0;
+    auto stamp = [&]() {
+        if constexpr (STAMP) {
+            if (stamper && ns < 512)
+                *reinterpret_cast<uint64_t *>(smem + 2 * PP_STAGE + grp * 4096 + ns * 8) = __builtin_amdgcn_s_memtime();
+            ++ns;
+        }
+    };
+
+    const int lr = wave * 8 + (lane >> 3);
+    const uint32_t voff = (uint32_t)(lr * K + (((lane & 7) ^ ((lr >> 1) & 7)) << 3)) * 2u;
+    auto stage4 = [&](int buf, int k0, int i0) {
+        uint8_t *base = smem + buf * PP_STAGE;
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = i < 4;
+            if constexpr (BUF) {  // one lane offset, the piece's rows in soffset, the K-step in the descriptor
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc((void *)((is_a ? Ag : Wg) + k0), (short)0, 0x7fffffff, 0x00020000);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(base + piece * 1024), 16, voff, (i & 3) * 64 * K * 2, 0, 0);
+            } else {
+                const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
+                const int c = (lane & 7) ^ ((r >> 1) & 7);
+                const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
+                __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+            }
+        }
+    };
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 2; ++l) acc[i][j][k][l] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    stamp();
+    stage4(0, 0, 0);
+    stage4(0, 0, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    stamp();
+    if (grp == 1) bar();
+
+    bf16x8 af[4][2], wf[2][2][2];  // [mi][s], [nq][ni][s]
+#pragma nounroll
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const uint8_t *As = smem + cur * PP_STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+        const bool more = kt + 1 < nk;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mq = p >> 1;
+            const int nq = (p == 1 || p == 2);
+            if (p == 0 || p == 2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        const int c = s * 4 + g;
+                        af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+            const bool wread = WKEEP ? (p == 0 || p == 1) : true;
+            if (wread) {
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                        const int c = s * 4 + g;
+                        wf[WKEEP ? nq : 0][ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+            if (more && p < 2) stage4(cur ^ 1, (kt + 1) * 64, p * 4);
+            if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            stamp();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[WKEEP ? nq : 0][ni][s], af[mi][s],
+                                                                                     acc[mq][nq][mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+            stamp();
+        }
+    }
+    if (grp == 0) bar();
+    stamp();
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                    const int col = n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                    const f32x4 v = acc[mq][nq][mi][ni];
+                    if (row < a.M)
+                        *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                }
+    if constexpr (STAMP) {
+        stamp();
+        __syncthreads();
+        if (blockIdx.x < 8 && tid < 64 * 8 && (wave & 3) == 0) {
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(smem + 2 * PP_STAGE + grp * 4096);
+            for (int i = lane; i < 512; i += 64) a.stamps[(blockIdx.x * 2 + grp) * 512 + i] = i < ns ? src[i] : 0;
+        }
+    }
+}
+
+// --------------------------------------------------- 4 waves, 128x128 per wave
+// 256x256x64 tile, wave w: rows (w >> 1) * 128, columns (w & 1) * 128; acc[mi][ni] =
+// 8 x 8 tiles of mfma_f32_16x16x32_bf16 (swapped operands: A-operand = weight rows).
+// K-step t: vmcnt(0) (this wave's DMA of stage t) + barrier; then for each 32-deep half s:
+// 16 fragment reads (8 A, 8 W) and 64 MFMAs, with this wave's 16 DMA pieces of stage t + 1
+// spread over the first half's MFMAs.
+__global__ __launch_bounds__(256, 1) void lab_w4(LabArgs a) {
+    constexpr int A_BYTES = 256 * 64 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 64;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+
+    // piece p = 0..63 (1 KB = 8 rows x 128 B): A rows 8p.. for p < 32, W rows 8(p-32).. after;
+    // wave w issues pieces w + 4 i, i = 0..15 (i < 8: A).  Row r = 8w + 32 (i % 8) + lane / 8, so
+    // the source chunk swizzle (r >> 1) & 7 does not depend on i: one lane offset for every
+    // piece, the piece's rows in the scalar offset, the K-step in the descriptor base.
+    const int lr = wave * 8 + (lane >> 3);
+    const uint32_t voff = (uint32_t)(lr * K + (((lane & 7) ^ ((lr >> 1) & 7)) << 3)) * 2u;
+    auto piece = [&](int buf, int k0, int i) {
+        const uint16_t *base = (i < 8 ? Ag : Wg) + k0;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, 0x7fffffff, 0x00020000);
+        lds_void_t *dst = (lds_void_t *)(smem + buf * PP_STAGE + (wave + 4 * i) * 1024);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, voff, (i & 7) * 32 * K * 2, 0, 0);
+    };
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) piece(0, 0, i);
+
+#pragma nounroll
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const uint8_t *As = smem + cur * PP_STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+        const bool more = kt + 1 < nk;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[8], wf[8];
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) {
+                const int r = wc * 128 + ni * 16 + li;
+                const int c = s * 4 + g;
+                wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                const int r = wr * 128 + mi * 16 + li;
+                const int c = s * 4 + g;
+                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                if (s == 0 && more) {
+                    piece(cur ^ 1, (kt + 1) * 64, 2 * mi);
+                    piece(cur ^ 1, (kt + 1) * 64, 2 * mi + 1);
+                }
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int row = m0 + wr * 128 + mi * 16 + li;
+            const int col = n0 + wc * 128 + ni * 16 + 4 * g;
+            const f32x4 v = acc[mi][ni];
+            if (row < a.M)
+                *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+}
+
+extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
+                        uint64_t *stamps, hipStream_t s) {
+    if (N % 256 || K % 64) return 1;
+    LabArgs a{A, W, C, M, N, K, stamps};
+    const int tiles = ((M + 255) / 256) * (N / 256);
+    switch (variant) {
+        case 0: hipLaunchKernelGGL(lab_pp<0>, dim3(tiles), dim3(512), 0, s, a); break;
+        case 1: hipLaunchKernelGGL(lab_pp<1>, dim3(tiles), dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(lab_pp<2>, dim3(tiles), dim3(512), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(lab_w4, dim3(tiles), dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(lab_pp<4>, dim3(tiles), dim3(512), 0, s, a); break;
+        default: return 2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
