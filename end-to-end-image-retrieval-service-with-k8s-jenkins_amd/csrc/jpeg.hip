@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t *__restri
 // ([y0, y0 + Hs)), into tmp [Hs][S][3], then the vertical pass into out [S][S][3]; an
 // axis whose size already is S is skipped (need_h / need_v), as Pillow skips it.
 struct RDesc {
-    int32_t S, need_h, need_v, y0, Hs, hk, vk, pad;
+    int32_t S, need_h, need_v, y0, Hs, hk, vk, bh;  // bh: output rows per block of the band kernel
     const int *hb, *hc;  // horizontal bounds [S][2] (xmin, count) / coefficients [S][hk]
     const int *vb, *vc;  // vertical bounds relative to y0 / coefficients [S][vk]
     int64_t tmp_off, out_off;
@@ -687,6 +687,124 @@ __global__ __launch_bounds__(256) void jpeg_resize_v_kernel(const RDesc *__restr
     o[2] = clip8_22(a2);
 }
 
+
+// Band-fused decode → resize (rc_jpeg_decode_resized when every image's band fits in LDS):
+// grid (max bands, n), 256 lanes; block (b, i) produces output rows [b·bh, b·bh + bh) of image
+// i whole.  It reads once the source rows their vertical taps span ([lo, hi), Pillow's
+// ImagingResampleInner order: the horizontal pass covers exactly the rows the vertical one
+// reads), colour-converts them into LDS (src, [rows][W][3]), runs the horizontal pass into
+// LDS (tmp, [rows][S][3], u8 as Pillow's intermediate image), then the vertical pass into an
+// LDS copy of the band, stored with 16-B writes.  No intermediate image in HBM and no
+// per-row blocks: each block streams its band's plane rows with every lane busy.  The
+// arithmetic is jpeg_color_resize_h_kernel's + jpeg_resize_v_kernel's, so the bytes equal
+// that path's (and PIL decode + Image.resize).
+// dynamic LDS = the largest per-image need (band_lds_bytes, host).
+// LDS layout of one band: src [rows][W][3] (need_h only), tmp [rows][S][3], the band's output
+// [nout][S][3] (need_v only: over src when it fits there, else after tmp); returns the bytes.
+struct BandLayout {
+    int tmp, band, total;
+};
+__host__ __device__ inline BandLayout band_layout(int rows, int nout, int W, int S, int need_h, int need_v) {
+    auto al = [](int b) { return (b + 15) & ~15; };
+    BandLayout L;
+    const int src = need_h ? al(rows * W * 3) : 0;
+    L.tmp = src;
+    L.total = src + al(rows * S * 3);
+    L.band = L.tmp;  // no vertical pass: tmp is the band
+    if (need_v) {
+        if (nout * S * 3 <= src) {
+            L.band = 0;
+        } else {
+            L.band = L.total;
+            L.total += al(nout * S * 3);
+        }
+    }
+    return L;
+}
+
+__global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
+                                                              const Desc *__restrict__ descs,
+                                                              const RDesc *__restrict__ rdescs, uint8_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const Desc d = descs[blockIdx.y];
+    const RDesc r = rdescs[blockIdx.y];
+    const int S = r.S, yo0 = (int)blockIdx.x * r.bh;
+    if (yo0 >= S) return;  // block-uniform: this image has fewer bands
+    const int yo1 = min(S, yo0 + r.bh), nout = yo1 - yo0;
+    // source rows of the band (relative to r.y0; Pillow's bounds are monotone in the output row)
+    const int lo = r.need_v ? r.vb[2 * yo0] : yo0;
+    const int hi = r.need_v ? r.vb[2 * (yo1 - 1)] + r.vb[2 * (yo1 - 1) + 1] : yo1;
+    const int rows = hi - lo, W = d.W;
+    const BandLayout L = band_layout(rows, nout, W, S, r.need_h, r.need_v);
+    uint8_t *src = lds, *tmp = lds + L.tmp, *band = lds + L.band;
+    // 1. colour: the band's source rows (straight into tmp when the width already is S)
+    {
+        uint8_t *dst = r.need_h ? src : tmp;
+        const int n = rows * W;
+        for (int idx = threadIdx.x; idx < n; idx += 256) {
+            const int rr = idx / W, x = idx - rr * W;
+            int R, G, B;
+            ycc_rgb(planes, d, x, r.y0 + lo + rr, R, G, B);
+            uint8_t *o = dst + 3 * idx;
+            o[0] = (uint8_t)R;
+            o[1] = (uint8_t)G;
+            o[2] = (uint8_t)B;
+        }
+    }
+    __syncthreads();
+    // 2. horizontal pass (Pillow's fixed point: 22 fractional bits, rounding 1 << 21, clip)
+    if (r.need_h) {
+        const int n = rows * S;
+        for (int idx = threadIdx.x; idx < n; idx += 256) {
+            const int rr = idx / S, xo = idx - rr * S;
+            const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
+            const int *c = r.hc + xo * r.hk;
+            const uint8_t *p = src + (rr * W + xmin) * 3;
+            int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+            for (int k = 0; k < xn; ++k) {
+                const int ck = c[k];
+                a0 += p[3 * k] * ck;
+                a1 += p[3 * k + 1] * ck;
+                a2 += p[3 * k + 2] * ck;
+            }
+            uint8_t *o = tmp + 3 * idx;
+            o[0] = clip8_22(a0);
+            o[1] = clip8_22(a1);
+            o[2] = clip8_22(a2);
+        }
+        __syncthreads();
+    }
+    // 3. vertical pass into the band's LDS image (over src, free now, when it fits), then 16-B stores
+    if (r.need_v) {
+        const int n = nout * S;
+        for (int idx = threadIdx.x; idx < n; idx += 256) {
+            const int j = idx / S, x = idx - j * S, yo = yo0 + j;
+            const int ymin = r.vb[2 * yo] - lo, yn = r.vb[2 * yo + 1];
+            const int *c = r.vc + yo * r.vk;
+            const uint8_t *q = tmp + (ymin * S + x) * 3;
+            int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+            for (int k = 0; k < yn; ++k) {
+                const int ck = c[k];
+                a0 += q[k * S * 3] * ck;
+                a1 += q[k * S * 3 + 1] * ck;
+                a2 += q[k * S * 3 + 2] * ck;
+            }
+            uint8_t *o = band + 3 * idx;
+            o[0] = clip8_22(a0);
+            o[1] = clip8_22(a1);
+            o[2] = clip8_22(a2);
+        }
+        __syncthreads();
+    }
+    uint8_t *g = out + r.out_off + (int64_t)yo0 * S * 3;
+    const int nbytes = nout * S * 3;
+    if (((r.out_off + (int64_t)yo0 * S * 3) & 15) == 0 && (nbytes & 15) == 0) {
+        for (int i = threadIdx.x; i < nbytes / 16; i += 256)
+            reinterpret_cast<uint4 *>(g)[i] = reinterpret_cast<const uint4 *>(band)[i];
+    } else {
+        for (int i = threadIdx.x; i < nbytes; i += 256) g[i] = band[i];
+    }
+}
 }  // namespace jpeg
 
 // Batched decoder: pinned host staging + device buffers sized at create.
@@ -713,6 +831,7 @@ struct JpegDecoder {
     struct Coeffs {
         int ksize = 0, first = 0, last = 0;
         int *bounds = nullptr, *coef = nullptr;
+        std::vector<int> hbounds;  // host copy of bounds (the band planner reads it)
     };
     std::map<std::tuple<int, int, int, int>, Coeffs> coeffs;
 };
@@ -814,6 +933,8 @@ static int huffman_threads() {
 
 namespace {
 
+std::atomic<int> g_active_decodes{0};  // decode calls in their Huffman pass right now (any decoder)
+
 // Header parse, host Huffman (threaded), pinned staging and H2D copies, IDCT into
 // h->d_planes; fills h->h_desc / h->d_desc (rgb_off from rgb_offsets, or 0).  The caller
 // records h->staged after its own uploads from pinned memory and launches the colour pass.
@@ -839,7 +960,13 @@ void stage_idct(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int
             errs[i] = e.what();
         }
     };
-    const int nthreads = std::max(1, std::min<int>(n, huffman_threads()));
+    // concurrent calls (an EmbedderPool decoding per member) split the worker budget
+    struct Active {
+        int n;
+        Active() : n(g_active_decodes.fetch_add(1) + 1) {}
+        ~Active() { g_active_decodes.fetch_sub(1); }
+    } active;
+    const int nthreads = std::max(1, std::min<int>(n, huffman_threads() / active.n));
     if (nthreads == 1) {
         for (int i = 0; i < n; ++i) work(i);
     } else {
@@ -897,6 +1024,7 @@ const rc_jpeg_decoder::Coeffs &resize_coeffs(rc_jpeg_decoder *h, int in_size, in
     d.first = c.bounds[0];
     d.last = c.bounds[2 * (out_size - 1)] + c.bounds[2 * (out_size - 1) + 1];
     for (int i = 0; i < out_size; ++i) c.bounds[2 * i] -= shift;
+    d.hbounds = c.bounds;
     d.bounds = (int *)dmalloc(c.bounds.size() * sizeof(int));
     try {
         d.coef = (int *)dmalloc(c.coef.size() * sizeof(int));
@@ -948,7 +1076,8 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
         stage_idct(h, n, jpgs, lens, nullptr, s, hd, maxpix);
         const int S = out_size;
         int64_t tmp_need = 0;
-        int maxrows = 1;
+        int maxrows = 1, maxbands = 1, band_lds = 0;
+        bool band_ok = true;  // every image's bands fit in LDS: the band kernel, else the two-pass path
         for (int i = 0; i < n; ++i) {
             const int W = hd[i].width, H = hd[i].height;
             jpeg::RDesc &r = h->h_rdesc[i];
@@ -963,6 +1092,7 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
                 r.hc = ch.coef;
                 r.hk = ch.ksize;
             }
+            const std::vector<int> *vb = nullptr;
             if (r.need_v) {
                 const auto &cv = resize_coeffs(h, H, S, resample, 0);
                 // ImagingResampleInner: the horizontal pass covers just the rows the vertical one reads
@@ -974,18 +1104,51 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
                 r.vb = cvs.bounds;
                 r.vc = cvs.coef;
                 r.vk = cvs.ksize;
+                vb = &cvs.hbounds;
                 r.tmp_off = tmp_need;
                 tmp_need += (int64_t)r.Hs * S * 3;
             }
             r.out_off = (int64_t)i * S * S * 3;
             maxrows = std::max(maxrows, r.Hs);
+            // band height: the tallest band (32 .. 1 output rows) whose LDS fits 32 KB, else 64 KB
+            r.bh = 0;
+            int need = 0;
+            for (const int cap : {32 * 1024, 64 * 1024}) {
+                for (int bh = 32; bh >= 1 && r.bh == 0; bh /= 2) {
+                    int worst = 0;
+                    for (int yo0 = 0; yo0 < S; yo0 += bh) {
+                        const int yo1 = std::min(S, yo0 + bh);
+                        const int lo = vb ? (*vb)[2 * yo0] : yo0;
+                        const int hi = vb ? (*vb)[2 * (yo1 - 1)] + (*vb)[2 * (yo1 - 1) + 1] : yo1;
+                        worst = std::max(worst, jpeg::band_layout(hi - lo, yo1 - yo0, W, S, r.need_h, r.need_v).total);
+                    }
+                    if (worst <= cap) {
+                        r.bh = bh;
+                        need = worst;
+                    }
+                }
+                if (r.bh) break;
+            }
+            if (r.bh == 0) band_ok = false;
+            else {
+                maxbands = std::max(maxbands, (S + r.bh - 1) / r.bh);
+                band_lds = std::max(band_lds, need);
+            }
         }
-        if ((size_t)tmp_need > h->tmp_bytes) {  // grows with the largest batch seen; steady state allocates nothing
+        if (band_ok) {
+            RC_HIP(hipMemcpyAsync(h->d_rdesc, h->h_rdesc, (size_t)n * sizeof(jpeg::RDesc), hipMemcpyHostToDevice, s));
+            RC_HIP(hipEventRecord(h->staged, s));
+            hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel, dim3((unsigned)maxbands, (unsigned)n), dim3(256),
+                               (size_t)band_lds, s, h->d_planes, h->d_desc, h->d_rdesc, out);
+            RC_LAUNCH_CHECK();
+            return;
+        }
+        if ((size_t)tmp_need > h->tmp_bytes) {  // grows geometrically with the largest batch seen
+            const size_t want = std::max<size_t>((size_t)tmp_need, 2 * h->tmp_bytes);
             RC_HIP(hipStreamSynchronize(s));
             dfree(h->d_tmp);
             h->d_tmp = nullptr;
             h->tmp_bytes = 0;
-            const size_t want = std::max<size_t>((size_t)tmp_need, 2 * h->tmp_bytes);
             h->d_tmp = (uint8_t *)dmalloc(want);
             h->tmp_bytes = want;
         }

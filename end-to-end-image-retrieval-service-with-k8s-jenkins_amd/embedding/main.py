@@ -113,6 +113,7 @@ def decode_many(blobs: List[bytes]) -> list:
     any stream the GPU decoder rejects — through PIL on the host at its own size
     (``UnidentifiedImageError`` → 400), resized later inside rc_embed."""
     import numpy as np
+    import torch
 
     out: list = [None] * len(blobs)
     gpu = [i for i, b in enumerate(blobs) if _gpu_jpeg(b)]
@@ -122,7 +123,8 @@ def decode_many(blobs: List[bytes]) -> list:
         out[i] = np.asarray(decode_image(blobs[i]), dtype=np.uint8)
     if gpu:
         try:
-            for i, im in zip(gpu, get_embedder().decode_jpeg_for_embed([blobs[i] for i in gpu]).unbind(0)):
+            ims = get_embedder().decode_jpeg_for_embed([blobs[i] for i in gpu])  # a pool decodes per member GPU
+            for i, im in zip(gpu, ims.unbind(0) if isinstance(ims, torch.Tensor) else ims):
                 out[i] = im
         except ValueError:  # a damaged stream: the reference's host decode decides (image or 400)
             for i in gpu:
@@ -133,7 +135,10 @@ def decode_many(blobs: List[bytes]) -> list:
 def embed_many_device(blobs: List[bytes], normalized: bool = False):
     """Image bytes → (raw [n,768], normed or None) device tensors (the batched ingest path)."""
     images = decode_many(blobs)
-    return get_embedder().embed_images(images, normalized=normalized)
+    emb = get_embedder()
+    if hasattr(emb, "assign_by_location"):  # a pool: embed each image on the GPU that decoded it
+        return emb.embed_images(images, normalized=normalized, assign=emb.assign_by_location(images))
+    return emb.embed_images(images, normalized=normalized)
 
 
 def embed_many(blobs: List[bytes]) -> list[list[float]]:

@@ -256,6 +256,10 @@ class ShardSet:
         check(self.lib.rc_sharded_create(self.n, arr, self.dim, _lib.DTYPES[dtype], int(capacity_per_shard),
                                          _lib.C.byref(h)))
         self._h = h
+        # rows upsert_parts had to copy from another GPU than their shard's (an EmbedderPool
+        # batch whose planned rows shifted under a concurrent ingest): results stay exact,
+        # this counts the extra xGMI traffic
+        self.cross_device_rows = 0
         self._shards = []
         for sh in range(self.n):
             ih = _lib.C.c_void_p()
@@ -349,6 +353,8 @@ class ShardSet:
             for s in torch.unique(sh).tolist():
                 sel = torch.nonzero(sh == s).reshape(-1)
                 d = self.devices[s]
+                if vecs.device != torch.device("cuda", d):
+                    self.cross_device_rows += int(sel.numel())
                 v = vecs if sel.numel() == rows.numel() else vecs[sel.to(vecs.device)]
                 with torch.cuda.device(d):
                     v = v.to(device=torch.device("cuda", d), dtype=torch.float32).contiguous()
@@ -579,7 +585,7 @@ class Index:
                 offs = torch.tensor([o for o, _ in lst], dtype=torch.int64)
                 v = t if len(lst) == t.shape[0] and offs.tolist() == list(range(t.shape[0])) else t[offs.to(t.device)]
                 out.append((torch.tensor([r for _, r in lst], dtype=torch.int64), v))
-            self._set.upsert_parts(out)  # raises before anything below registers the ids
+            self._device_write(self._set.upsert_parts, out)
             self._commit_rows(items, rows)
         return {"upserted_count": len(items)}
 
@@ -603,10 +609,20 @@ class Index:
             self._meta[vid] = md
         self._gen += 1
 
+    def _device_write(self, fn, *args) -> None:
+        """A shard write under the lock.  If it raises part-way (an earlier shard already
+        overwrote the rows of existing ids), the values cached by the last query no longer
+        match the device: invalidate them before re-raising, so fetch reads the device."""
+        try:
+            fn(*args)
+        except BaseException:
+            self._gen += 1
+            raise
+
     def _upsert_locked(self, items, vecs: torch.Tensor) -> None:
         # device write first: if it raises, no id is registered (no zero rows behind live ids)
         rows = self._plan_rows(items)
-        self._set.upsert_rows(vecs, rows)
+        self._device_write(self._set.upsert_rows, vecs, rows)
         self._commit_rows(items, rows)
 
     def query(self, vector=None, top_k: int = 10, include_values: bool = False, include_metadata: bool = False,

@@ -82,14 +82,19 @@ def _prepare(files: Sequence[tuple]):
 
 def _embed_for(embedder, images, index):
     """The batch's vectors in the form ``Index.upsert_tensor`` takes: one device tensor, or with
-    an ``EmbedderPool`` the per-GPU slices, each image embedded on the GPU of the shard its new
-    row will live on (rows are taken in order from len(index), global row g on shard g % S), so
-    the vectors go from the embedding straight into that shard.  A concurrent ingest can shift
-    the rows; the index then copies the few vectors that landed elsewhere."""
+    an ``EmbedderPool`` the per-GPU slices.  A GPU-decoded image is embedded on the GPU that
+    decoded it (no 150 KB image crosses GPUs); a host-decoded one on the GPU of the shard its
+    new row will live on (rows are taken in order from len(index), global row g on shard g % S).
+    A vector whose shard is on another GPU is copied there by the index (3 KB, counted in
+    ``ShardSet.cross_device_rows``)."""
+    import torch
+
     from ..vit import EmbedderPool
 
     if isinstance(embedder, EmbedderPool):
-        assign = embedder.assign(len(images), base=len(index), shard_devices=getattr(index, "shard_devices", None))
+        plan = embedder.assign(len(images), base=len(index), shard_devices=getattr(index, "shard_devices", None))
+        here = embedder.assign_by_location(images)
+        assign = [h if isinstance(im, torch.Tensor) and im.is_cuda else p for im, h, p in zip(images, here, plan)]
         return [(pos, r) for pos, r, _ in embedder.embed_parts(images, normalized=False, assign=assign)]
     raw, _ = embedder.embed_images(images)
     return raw

@@ -27,6 +27,51 @@ import torch
 import torch.distributed as dist
 
 
+class RowCoverage:
+    """The local rows a shard holds, as sorted disjoint [lo, hi) runs.  ``prefix`` is the
+    gap-free count: rows [0, prefix) all hold data.  Rows past a gap are tracked but never
+    counted, so a row range with a hole (zero rows that would score 0 and come back as
+    matches for ids that do not exist) is never published."""
+
+    def __init__(self):
+        self.runs: list[list[int]] = []
+
+    def add(self, lo: int, hi: int) -> None:
+        if hi <= lo:
+            return
+        keep = []
+        for a, b in self.runs:
+            if b < lo or a > hi:  # disjoint and not touching
+                keep.append([a, b])
+            else:  # overlapping or adjacent: merged into [lo, hi)
+                lo, hi = min(lo, a), max(hi, b)
+        keep.append([lo, hi])
+        keep.sort()
+        self.runs = keep
+
+    def add_rows(self, rows: torch.Tensor) -> None:
+        """Every row in ``rows`` (any order, repeats allowed, host or device)."""
+        u = torch.unique(torch.as_tensor(rows).reshape(-1))
+        if u.numel() == 0:
+            return
+        lo, hi = int(u[0]), int(u[-1])
+        if hi - lo + 1 == u.numel():  # one contiguous run (the common case: no host copy of the rows)
+            self.add(lo, hi + 1)
+            return
+        v = u.cpu().tolist()
+        start = prev = v[0]
+        for x in v[1:]:
+            if x != prev + 1:
+                self.add(start, prev + 1)
+                start = x
+            prev = x
+        self.add(start, prev + 1)
+
+    @property
+    def prefix(self) -> int:
+        return self.runs[0][1] if self.runs and self.runs[0][0] == 0 else 0
+
+
 class ShardedIndex:
     def __init__(self, dim: int, dtype: str = "float16", capacity_per_rank: int = 1 << 20, group=None,
                  device=None, backend_factory: Callable | None = None, merge_fn: Callable | None = None,
@@ -53,7 +98,12 @@ class ShardedIndex:
             self.local.set_filter(filter)
         self.merge = merge_fn
         self.n_rows = 0  # global rows [0, n_rows) hold data (the same value on every rank)
-        self.written = 0  # local rows [0, written) of this rank's shard hold data (high-water mark)
+        self.coverage = RowCoverage()  # local rows of this rank's shard that hold data
+
+    @property
+    def written(self) -> int:
+        """Local rows [0, written) of this rank's shard hold data, with no gap."""
+        return self.coverage.prefix
 
     @property
     def n_local(self) -> int:
@@ -75,7 +125,7 @@ class ShardedIndex:
             idx = torch.nonzero(mine).reshape(-1)
             loc = torch.div(gr[idx], self.world, rounding_mode="floor")
             self.local.upsert_rows(vecs[idx.to(vecs.device)], loc)
-            self.written = max(self.written, int(loc.max()) + 1)
+            self.coverage.add_rows(loc)
         self.n_rows = max(self.n_rows, int(gr.max()) + 1)
         return int(mine.sum())
 
@@ -91,14 +141,14 @@ class ShardedIndex:
         if lo < 0 or hi >= self.capacity:
             raise ValueError(f"local rows [{lo}, {hi}] outside the shard's capacity {self.capacity}")
         self.local.upsert_rows(vecs, lr)
-        self.written = max(self.written, hi + 1)
+        self.coverage.add_rows(lr)
 
     def _rows_ok(self, n_rows: int) -> bool:
         return (n_rows - self.rank + self.world - 1) // self.world <= self.written if n_rows > self.rank else True
 
     def set_rows(self, n_rows: int) -> None:
         """Publish the global row count (the same value on every rank).  Raises if this rank's
-        part of [0, n_rows) reaches past the local rows it has written: those slots are
+        part of [0, n_rows) reaches past its gap-free written prefix: unwritten slots are
         zero rows that would score 0 and come back as matches with ids that do not exist."""
         n_rows = int(n_rows)
         if n_rows < 0 or not self._rows_ok(n_rows):
@@ -124,7 +174,7 @@ class ShardedIndex:
         """Synthetic shard (benchmarks): every rank fills n_local rows, so the index holds
         n_local * W global rows."""
         self.local.fill_random(seed, 0, n_local)
-        self.written = max(self.written, int(n_local))
+        self.coverage.add(0, int(n_local))
         self.n_rows = n_local * self.world
 
     def search(self, queries: torch.Tensor, k: int, **kw):
@@ -177,7 +227,8 @@ class ShardedIndex:
         self.n_rows = int(man["n_rows"])
         if self.n_local:
             self.local.import_rows(0, torch.from_numpy(rows), torch.from_numpy(norms))
-        self.written = self.n_local
+        self.coverage = RowCoverage()
+        self.coverage.add(0, self.n_local)
 
     def close(self) -> None:
         close = getattr(self.local, "close", None)

@@ -443,9 +443,30 @@ class EmbedderPool:
                 out.append((base + j) % D)
         return out
 
+    def assign_by_location(self, images: Sequence) -> list[int]:
+        """Member of each image: a device tensor goes to a member on the GPU it lives on (several
+        members there take turns), anything else round-robin — so a GPU-decoded image is embedded
+        where it was decoded and never crosses GPUs."""
+        by_dev: dict[int, list[int]] = {}
+        for i, m in enumerate(self.members):
+            by_dev.setdefault(m.device.index, []).append(i)
+        D = len(self.members)
+        turn: dict[int, int] = {}
+        out = []
+        for j, im in enumerate(images):
+            cands = by_dev.get(im.device.index) if isinstance(im, torch.Tensor) and im.is_cuda else None
+            if cands:
+                k = turn.get(im.device.index, 0)
+                turn[im.device.index] = k + 1
+                out.append(cands[k % len(cands)])
+            else:
+                out.append(j % D)
+        return out
+
     def embed_parts(self, images: Sequence, normalized: bool = True, assign: Sequence[int] | None = None):
         """[(positions, raw [m, H], normed [m, H] or None)] per member that got images, each on
-        its member's GPU (queued on that GPU's current stream; no host synchronisation)."""
+        its member's GPU (queued on that GPU's current stream; no host synchronisation).  Default
+        assignment round-robin; after ``decode_jpeg_for_embed`` pass ``assign_by_location``."""
         n = len(images)
         assign = list(assign) if assign is not None else self.assign(n)
         if len(assign) != n:
@@ -486,13 +507,45 @@ class EmbedderPool:
     def decode_jpeg(self, datas: Sequence[bytes]) -> list[torch.Tensor]:
         return self.members[0].decode_jpeg(datas)
 
-    def decode_jpeg_for_embed(self, datas: Sequence[bytes]) -> torch.Tensor:
-        """Decoded + resized on the first member's GPU (the host Huffman pass is the shared
-        cost; the slices move to their members inside embed_parts, 150 KB per image)."""
-        return self.members[0].decode_jpeg_for_embed(datas)
+    def decode_jpeg_for_embed(self, datas: Sequence[bytes], assign: Sequence[int] | None = None) -> list[torch.Tensor]:
+        """Per-image device u8 [S, S, 3] inputs (input order).  Each member decodes its share
+        (``assign``, default round-robin) on its own GPU — host Huffman, reconstruction and the
+        fused resize — concurrently with the others (the library splits its host Huffman workers
+        between concurrent calls), queued on the caller's current stream of that GPU.  An image
+        stays on the GPU that decoded it and ``embed_parts`` embeds it there: only its 768-float
+        vector ever crosses GPUs, not the 150 KB image."""
+        n = len(datas)
+        assign = list(assign) if assign is not None else self.assign(n)
+        if len(assign) != n:
+            raise ValueError("assign needs one member per image")
+        groups: dict[int, list[int]] = {}
+        for j, mi in enumerate(assign):
+            groups.setdefault(mi, []).append(j)
+        streams = {m.device.index: torch.cuda.current_stream(m.device) for m in self.members}
+
+        def work(item):
+            mi, pos = item
+            m = self.members[mi]
+            with torch.cuda.device(m.device), torch.cuda.stream(streams[m.device.index]):
+                return pos, m.decode_jpeg_for_embed([datas[j] for j in pos])
+
+        items = list(groups.items())
+        if len(items) == 1:
+            results = [work(items[0])]
+        else:
+            import concurrent.futures as cf
+
+            with cf.ThreadPoolExecutor(len(items)) as ex:
+                results = list(ex.map(work, items))
+        out: list = [None] * n
+        for pos, x in results:
+            for j, im in zip(pos, x.unbind(0)):
+                out[j] = im
+        return out
 
     def embed_jpeg(self, datas: Sequence[bytes]) -> list[list[float]]:
-        raw, _ = self.embed_images(list(self.decode_jpeg_for_embed(datas).unbind(0)))
+        ims = self.decode_jpeg_for_embed(datas)
+        raw, _ = self.embed_images(ims, assign=self.assign_by_location(ims))
         return raw.cpu().tolist()
 
     def preprocess(self, images_u8: torch.Tensor, stream=None) -> torch.Tensor:

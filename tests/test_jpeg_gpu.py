@@ -160,3 +160,30 @@ def test_fused_decode_embedding_equals_pil_path(cuda):
         ref, _ = m.embed(torch.from_numpy(pil_rgb(data).copy())[None])
         assert torch.equal(raw[i], ref[0].cpu())
     m.close()
+
+
+def test_decode_resized_band_and_two_pass_paths(J, cuda):
+    """The band kernel (every image's band fits in LDS: short bands for the larger downscales)
+    and the two-pass path (a batch holding a 17000-px row) are both bit-exact with PIL; the
+    two-pass path's scratch grows geometrically: ever larger batches reallocate
+    on fewer steps than they grow, and a second sweep allocates nothing."""
+    lib = import_pkg("_lib").load()
+    d = J.JpegDecoder(device=0, max_images=16, max_pixels=1 << 22)
+    band = [synthetic(640, 480, 51), synthetic(1024, 768, 52, subsampling=2), synthetic(300, 168, 53),
+            synthetic(224, 100, 54), synthetic(100, 224, 55, subsampling=1), synthetic(224, 224, 56)]
+    for x, data in zip(d.decode_resized(band, 224, 3), band):
+        assert np.array_equal(x.cpu().numpy(), _pil_resized(data))
+    for x, data in zip(d.decode_resized(band, 224, 2), band):
+        assert np.array_equal(x.cpu().numpy(), _pil_resized(data, 224, 2))
+    wide, small = synthetic(17000, 12, 57, subsampling=2), synthetic(300, 168, 58)
+    rises = []
+    for sweep in range(2):
+        for n in range(1, 9):
+            c0 = lib.rc_alloc_count()
+            got = d.decode_resized([wide] + [small] * (n - 1), 224, 3)
+            rises.append(lib.rc_alloc_count() > c0)
+            if sweep == 0 and n in (1, 8):
+                assert np.array_equal(got[0].cpu().numpy(), _pil_resized(wide))
+                assert np.array_equal(got[-1].cpu().numpy(), _pil_resized(wide if n == 1 else small))
+    assert sum(rises[:8]) <= 6 and not any(rises[8:]), rises
+    d.close()

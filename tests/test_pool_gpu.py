@@ -158,3 +158,48 @@ def test_index_parts_upsert_equals_tensor_upsert(cuda):
         b.upsert_tensor(ids, [(p0, v[p0])])  # positions not covered
     a.close()
     b.close()
+
+
+def test_pool_decodes_per_member(vitmod, sd2, cuda):
+    """decode_jpeg_for_embed on a pool: each member decodes its share with its own decoder (not
+    everything through member 0), the images are bit-identical to one decoder's, and embedding
+    them where they were decoded equals the single embedder."""
+    import torch
+
+    pool = vitmod.EmbedderPool(sd2, [0, 0], max_batch=4)
+    single = vitmod.VitMsnEmbedder(sd2, device=0, max_batch=4)
+    datas = [d for _, d, _ in _jpegs(9, 11)]
+    ims = pool.decode_jpeg_for_embed(datas)
+    assert all(m._jpeg is not None for m in pool.members)  # both members decoded
+    ref = single.decode_jpeg_for_embed(datas)
+    assert len(ims) == 9 and all(torch.equal(a, b) for a, b in zip(ims, ref.unbind(0)))
+    raw, _ = pool.embed_images(ims, assign=pool.assign_by_location(ims))
+    want, _ = single.embed(ref, normalized=False)
+    assert torch.equal(raw, want)
+    assert pool.embed_jpeg(datas) == single.embed_jpeg(datas)
+    pool.close()
+    single.close()
+
+
+def test_pool_concurrent_ingests_store_their_own_vectors(service_pool, cuda):
+    """Two ingest_many calls racing on one pool and one index (the row plan is made
+    outside the index lock): every id ends up with exactly the vector of its own image."""
+    import concurrent.futures as cf
+
+    core = import_pkg("ingesting.core")
+    index = import_pkg("index")
+    emb = service_pool
+    a, b = _jpegs(12, 21), _jpegs(12, 22)
+    ix = index.Index("pool-race", dimension=768, capacity=64, device=cuda, shards=2)
+    with cf.ThreadPoolExecutor(2) as ex:
+        fa = ex.submit(core.ingest_many, a, ix, None, (lambda c=itertools.count(): f"a-{next(c)}"))
+        fb = ex.submit(core.ingest_many, b, ix, None, (lambda c=itertools.count(): f"b-{next(c)}"))
+        ra, rb = fa.result(), fb.result()
+    assert len(ix) == 24
+    for files, resp in ((a, ra), (b, rb)):
+        want = emb.embed_many([f[1] for f in files])
+        got = ix.fetch([r["file_id"] for r in resp])["vectors"]
+        for r, w in zip(resp, want):
+            assert np.allclose(got[r["file_id"]]["values"], w, rtol=1e-5, atol=1e-6)
+    assert ix.shard_set.cross_device_rows == 0  # one GPU: nothing crossed
+    ix.close()

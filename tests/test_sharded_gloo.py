@@ -182,3 +182,29 @@ def test_rank_local_ingest_publishes_consistent_rows(world, counts):
         assert errors == ["capacity", "set_rows"]
         assert np.array_equal(r, ref_r)
         assert np.allclose(s, ref_s, atol=1e-6)
+
+
+def test_row_coverage_counts_only_the_gap_free_prefix():
+    """upsert_local of local rows 0-9 then 20-29 leaves a hole: written stays 10 and set_rows
+    refuses a range over the hole; filling 10-19 closes it (written was a high-water
+    mark that accepted the zero rows)."""
+    sharded = import_pkg("sharded")
+    cap, dim = 64, 8
+    idx = sharded.ShardedIndex(dim, capacity_per_rank=cap, backend_factory=lambda: OracleShard(dim, cap, 0, 1),
+                               merge_fn=cpu_merge)
+    X = torch.randn(40, dim)
+    idx.upsert_local(X[:10], torch.arange(10))
+    idx.upsert_local(X[20:30], torch.arange(20, 30))
+    assert idx.written == 10 and idx.coverage.runs == [[0, 10], [20, 30]]
+    with pytest.raises(ValueError):
+        idx.set_rows(30)
+    idx.set_rows(10)
+    idx.upsert_local(X[10:20], torch.tensor([19, 10, 11, 12, 13, 14, 15, 16, 17, 18]))
+    assert idx.written == 30 and idx.coverage.runs == [[0, 30]]
+    assert idx.publish_rows() == 30
+    idx.upsert_rows(X[:3], torch.tensor([35, 33, 33]))  # scattered, repeated rows
+    assert idx.coverage.runs == [[0, 30], [33, 34], [35, 36]] and idx.written == 30
+    cov = sharded.RowCoverage()
+    for lo, hi in [(5, 7), (0, 2), (2, 5), (9, 10)]:
+        cov.add(lo, hi)
+    assert cov.runs == [[0, 7], [9, 10]] and cov.prefix == 7
