@@ -117,6 +117,7 @@ SIGNATURES = {
     "rc_sharded_upsert": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "rc_sharded_fetch": (C.c_int, [_vp, _vp, _i64, _vp, _i32]),
     "rc_sharded_search": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _i32, _vp]),
+    "rc_sharded_query_host": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _i32, _vp, _vp, _vp]),
     "rc_index_timing": (C.c_int, [_vp, _i32]),
     "rc_index_timing_read": (C.c_int, [_vp, _pd, _pi64, _pd]),
     "rc_model_create": (C.c_int, [_i32, C.POINTER(VitConfig), C.POINTER(_vp)]),

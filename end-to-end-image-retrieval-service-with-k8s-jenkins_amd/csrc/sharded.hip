@@ -17,6 +17,7 @@
 // A multi-PROCESS deployment (one process per GPU) uses the same shard row map
 // with an RCCL all-gather instead (sharded.py).
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "index_common.h"
@@ -67,6 +68,12 @@ struct rc_sharded {
     std::vector<int64_t *> row_h;
     std::vector<float *> fo_h;     // [st_cap][dim] pinned host landing of fetched rows
     hipEvent_t ev_gather = nullptr;  // leader stream: the remote subsets are gathered
+    // host-in / host-out query (rc_sharded_query_host): its own leader stream, one pinned
+    // staging block and one device block, each laid out [queries | scores | rows | values]
+    hipStream_t qs = nullptr;
+    int64_t qh_bytes = 0;
+    uint8_t *qh = nullptr;  // pinned
+    uint8_t *qd = nullptr;  // leader device
 };
 
 namespace {
@@ -159,9 +166,49 @@ void ensure_staging(rc_sharded *h, int64_t m) {
 // rows of the global range [0, n_rows) that shard s holds
 int64_t shard_rows(const rc_sharded *h, int s, int64_t n_rows) { return n_rows > s ? (n_rows - s + h->n - 1) / h->n : 0; }
 
+void free_query(rc_sharded *h) {
+    DeviceScope dl(h->dev[0]);
+    hfree(h->qh);
+    dfree(h->qd);
+    h->qh = nullptr;
+    h->qd = nullptr;
+    h->qh_bytes = 0;
+}
+
+// offsets of the query block for nq queries, top-k, with or without values (16-B aligned parts)
+struct QueryLayout {
+    int64_t q, sc, rw, val, total;
+};
+QueryLayout query_layout(const rc_sharded *h, int nq, int k, bool values) {
+    auto al = [](int64_t b) { return (b + 15) & ~(int64_t)15; };
+    QueryLayout L;
+    L.q = 0;
+    L.sc = al((int64_t)nq * h->dim * 4);
+    L.rw = L.sc + al((int64_t)nq * k * 4);
+    L.val = L.rw + al((int64_t)nq * k * 8);
+    L.total = L.val + (values ? al((int64_t)nq * k * h->dim * 4) : 0);
+    return L;
+}
+
+void ensure_query(rc_sharded *h, int64_t bytes) {
+    if (bytes <= h->qh_bytes) return;
+    const int64_t b2 = std::max<int64_t>(bytes, 2 * h->qh_bytes);
+    RC_HIP(hipStreamSynchronize(h->qs));
+    free_query(h);
+    DeviceScope dl(h->dev[0]);
+    h->qh = (uint8_t *)hmalloc((size_t)b2);
+    h->qd = (uint8_t *)dmalloc((size_t)b2);
+    h->qh_bytes = b2;
+}
+
 void destroy(rc_sharded *h) {
     free_search(h);
     free_staging(h);
+    if (h->qs) {
+        free_query(h);
+        DeviceScope dl(h->dev[0]);
+        (void)hipStreamDestroy(h->qs);
+    }
     for (int s = 0; s < h->n; ++s) {
         DeviceScope ds(h->dev[s]);
         if (h->st[s]) (void)hipStreamDestroy(h->st[s]);
@@ -227,6 +274,7 @@ int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int6
             DeviceScope dl(h->dev[0]);
             for (int s = 0; s < n_shards; ++s) RC_HIP(hipEventCreateWithFlags(&h->ev_start[s], hipEventDisableTiming));
             RC_HIP(hipEventCreateWithFlags(&h->ev_gather, hipEventDisableTiming));
+            RC_HIP(hipStreamCreateWithFlags(&h->qs, hipStreamNonBlocking));
         } catch (...) {
             destroy(h);
             throw;
@@ -273,7 +321,12 @@ int rc_sharded_set_filter(rc_sharded *h, int kind) {
     return guard([&] {
         RC_REQUIRE(h, RC_ERR_INVALID, "null index");
         std::lock_guard<std::mutex> lk(h->mu);
-        for (int s = 0; s < h->n; ++s) check_status(rc_index_set_filter(h->shard[s], kind, h->st[s]));
+        try {
+            for (int s = 0; s < h->n; ++s) check_status(rc_index_set_filter(h->shard[s], kind, h->st[s]));
+        } catch (...) {  // all or nothing: a failed shard (e.g. no room for the int8 copy) rolls every shard back
+            for (int s = 0; s < h->n; ++s) (void)rc_index_set_filter(h->shard[s], RC_FILTER_NATIVE, h->st[s]);
+            throw;
+        }
     });
 }
 
@@ -341,13 +394,12 @@ int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t
     });
 }
 
-int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, int stored) {
-    return guard([&] {
-        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
-        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
-        if (n == 0) return;
-        RC_REQUIRE(rows && out, RC_ERR_INVALID, "null buffer");
-        std::lock_guard<std::mutex> lk(h->mu);
+}  // extern "C"
+
+namespace {
+
+// rc_sharded_fetch's body (caller holds h->mu)
+void fetch_locked(rc_sharded *h, const int64_t *rows, int64_t n, float *out, int stored) {
         std::vector<int64_t> cnt(h->n, 0);
         for (int64_t i = 0; i < n; ++i) {
             const int64_t g = rows[i];
@@ -383,19 +435,11 @@ int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, 
             for (int64_t j = 0; j < cnt[s]; ++j)
                 std::memcpy(out + h->idx_h[s][j] * h->dim, h->fo_h[s] + j * h->dim, (size_t)h->dim * sizeof(float));
         }
-    });
 }
 
-int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
-                      int64_t *out_rows, int mode, void *stream) {
-    return guard([&] {
-        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
-        RC_REQUIRE(nq >= 0, RC_ERR_INVALID, "negative query count");
-        RC_REQUIRE(k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "top_k must be in [1, 256]");
-        RC_REQUIRE(n_rows >= 0 && n_rows <= h->cap * h->n, RC_ERR_INVALID, "n_rows out of range");
-        if (nq == 0) return;
-        RC_REQUIRE(queries && scores && out_rows, RC_ERR_INVALID, "null buffer");
-        std::lock_guard<std::mutex> lk(h->mu);
+// rc_sharded_search's body (caller holds h->mu; device buffers on the leader, stream = leader stream)
+void search_locked(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores, int64_t *out_rows,
+                   int mode, void *stream) {
         hipStream_t ls = (hipStream_t)stream;
         if (h->n == 1) {
             check_status(rc_index_search_ex(h->shard[0], queries, nq, n_rows, k, scores, out_rows, mode, stream));
@@ -428,6 +472,88 @@ int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_row
         DeviceScope dl(h->dev[0]);
         for (int s = 0; s < h->n; ++s) RC_HIP(hipStreamWaitEvent(ls, h->ev_done[s], 0));
         check_status(rc_topk_merge(h->g_s, h->g_r, h->n, nq, k, k, scores, out_rows, stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, int stored) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(n >= 0, RC_ERR_INVALID, "negative count");
+        if (n == 0) return;
+        RC_REQUIRE(rows && out, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        fetch_locked(h, rows, n, out, stored);
+    });
+}
+
+int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
+                      int64_t *out_rows, int mode, void *stream) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(nq >= 0, RC_ERR_INVALID, "negative query count");
+        RC_REQUIRE(k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "top_k must be in [1, 256]");
+        RC_REQUIRE(n_rows >= 0 && n_rows <= h->cap * h->n, RC_ERR_INVALID, "n_rows out of range");
+        if (nq == 0) return;
+        RC_REQUIRE(queries && scores && out_rows, RC_ERR_INVALID, "null buffer");
+        std::lock_guard<std::mutex> lk(h->mu);
+        search_locked(h, queries, nq, n_rows, k, scores, out_rows, mode, stream);
+    });
+}
+
+int rc_sharded_query_host(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, int with_values,
+                          float *scores, int64_t *out_rows, float *values) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        RC_REQUIRE(nq >= 0, RC_ERR_INVALID, "negative query count");
+        RC_REQUIRE(k >= 1 && k <= RC_TOPK_MAX, RC_ERR_INVALID, "top_k must be in [1, 256]");
+        RC_REQUIRE(n_rows >= 0 && n_rows <= h->cap * h->n, RC_ERR_INVALID, "n_rows out of range");
+        if (nq == 0) return;
+        RC_REQUIRE(queries && scores && out_rows && (!with_values || values), RC_ERR_INVALID, "null buffer");
+        const int64_t nk = (int64_t)nq * k;
+        if (n_rows == 0) {  // an empty index: empty lists, no device work
+            std::fill(scores, scores + nk, -INFINITY);
+            std::fill(out_rows, out_rows + nk, (int64_t)-1);
+            return;
+        }
+        std::lock_guard<std::mutex> lk(h->mu);
+        // one shard: the matched rows' values are gathered on the device and come back in the
+        // same copy as the lists; several shards: values through the staged fetch afterwards
+        const bool dev_values = with_values && h->n == 1;
+        const QueryLayout L = query_layout(h, nq, k, dev_values);
+        ensure_query(h, L.total);
+        DeviceScope dl(h->dev[0]);
+        std::memcpy(h->qh + L.q, queries, (size_t)nq * h->dim * sizeof(float));
+        RC_HIP(hipMemcpyAsync(h->qd + L.q, h->qh + L.q, (size_t)nq * h->dim * sizeof(float), hipMemcpyHostToDevice, h->qs));
+        float *dsc = (float *)(h->qd + L.sc);
+        int64_t *drw = (int64_t *)(h->qd + L.rw);
+        search_locked(h, (const float *)(h->qd + L.q), nq, n_rows, k, dsc, drw, RC_SEARCH_AUTO, h->qs);
+        if (dev_values) check_status(rc_index_fetch(h->shard[0], drw, nk, (float *)(h->qd + L.val), h->qs));
+        RC_HIP(hipMemcpyAsync(h->qh + L.sc, h->qd + L.sc, (size_t)(L.total - L.sc), hipMemcpyDeviceToHost, h->qs));
+        RC_HIP(hipStreamSynchronize(h->qs));
+        std::memcpy(scores, h->qh + L.sc, (size_t)nk * sizeof(float));
+        std::memcpy(out_rows, h->qh + L.rw, (size_t)nk * sizeof(int64_t));
+        if (dev_values) {
+            std::memcpy(values, h->qh + L.val, (size_t)nk * h->dim * sizeof(float));
+        } else if (with_values) {
+            std::vector<int64_t> live;
+            std::vector<int64_t> at;
+            for (int64_t i = 0; i < nk; ++i)
+                if (out_rows[i] >= 0) {
+                    live.push_back(out_rows[i]);
+                    at.push_back(i);
+                } else {
+                    std::fill(values + i * h->dim, values + (i + 1) * h->dim, NAN);
+                }
+            if (!live.empty()) {
+                std::vector<float> tmp(live.size() * (size_t)h->dim);
+                fetch_locked(h, live.data(), (int64_t)live.size(), tmp.data(), 0);
+                for (size_t j = 0; j < live.size(); ++j)
+                    std::memcpy(values + at[j] * h->dim, tmp.data() + j * h->dim, (size_t)h->dim * sizeof(float));
+            }
+        }
     });
 }
 

@@ -19,6 +19,7 @@ import os
 import threading
 from typing import Any, Iterable, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -232,6 +233,20 @@ def _as_vector(values: Any, dim: int) -> list[float]:
     return vals
 
 
+def _as_vector_np(values: Any, dim: int) -> np.ndarray:
+    """``_as_vector`` as a C-contiguous f32 [1, dim] host array (the request path: no per-element
+    Python loop)."""
+    if isinstance(values, torch.Tensor):
+        a = values.detach().to(device="cpu", dtype=torch.float32).reshape(-1).numpy()
+    else:
+        a = np.asarray(values, dtype=np.float32).reshape(-1)
+    if a.shape[0] != dim:
+        raise ValueError(f"Vector dimension {a.shape[0]} does not match the dimension of the index {dim}")
+    if not a.any():
+        raise ValueError("Dense vectors must contain at least one non-zero value for the cosine metric")
+    return np.ascontiguousarray(a[None])
+
+
 class ShardSet:
     """One ``rc_sharded`` handle: ``n`` shards (``rc_index`` each) in this process.
 
@@ -260,6 +275,7 @@ class ShardSet:
         # batch whose planned rows shifted under a concurrent ingest): results stay exact,
         # this counts the extra xGMI traffic
         self.cross_device_rows = 0
+        self._qbufs: dict = {}  # query_host's reused host buffers per (nq, k, values)
         self._shards = []
         for sh in range(self.n):
             ih = _lib.C.c_void_p()
@@ -362,6 +378,25 @@ class ShardSet:
                 touched.add(d)
         for d in touched:
             torch.cuda.synchronize(d)
+
+    def query_host(self, q: np.ndarray, k: int, n_rows: int, with_values: bool):
+        """Host f32 [nq, dim] → host (scores [nq, k], global rows [nq, k], values [nq, k, dim] or
+        None): rc_sharded_query_host — one H2D copy, the search and the matched rows' gather, one
+        D2H copy, one synchronisation.  The arrays are this ShardSet's reused buffers: valid
+        until its next query_host call (the Index consumes them under its lock)."""
+        nq = int(q.shape[0])
+        key = (nq, int(k), bool(with_values))
+        bufs = self._qbufs.get(key)
+        if bufs is None:
+            if len(self._qbufs) > 16:
+                self._qbufs.clear()
+            bufs = (np.empty((nq, k), np.float32), np.empty((nq, k), np.int64),
+                    np.empty((nq, k, self.dim), np.float32) if with_values else None)
+            self._qbufs[key] = bufs
+        sc, rw, val = bufs
+        check(self.lib.rc_sharded_query_host(self.handle, q.ctypes.data, nq, int(n_rows), int(k), int(bool(with_values)),
+                                             sc.ctypes.data, rw.ctypes.data, val.ctypes.data if val is not None else None))
+        return sc, rw, val
 
     def fetch_rows(self, rows, stored: bool = False) -> torch.Tensor:
         """Host f32 [n, dim]: the upserted values (or, ``stored``, the normalised stored rows)."""
@@ -640,8 +675,8 @@ class Index:
                 if r is None:
                     return {"matches": [], "namespace": namespace}
                 vector = self._set.fetch_rows([r])[0]
-            q = torch.tensor([_as_vector(vector, self.dimension)], dtype=torch.float32)
-            res = self._query_locked(q, top_k, include_values, include_metadata)[0]
+            q = _as_vector_np(vector, self.dimension)
+            res = self._query_host_locked(q, top_k, include_values, include_metadata)[0]
         return {"matches": res, "namespace": namespace}
 
     def query_batch(self, vectors, top_k: int = 10, include_values: bool = False,
@@ -681,6 +716,34 @@ class Index:
                     m["values"] = vals[j]
                 if include_metadata:
                     m["metadata"] = dict(self._meta.get(self._ids[r], {}))
+                matches.append(m)
+            out.append(matches)
+        if include_values:
+            self._recent = (self._gen, recent)
+        return out
+
+    def _query_host_locked(self, q: np.ndarray, k: int, include_values: bool, include_metadata: bool) -> list[list[dict]]:
+        """The request path (a query or a few): ``ShardSet.query_host``, one library call, the
+        lists and (include_values) the matched rows' values come back together."""
+        n = len(self._ids)
+        if n == 0:
+            return [[] for _ in range(q.shape[0])]
+        sc, rw, val = self._set.query_host(q, k, n, include_values)
+        out = []
+        recent: dict[str, list[float]] = {}
+        ids, meta = self._ids, self._meta
+        for qi in range(q.shape[0]):
+            matches = []
+            for j, (s, r) in enumerate(zip(sc[qi].tolist(), rw[qi].tolist())):
+                if r < 0:
+                    continue
+                vid = ids[r]
+                m = {"id": vid, "score": s}
+                if include_values:
+                    m["values"] = v = val[qi, j].tolist()
+                    recent[vid] = v
+                if include_metadata:
+                    m["metadata"] = dict(meta.get(vid, {}))
                 matches.append(m)
             out.append(matches)
         if include_values:

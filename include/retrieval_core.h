@@ -204,7 +204,19 @@ int rc_sharded_fetch(rc_sharded *h, const int64_t *rows, int64_t n, float *out, 
  * leader-device [nq, k], identical to one rc_index holding the same rows. */
 int rc_sharded_search(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, float *scores,
                       int64_t *out_rows, int mode, void *stream);
-/* rc_index_set_filter on every shard. */
+/* replaces index.query(vector, top_k, include_values=True) on the request path —
+ * retriever/utils.py:62-64 (the call retriever/main.py:127-130 times).  Host in,
+ * host out: queries HOST f32 [nq, dim]; scores HOST f32 [nq, k], out_rows HOST i64
+ * [nq, k] (global rows, -1 past the index), values HOST f32 [nq, k, dim] (the
+ * upserted values of each match, NaN for -1 slots; only when with_values).  One
+ * H2D copy, the search, the matched rows' gather and ONE D2H copy on the index's
+ * own leader stream, then one synchronisation; no allocation once the staging
+ * has grown to the call's size.  Results equal rc_sharded_search +
+ * rc_sharded_fetch. */
+int rc_sharded_query_host(rc_sharded *h, const float *queries, int nq, int64_t n_rows, int k, int with_values,
+                          float *scores, int64_t *out_rows, float *values);
+/* rc_index_set_filter on every shard; all or nothing (a failure restores
+ * RC_FILTER_NATIVE on every shard). */
 int rc_sharded_set_filter(rc_sharded *h, int kind);
 
 /* ------------------------------------------------------------------------

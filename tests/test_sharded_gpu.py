@@ -234,9 +234,9 @@ def test_world2_real_shards_equal_single_index(idxmod, cuda, n):
 def test_search_image_steady_state_allocates_nothing_and_fetches_once(cuda, monkeypatch):
     """/search_image over a multi-shard index (reference retriever/main.py:104-169): once the
     workspaces exist, a request makes no device / pinned allocation in the library
-    (rc_alloc_count), and the search's include_values fetch (retriever/utils.py:62-64)
-    serves the handler's fetch(ids) (retriever/main.py:142): each row is read from the GPU
-    once per request."""
+    (rc_alloc_count), and the search's include_values (retriever/utils.py:62-64) comes back
+    with the query itself (one rc_sharded_query_host call per request) and serves the
+    handler's fetch(ids) (retriever/main.py:142): no second device read."""
     import io
 
     from fastapi.testclient import TestClient
@@ -260,18 +260,52 @@ def test_search_image_steady_state_allocates_nothing_and_fetches_once(cuda, monk
     for i, b in enumerate(blobs):
         ix.upsert([(f"img-{i}", main.get_feature_vector(b), {"gcs_path": f"images/img-{i}.png"})])
     client = TestClient(main.app)
-    fetches = []
-    real_fetch = idxmod.ShardSet.fetch_rows
+    fetches, queries = [], []
+    real_fetch, real_query = idxmod.ShardSet.fetch_rows, idxmod.ShardSet.query_host
     monkeypatch.setattr(idxmod.ShardSet, "fetch_rows",
                         lambda self, rows, stored=False: fetches.append(len(rows)) or real_fetch(self, rows, stored))
+    monkeypatch.setattr(idxmod.ShardSet, "query_host",
+                        lambda self, q, k, n, v: queries.append((k, v)) or real_query(self, q, k, n, v))
     first = client.post("/search_image", files={"file": ("q.png", blobs[2], "image/png")})
     assert first.status_code == 200 and first.json()[0].endswith("images/img-2.png")
     client.post("/search_image", files={"file": ("q.png", blobs[3], "image/png")})  # warm
     fetches.clear()
+    queries.clear()
     n0 = lib.rc_alloc_count()
     for b in blobs:
         r = client.post("/search_image", files={"file": ("q.png", b, "image/png")})
         assert r.status_code == 200 and len(r.json()) == 5
     assert lib.rc_alloc_count() == n0
-    assert fetches == [5] * len(blobs)  # one device fetch of the 5 matches per request
+    assert queries == [(5, True)] * len(blobs) and fetches == []  # values came with the query
     ix.close()
+
+
+@pytest.mark.parametrize("shards,n", [(1, 700), (3, 700), (1, 3), (3, 2)])
+def test_query_host_equals_search_plus_fetch(cuda, shards, n):
+    """rc_sharded_query_host (host in / host out, values gathered with the lists) returns what
+    rc_sharded_search + rc_sharded_fetch return, bit for bit, including indexes smaller than k
+    (-1 rows, NaN values) and an empty index; the Index query built on it matches too."""
+    import torch
+
+    idxmod = import_pkg("index")
+    ss = idxmod.ShardSet(96, dtype="float16", capacity_per_shard=512, devices=[0] * shards)
+    g = torch.Generator().manual_seed(n + shards)
+    X = torch.randn(n, 96, generator=g)
+    ss.upsert_rows(X, torch.arange(n))
+    q = torch.randn(4, 96, generator=g)
+    q[1] = X[n // 2]
+    for k in (1, 5, 17):
+        sc, rw, val = ss.query_host(q.numpy().copy(), k, n, True)
+        s_ref, r_ref = ss.search(q, k, n)
+        assert np.array_equal(sc, s_ref.cpu().numpy()) and np.array_equal(rw, r_ref.cpu().numpy())
+        for qi in range(4):
+            for j in range(k):
+                if rw[qi, j] < 0:
+                    assert np.isnan(val[qi, j]).all()
+                else:
+                    assert np.array_equal(val[qi, j], ss.fetch_rows([int(rw[qi, j])])[0].numpy())
+        sc2, rw2, v2 = ss.query_host(q.numpy().copy(), k, n, False)
+        assert np.array_equal(sc2, sc) and np.array_equal(rw2, rw) and v2 is None
+    e_s, e_r, _ = ss.query_host(q.numpy().copy(), 3, 0, True)
+    assert np.isneginf(e_s).all() and (e_r == -1).all()
+    ss.close()
