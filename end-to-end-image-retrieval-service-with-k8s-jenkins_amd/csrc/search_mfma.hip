@@ -538,6 +538,21 @@ __global__ __launch_bounds__(64) void prepare_queries_i8_kernel(const float *__r
 // this tile's 4 scale loads while they are younger than the awaited step.
 // RT = rows per tile: 128, or 64 at ld 768 (NKT 6), where the 96 query-fragment registers
 // leave room for only half the accumulators.
+constexpr int I8_SL = 24;  // candidate rows staged in LDS per query per block (filter_i8_kernel)
+
+// LDS atomic add / store as inline asm: written in C++, hipcc cannot tell these words from the
+// LDS-DMA ring in the same __shared__ array and waits vmcnt(0) (the whole ring) before each one.
+// The add's own lgkmcnt(0) is inside the statement, so its result is ready when it ends; the
+// stores are retired by the block barrier before the flush reads them.
+__device__ __forceinline__ uint32_t lds_add_rtn_u32(uint32_t *p, uint32_t v) {
+    uint32_t r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"((uint32_t)(uintptr_t)p), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_write_u32(uint32_t *p, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)p), "v"(v) : "memory");
+}
+
 template <int NKT, int RT>
 __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     typedef int i32x4_t __attribute__((ext_vector_type(4)));
@@ -546,7 +561,13 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     constexpr int SPS = 2, SXL = 2 * RH;
     constexpr int PPW = 2 * RF / WAVES;
     static_assert((RT == 128 || RT == 64) && NKT % SPS == 0 && (QS_NS - 2 * SPS) * PPW + SXL < 64, "layout");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES];
+    // behind the ring (one __shared__ array): per query of the block a counter and I8_SL staged
+    // candidate rows, appended with LDS atomics (lgkmcnt only) and flushed to the global lists
+    // once at the block's end — a returning global atomic per append would wait for every
+    // older vector-memory op, i.e. drain the DMA ring (vmcnt(0)) in the middle of the K loop
+    __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES + SB_TILE * 4 * (1 + I8_SL)];
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(smem + QS_NS * STEP_BYTES);
+    uint32_t *lbuf = lcnt + SB_TILE;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -564,6 +585,7 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     const int nsteps = ntiles * NKT;
     const int64_t row0 = a.r_begin + rt0 * RT;  // a multiple of RT (host check)
     const uint8_t *Rg = (const uint8_t *)a.rows + row0 * ldb;
+    if (tid < SB_TILE) lcnt[tid] = 0u;  // visible to every wave after the K loop's first barrier
 
     i32x4_t qf[QT][2 * NKT];  // bytes [64 kk + 16 g, +16) of query q0 + 16 qt + li
     const int q0 = qb * SB_TILE + wave * 16 * QT;
@@ -701,13 +723,30 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
                         const int64_t row = rbase + rf * 16;
                         const float v = fmaf(ex[rf], aq[qt][j], sq[qt][j] * (sx[rf] * (float)acc[rf][qt][j]));
                         if (v >= thr[qt][j] && row < a.r_end) {
-                            const uint32_t pos = atomicAdd(&a.cnt[q], 1u);
-                            if ((int)pos < a.cap) a.cand[(int64_t)q * a.cap + pos] = (uint32_t)row;
+                            const int ql = q - qb * SB_TILE;
+                            const uint32_t p = lds_add_rtn_u32(&lcnt[ql], 1u);
+                            if (p < (uint32_t)I8_SL) {
+                                lds_write_u32(&lbuf[ql * I8_SL + p], (uint32_t)row);
+                            } else {  // this block's slots of q are full: straight to the global list
+                                const uint32_t pos = atomicAdd(&a.cnt[q], 1u);
+                                if ((int)pos < a.cap) a.cand[(int64_t)q * a.cap + pos] = (uint32_t)row;
+                            }
                         }
                     }
                 }
         }
         load_scales(min(tile + 1, ntiles - 1));  // unconditional: the same wait counts on every path
+    }
+    // flush the staged candidates: one global atomic per query that has any
+    __syncthreads();
+    if (tid < SB_TILE) {
+        const uint32_t n = min(lcnt[tid], (uint32_t)I8_SL);
+        if (n) {
+            const int q = qb * SB_TILE + tid;
+            const uint32_t base = atomicAdd(&a.cnt[q], n);
+            for (uint32_t i = 0; i < n; ++i)
+                if (base + i < (uint32_t)a.cap) a.cand[(int64_t)q * a.cap + base + i] = lbuf[tid * I8_SL + i];
+        }
     }
 }
 

@@ -125,10 +125,12 @@ def test_mfma_f32_index_rejected(idxmod, cuda):
 
 def test_config4_shard_full_size_properties(idxmod, cuda):
     """Config 4 at its real per-GPU workload: one 125M x 512 fp16 shard (1B rows over 8 GPUs),
-    1024 queries, top-100, batched MFMA path.  Size-independent properties: planted exact hits
-    come back first at score ||x̂||; results sorted; a query sample is bit-identical to the exact
-    scan; and on a random row sample the float64 oracle finds no row that beats the returned
-    kth score without being returned (with the returned rows' scores matching the oracle)."""
+    1024 queries, top-100, batched MFMA path with the f16 filter and with the int8 filter copy
+    (the bench's headline).  Size-independent properties: planted exact hits come back first at
+    score ||x̂||; results sorted; a query sample is bit-identical to the exact scan, and the
+    int8-filter results to the f16-filter ones; and on a random row sample the float64 oracle
+    finds no row that beats the returned kth score without being returned (with the returned
+    rows' scores matching the oracle)."""
     import torch
 
     n, dim, nq, k = 125_000_000, 512, 1024, 100
@@ -146,6 +148,12 @@ def test_config4_shard_full_size_properties(idxmod, cuda):
     sel = torch.tensor([0, 5, 511, 512, 1023])
     s2, r2 = dev.search(Q[sel], k, n, mode="scan")
     assert torch.equal(r[sel.cuda()], r2) and torch.equal(s[sel.cuda()], s2)
+    # the int8 filter copy at this size (64.5 GB beside the 128 GB of f16 rows): the batched
+    # search must return the f16 filter's results bit for bit (both rescore on the stored rows)
+    dev.set_filter("i8")
+    s8, r8 = dev.search(Q, k, n, mode="mfma")
+    assert torch.equal(r8, r) and torch.equal(s8, s)
+    dev.set_filter("native")
     # row-sample oracle check (float64 numpy on host over 262144 random stored rows)
     rng = np.random.default_rng(0)
     sample = np.unique(rng.integers(0, n, 1 << 18))
