@@ -551,6 +551,25 @@ def main():
     att_ms, att_n, _ = model.timing_read("attention")
     model.timing(False)
     model.set_parts(args.parts)
+    # yardstick: the vendor library's plain GEMM on each shape (torch.mm -> hipBLASLt, random bf16
+    # operands, no epilogue; min over 3 rounds of 10); never on the product path
+    for role, (gm, gn, gk, _) in shapes.items():
+        gv = torch.Generator(device=dev).manual_seed(7)
+        Av = (torch.rand(gm, gk, device=dev, generator=gv) * 2 - 1).to(torch.bfloat16)
+        Wv = ((torch.rand(gn, gk, device=dev, generator=gv) * 2 - 1) * 0.05).to(torch.bfloat16)
+        best = float("inf")
+        for _ in range(3):
+            torch.mm(Av, Wv.t())
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                torch.mm(Av, Wv.t())
+            e1.record()
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1) / 10)
+        gemms[role]["vendor_ms"] = best
+        gemms[role]["vs_vendor"] = gemms[role]["avg_launch_ms"] / best
+        del Av, Wv
     dominant = max(gemms, key=lambda r: gemms[r]["ms_per_step"])
     dom = gemms[dominant]
     gemm_step_ms = sum(g["ms_per_step"] for g in gemms.values())

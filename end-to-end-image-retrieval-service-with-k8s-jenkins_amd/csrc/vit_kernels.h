@@ -410,7 +410,7 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 template <int TOK>
 __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
                                                           int tokens_rt, int heads, float scale_log2e) {
-    constexpr int HD = 64;
+    constexpr int HD = 64, PPW = ATT2_TILES * 2 / 2;  // 13 DMA pieces per wave
     const int tokens = TOK > 0 ? TOK : tokens_rt;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];
     uint8_t *Ks = lds, *Vs = lds + ATT2_ROWS * 128;
@@ -420,8 +420,28 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD;
 
-    // 26 pieces of 1 KB for K and 26 for V; wave w issues pieces w, w+4, ...
-    for (int piece = wave; piece < 2 * ATT2_TILES * 2; piece += 4) {
+    const int g = lane >> 4, li = lane & 15;
+    const int nqt = (tokens + 15) / 16;
+    // Q of a query tile: 2 x 16 B per lane, as inline asm — beside LDS-DMA, hipcc waits vmcnt(0)
+    // (every DMA, and in the loop the loads just issued) before the first use of a plain load;
+    // the counted waits below are exact (every load here is waited for by an explicit vmcnt)
+    auto load_q = [&](int qt, bf16x8 (&qv)[2]) {
+        const int q = qt * 16 + li;
+        const uint16_t *qp = base + (int64_t)(q < tokens ? q : tokens - 1) * H3 + g * 8;
+        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:64"
+                     : "=&v"(qv[0]), "=&v"(qv[1])
+                     : "v"(qp)
+                     : "memory");
+    };
+    // the first query tile's Q (older than every DMA below), then 13 pieces of 1 KB per wave:
+    // waves 0-1 stage K (pieces 0-25), waves 2-3 stage V (26-51).  K is waited for before the
+    // scores, V only before the first P·V: V's transfer runs under the first tile's QKᵀ and
+    // softmax (one block's load is no longer one serial phase ahead of its math).
+    bf16x8 qf[2];
+    load_q(wave < nqt ? wave : 0, qf);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int piece = wave * PPW + i;
         const bool isv = piece >= ATT2_TILES * 2;
         const int r = (isv ? piece - ATT2_TILES * 2 : piece) * 8 + (lane >> 3);
         const int pc = lane & 7;
@@ -430,27 +450,21 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
         const uint16_t *src = base + (int64_t)rr * H3 + (isv ? 2 * H : H) + c * 8;
         __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(lds + piece * 1024), 16, 0, 0);
     }
-
-    const int g = lane >> 4, li = lane & 15;
-    const int nqt = (tokens + 15) / 16;
-    auto load_q = [&](int qt, bf16x8 (&qf)[2]) {
-        const int q = qt * 16 + li;
-        const int qc = q < tokens ? q : tokens - 1;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) qf[s] = *reinterpret_cast<const bf16x8 *>(base + (int64_t)qc * H3 + s * 32 + g * 8);
+    auto bar = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     };
-    bf16x8 qf[2];
-    load_q(wave < nqt ? wave : 0, qf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (wave < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K staged (and Q)
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");  // Q only: V may fly
+    bar();
+    __builtin_amdgcn_sched_barrier(0);  // nothing that reads qf moves above the wait
 
     const int qq = li >> 2, pp = li & 3;
-    for (int qt = wave; qt < nqt; qt += 4) {
-        bf16x8 qn[2];
-        const bool has_next = qt + 4 < nqt;
-        if (has_next) load_q(qt + 4, qn);  // prefetch the next tile's queries
-
-        f32x4 st[ATT2_TILES];
+    f32x4 st[ATT2_TILES];
+    float sum = 0.f;
+    // scores + softmax of query tile qt (K in LDS): st = p, sum = Σp
+    auto scores = [&](const bf16x8 (&qf)[2]) {
 #pragma unroll
         for (int t = 0; t < ATT2_TILES; ++t) {
             st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -480,7 +494,7 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
         mx = fmaxf(mx, __shfl_xor(mx, 16));
         mx = fmaxf(mx, __shfl_xor(mx, 32));
         const float nmc = -mx * scale_log2e;
-        float sum = 0.f;
+        sum = 0.f;
 #pragma unroll
         for (int t = 0; t < ATT2_TILES; ++t)
 #pragma unroll
@@ -491,7 +505,9 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
             }
         sum += __shfl_xor(sum, 16);
         sum += __shfl_xor(sum, 32);
-
+    };
+    // O = P·V of query tile qt (V in LDS), normalised and stored
+    auto pv_store = [&](int qt) {
         f32x4 o[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -538,10 +554,26 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
                 *reinterpret_cast<uint2 *>(orow + d * 16 + g * 4) =
                     make_uint2(pack_bf16x2(o[d][0] * inv, o[d][1] * inv), pack_bf16x2(o[d][2] * inv, o[d][3] * inv));
         }
-        if (has_next) {
-            qf[0] = qn[0];
-            qf[1] = qn[1];
-        }
+    };
+
+    // first tile: scores while V lands, then every wave waits for V once
+    const bool first = wave < nqt;
+    bf16x8 qn[2];
+    if (first && wave + 4 < nqt) load_q(wave + 4, qn);  // the next tile's queries, under the scores
+    if (first) scores(qf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V staged (waves 2-3), qn landed
+    bar();
+    __builtin_amdgcn_sched_barrier(0);
+    if (first) pv_store(wave);
+    for (int qt = wave + 4; qt < nqt; qt += 4) {
+        // qn (issued a tile ago) has landed; the previous tile's 4 output stores may still fly
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        qf[0] = qn[0];
+        qf[1] = qn[1];
+        if (qt + 4 < nqt) load_q(qt + 4, qn);  // prefetch the next tile's queries
+        scores(qf);
+        pv_store(qt);
     }
 }
 

@@ -9,6 +9,9 @@
 //  variant 3: 4 waves, one per SIMD, 128x128 outputs per wave, one barrier per K-step,
 //             the next K-tile's LDS-DMA interleaved with this one's MFMAs
 //  variant 4: 0 with the LDS-DMA as buffer loads (one lane offset, scalar row offsets)
+//  variant 5: 3 at BK = 32 in a 4-slot ring, three steps in flight, one barrier per step
+//  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
+//             wrong results, timing only)
 // Every variant accumulates each output over K in the same order (chunks of 32, k
 // ascending), so their results are bit-identical.
 #include <hip/hip_runtime.h>
@@ -60,6 +63,7 @@ constexpr int PP_STAGE = 2 * 256 * 64 * 2;  // A tile then W tile, 32 KB each
 template <int VAR>
 __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
     constexpr bool STAMP = VAR == 1, WKEEP = VAR == 2, BUF = VAR == 4;
+    constexpr bool NO_DMA = (VAR & 16) != 0, NO_READ = (VAR & 32) != 0, NO_MFMA = (VAR & 64) != 0;
     constexpr int A_BYTES = 256 * 64 * 2;
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + (STAMP ? 8192 : 0)];
     int tm, tn;
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
         for (int p = 0; p < 4; ++p) {
             const int mq = p >> 1;
             const int nq = (p == 1 || p == 2);
-            if (p == 0 || p == 2) {
+            if ((p == 0 || p == 2) && !(NO_READ && kt > 0)) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
                         af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                     }
             }
-            const bool wread = WKEEP ? (p == 0 || p == 1) : true;
+            const bool wread = (WKEEP ? (p == 0 || p == 1) : true) && !(NO_READ && kt > 0);
             if (wread) {
 #pragma unroll
                 for (int ni = 0; ni < 2; ++ni)
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
                         wf[WKEEP ? nq : 0][ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                     }
             }
-            if (more && p < 2) stage4(cur ^ 1, (kt + 1) * 64, p * 4);
+            if (more && p < 2 && !NO_DMA) stage4(cur ^ 1, (kt + 1) * 64, p * 4);
             if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             bar();
@@ -164,8 +168,11 @@ __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int ni = 0; ni < 2; ++ni)
-                        acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[WKEEP ? nq : 0][ni][s], af[mi][s],
-                                                                                     acc[mq][nq][mi][ni], 0, 0, 0);
+                        if constexpr (NO_MFMA)
+                            asm volatile("" ::"v"(wf[WKEEP ? nq : 0][ni][s]), "v"(af[mi][s]));
+                        else
+                            acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                wf[WKEEP ? nq : 0][ni][s], af[mi][s], acc[mq][nq][mi][ni], 0, 0, 0);
             __builtin_amdgcn_s_setprio(0);
             bar();
             stamp();
@@ -284,6 +291,82 @@ __global__ __launch_bounds__(256, 1) void lab_w4(LabArgs a) {
         }
 }
 
+
+// --------------------------------- 4 waves, 128x128 per wave, BK = 32, 4-slot ring
+// Slot = A[256][32] + W[256][32] bf16 (32 KB, 64-B rows, chunk c of row r at c ^ ((r >> 3) & 1) << 1:
+// conflict-free ds_read_b128 fragments, gemm_ring_kernel's image).  Steps t+1..t+2 stay in flight
+// while step t computes; step t+3 is issued into the slot step t-1 used, after the barrier that
+// closes every wave's reads of it.  One barrier per 32-deep step, counted vmcnt (never 0 in the
+// loop); the DMA is issued for every step (past the end: a clamped, unused re-read), so the
+// counts hold on every path.
+__global__ __launch_bounds__(256, 1) void lab_w4r(LabArgs a) {
+    constexpr int NS = 4, SLOT = 2 * 256 * 32 * 2, A_BYTES = 256 * 32 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NS * SLOT];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 32;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+    // piece p (1 KB = 16 rows x 64 B): A rows 16p.. for p < 16, W rows 16(p-16).. after; wave w
+    // issues p = w + 4 i, i = 0..7 (i < 4: A).  Lane l writes row l >> 2, stored chunk l & 3 =
+    // source chunk (l & 3) ^ (((l >> 5) & 1) << 1): one lane offset for every piece.
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    const uint32_t voff = (uint32_t)((16 * wave + prow) * K + pchunk * 8) * 2u;
+    auto issue = [&](int t) {
+        const int tc = t < nk ? t : nk - 1;
+        uint8_t *base = smem + (t % NS) * SLOT;
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)(Ag + tc * 32), (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)(Wg + tc * 32), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 4 ? ra : rw, (lds_void_t *)(base + (wave + 4 * i) * 1024), 16, voff,
+                                                     (i & 3) * 64 * K * 2, 0, 0);
+    };
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    issue(0);
+    issue(1);
+    issue(2);
+#pragma nounroll
+    for (int t = 0; t < nk; ++t) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this wave's step t landed (t+1, t+2 fly)
+        bar();
+        issue(t + 3);
+        const uint8_t *As = smem + (t % NS) * SLOT;
+        const uint8_t *Ws = As + A_BYTES;
+        bf16x8 af[8], wf[8];
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + (wc * 128 + ni * 16 + li) * 64 + fchunk);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(As + (wr * 128 + mi * 16 + li) * 64 + fchunk);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail re-reads
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int row = m0 + wr * 128 + mi * 16 + li;
+            const int col = n0 + wc * 128 + ni * 16 + 4 * g;
+            const f32x4 v = acc[mi][ni];
+            if (row < a.M)
+                *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+}
+
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
                         uint64_t *stamps, hipStream_t s) {
     if (N % 256 || K % 64) return 1;
@@ -295,6 +378,11 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 2: hipLaunchKernelGGL(lab_pp<2>, dim3(tiles), dim3(512), 0, s, a); break;
         case 3: hipLaunchKernelGGL(lab_w4, dim3(tiles), dim3(256), 0, s, a); break;
         case 4: hipLaunchKernelGGL(lab_pp<4>, dim3(tiles), dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(lab_w4r, dim3(tiles), dim3(256), 0, s, a); break;
+        case 16: hipLaunchKernelGGL(lab_pp<16>, dim3(tiles), dim3(512), 0, s, a); break;   // ablation: no DMA in the loop
+        case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
+        case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers
+        case 64: hipLaunchKernelGGL(lab_pp<64>, dim3(tiles), dim3(512), 0, s, a); break;   // no MFMA
         default: return 2;
     }
     return hipGetLastError() == hipSuccess ? 0 : 3;

@@ -19,7 +19,7 @@ SHAPES = {"qkv": (2304, 768), "o": (768, 768), "fc1": (3072, 768), "fc2": (768, 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,2,3,4")
+    ap.add_argument("--variants", default="0,2,3,4,5,16,32,48,64")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--stamps", action="store_true")
@@ -68,7 +68,7 @@ def main():
         res = {k: {"us_min": round(min(t), 2), "us_med": round(sorted(t)[len(t) // 2], 2),
                    "TFLOPs": round(flops / (min(t) * 1e-6) / 1e12, 1)} for k, t in times.items()}
         res["check"] = {"v%d_vs_torch_max_rel" % v0: err,
-                        "bit_identical": {f"v{v}": bool(torch.equal(Cs[v], Cs[v0])) for v in variants}}
+                        "bit_identical": {f"v{v}": bool(torch.equal(Cs[v], Cs[v0])) for v in variants if v < 16}}
         print(name, json.dumps(res), flush=True)
         out[name] = res
         if args.stamps:
