@@ -46,6 +46,10 @@ struct rc_sharded {
     int n = 0, dim = 0, dtype = 0;
     int64_t cap = 0;  // rows per shard
     std::vector<int> dev;
+    // shard s is driven through the cross-device path (peer copies to / from the leader):
+    // dev[s] != dev[0], or every shard s > 0 when RC_SHARDED_FORCE_REMOTE=1 at create (a test
+    // hook: the 8-GPU code path — gather, peer copies, leader merge — exercised on one GPU)
+    std::vector<char> remote;
     std::vector<rc_index *> shard;
     std::vector<hipStream_t> st;
     std::vector<hipEvent_t> ev_done;   // per shard, recorded on st[s]
@@ -101,7 +105,7 @@ void ensure_search(rc_sharded *h, int nq, int k) {
     const int nq2 = std::max(nq, h->nq_cap), k2 = std::max(k, h->k_cap);
     free_search(h);
     for (int s = 0; s < h->n; ++s) {
-        if (h->dev[s] == h->dev[0]) continue;
+        if (!h->remote[s]) continue;
         DeviceScope ds(h->dev[s]);
         h->q[s] = (float *)dmalloc((size_t)nq2 * h->dim * sizeof(float));
         h->s_loc[s] = (float *)dmalloc((size_t)nq2 * k2 * sizeof(float));
@@ -146,7 +150,7 @@ void ensure_staging(rc_sharded *h, int64_t m) {
     free_staging(h);
     const size_t vb = (size_t)m2 * h->dim * sizeof(float);
     for (int s = 0; s < h->n; ++s) {
-        const bool remote = h->dev[s] != h->dev[0];
+        const bool remote = h->remote[s];
         {
             DeviceScope ds(h->dev[s]);
             h->row_d[s] = (int64_t *)dmalloc((size_t)m2 * sizeof(int64_t));
@@ -243,6 +247,10 @@ int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int6
         h->dtype = dtype;
         h->cap = capacity_per_shard;
         h->dev.assign(devices, devices + n_shards);
+        const char *fr = std::getenv("RC_SHARDED_FORCE_REMOTE");
+        const bool force_remote = fr && fr[0] == '1';
+        h->remote.assign(n_shards, 0);
+        for (int s = 1; s < n_shards; ++s) h->remote[s] = (devices[s] != devices[0] || force_remote) ? 1 : 0;
         h->shard.assign(n_shards, nullptr);
         h->st.assign(n_shards, nullptr);
         h->ev_done.assign(n_shards, nullptr);
@@ -362,7 +370,7 @@ int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t
             for (int s = 0; s < h->n; ++s) {
                 if (cnt[s] == 0) continue;
                 RC_HIP(hipMemcpyAsync(h->idx_d[s], h->idx_h[s], cnt[s] * sizeof(int64_t), hipMemcpyHostToDevice, ls));
-                if (h->dev[s] != h->dev[0]) {
+                if (h->remote[s]) {
                     hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((cnt[s] + 3) / 4)), dim3(256), 0, ls, vecs,
                                        h->idx_d[s], cnt[s], h->dim, h->gat_d[s]);
                     RC_LAUNCH_CHECK();
@@ -376,7 +384,7 @@ int rc_sharded_upsert(rc_sharded *h, const float *vecs, int64_t n, const int64_t
             const int64_t ms = cnt[s];
             RC_HIP(hipStreamWaitEvent(h->st[s], h->ev_gather, 0));
             RC_HIP(hipMemcpyAsync(h->row_d[s], h->row_h[s], ms * sizeof(int64_t), hipMemcpyHostToDevice, h->st[s]));
-            if (h->dev[s] != h->dev[0]) {
+            if (h->remote[s]) {
                 RC_HIP(hipMemcpyPeerAsync(h->vec_d[s], h->dev[s], h->gat_d[s], h->dev[0], (size_t)ms * h->dim * sizeof(float),
                                           h->st[s]));
                 index_upsert_gather(h->shard[s], h->vec_d[s], nullptr, ms, h->row_d[s], h->st[s]);
@@ -454,7 +462,7 @@ void search_locked(rc_sharded *h, const float *queries, int nq, int64_t n_rows, 
         for (int s = 0; s < h->n; ++s) {
             DeviceScope ds(h->dev[s]);
             RC_HIP(hipStreamWaitEvent(h->st[s], h->ev_start[s], 0));
-            const bool local = h->dev[s] == h->dev[0];
+            const bool local = !h->remote[s];
             const float *q = queries;
             if (!local) {
                 RC_HIP(hipMemcpyPeerAsync(h->q[s], h->dev[s], queries, h->dev[0], (size_t)nq * h->dim * sizeof(float), h->st[s]));

@@ -33,12 +33,20 @@ def _items(rng, n, dim, prefix="v", start=0):
                for i in range(n)]
 
 
-@pytest.mark.parametrize("dtype,shards", [("float32", 3), ("float16", 4), ("bfloat16", 2)])
-def test_sharded_index_equals_single_shard(idxmod, cuda, dtype, shards):
+@pytest.mark.parametrize("dtype,shards,remote", [("float32", 3, False), ("float16", 4, False), ("bfloat16", 2, False),
+                                                 ("float16", 3, True), ("float32", 4, True)])
+def test_sharded_index_equals_single_shard(idxmod, cuda, dtype, shards, remote, monkeypatch):
+    """A multi-shard index answers exactly like one shard.  remote: every shard but the leader
+    is driven through the cross-device path (RC_SHARDED_FORCE_REMOTE: subset gather on the
+    leader, peer copies of queries / subsets / result lists, leader merge) — the code the
+    8-GPU node runs, exercised on one GPU."""
     rng = np.random.default_rng(7)
     dim = 768
     one = idxmod.Index("one", dimension=dim, dtype=dtype, capacity=512, device=cuda)
+    if remote:
+        monkeypatch.setenv("RC_SHARDED_FORCE_REMOTE", "1")
     many = idxmod.Index("many", dimension=dim, dtype=dtype, capacity=512, device=cuda, shards=shards)
+    monkeypatch.delenv("RC_SHARDED_FORCE_REMOTE", raising=False)
     X, items = _items(rng, 3000, dim)
     X[1001] = X[17]  # exact ties on different shards (17 % n != 1001 % n for n = 2, 3, 4)
     items[1001] = ("v1001", X[17].tolist(), items[1001][2])

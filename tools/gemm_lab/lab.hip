@@ -10,6 +10,7 @@
 //             the next K-tile's LDS-DMA interleaved with this one's MFMAs
 //  variant 4: 0 with the LDS-DMA as buffer loads (one lane offset, scalar row offsets)
 //  variant 5: 3 at BK = 32 in a 4-slot ring, three steps in flight, one barrier per step
+//  variant 6: ping-pong with 2 phases per K-step (32-MFMA segments, 4 barriers per step), W kept
 //  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
 //             wrong results, timing only)
 // Every variant accumulates each output over K in the same order (chunks of 32, k
@@ -367,6 +368,107 @@ __global__ __launch_bounds__(256, 1) void lab_w4r(LabArgs a) {
         }
 }
 
+
+// ------------------------------------- ping-pong, 2 phases per K-step, W kept
+// lab_pp with the K-step in 2 phases (one per 64-row half mq of the wave's 128 rows) instead of
+// 4: a C segment is 32 MFMAs (the half's 4 x 4 tiles x 2 k-halves), so a K-step has 4 barriers,
+// not 8.  M0 reads the half's A fragments (8) and the step's W fragments (8, kept for both
+// halves) and issues this wave's 8 DMA pieces of step t+1; M1 reads the other half's A (8) and
+// waits for this wave's pieces.  G1 runs one segment behind G0 (the stagger barrier), so the
+// buffer step t+1 goes to was last read in the segment before G0's M0(t) (G1's M1(t-1)).
+__global__ __launch_bounds__(512, 1) void lab_pp2(LabArgs a) {
+    constexpr int A_BYTES = 256 * 64 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 64;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+    const int lr = wave * 8 + (lane >> 3);
+    const uint32_t voff = (uint32_t)(lr * K + (((lane & 7) ^ ((lr >> 1) & 7)) << 3)) * 2u;
+    auto stage8 = [&](int buf, int k0) {
+        uint8_t *base = smem + buf * PP_STAGE;
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)(Ag + k0), (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)(Wg + k0), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 4 ? ra : rw, (lds_void_t *)(base + (wave + 8 * i) * 1024), 16, voff,
+                                                     (i & 3) * 64 * K * 2, 0, 0);
+    };
+    f32x4 acc[2][4][4];  // [mq][mi][ni]: rows grp*128 + mq*64 + mi*16, columns wc*64 + ni*16
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[i][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    stage8(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (grp == 1) bar();
+    bf16x8 af[4][2], wf[4][2];
+#pragma nounroll
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const uint8_t *As = smem + cur * PP_STAGE;
+        const uint8_t *Ws = As + A_BYTES;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int r = grp * 128 + p * 64 + mi * 16 + li;
+                    const int c = s * 4 + g;
+                    af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                }
+            if (p == 0) {
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = wc * 64 + ni * 16 + li;
+                        const int c = s * 4 + g;
+                        wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+                if (kt + 1 < nk) stage8(cur ^ 1, (kt + 1) * 64);
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni)
+                        acc[p][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], acc[p][mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+    }
+    if (grp == 0) bar();
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                const int col = n0 + wc * 64 + ni * 16 + 4 * g;
+                const f32x4 v = acc[mq][mi][ni];
+                if (row < a.M)
+                    *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+            }
+}
+
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
                         uint64_t *stamps, hipStream_t s) {
     if (N % 256 || K % 64) return 1;
@@ -379,6 +481,7 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 3: hipLaunchKernelGGL(lab_w4, dim3(tiles), dim3(256), 0, s, a); break;
         case 4: hipLaunchKernelGGL(lab_pp<4>, dim3(tiles), dim3(512), 0, s, a); break;
         case 5: hipLaunchKernelGGL(lab_w4r, dim3(tiles), dim3(256), 0, s, a); break;
+        case 6: hipLaunchKernelGGL(lab_pp2, dim3(tiles), dim3(512), 0, s, a); break;
         case 16: hipLaunchKernelGGL(lab_pp<16>, dim3(tiles), dim3(512), 0, s, a); break;   // ablation: no DMA in the loop
         case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
         case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers

@@ -19,7 +19,7 @@ SHAPES = {"qkv": (2304, 768), "o": (768, 768), "fc1": (3072, 768), "fc2": (768, 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,2,3,4,5,16,32,48,64")
+    ap.add_argument("--variants", default="0,2,3,4,5,6,16,32,48,64")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--stamps", action="store_true")
