@@ -741,7 +741,8 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
     {
         uint8_t *dst = r.need_h ? src : tmp;
         const int n = rows * W;
-        for (int idx = threadIdx.x; idx < n; idx += 256) {
+#pragma unroll 4
+        for (int idx = threadIdx.x; idx < n; idx += 256) {  // (unrolled: several pixels' plane loads in flight)
             const int rr = idx / W, x = idx - rr * W;
             int R, G, B;
             ycc_rgb(planes, d, x, r.y0 + lo + rr, R, G, B);
