@@ -28,6 +28,7 @@ struct LabArgs {
     uint16_t *C;
     int M, N, K;
     uint64_t *stamps;  // variant 1: [16 (block, group)][512]
+    int group_m;       // tile order: groups of group_m row tiles (column-major inside); -1 = auto
 };
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -44,8 +45,9 @@ __device__ __forceinline__ void tile_coords(const LabArgs &a, int BM, int BN, in
     const int ntn = a.N / BN, ntm = (a.M + BM - 1) / BM;
     tm = tile / ntn;
     tn = tile % ntn;
-    if (ntn >= 6) {
-        const int G = 8, gt = G * ntn, gi = tile / gt, in = tile - gi * gt;
+    const int G = a.group_m >= 0 ? a.group_m : (ntn >= 6 ? 8 : 0);
+    if (G > 0) {
+        const int gt = G * ntn, gi = tile / gt, in = tile - gi * gt;
         const int gm = min(G, ntm - gi * G);
         tm = gi * G + in % gm;
         tn = in / gm;
@@ -470,9 +472,9 @@ __global__ __launch_bounds__(512, 1) void lab_pp2(LabArgs a) {
 }
 
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
-                        uint64_t *stamps, hipStream_t s) {
+                        uint64_t *stamps, hipStream_t s, int group_m) {
     if (N % 256 || K % 64) return 1;
-    LabArgs a{A, W, C, M, N, K, stamps};
+    LabArgs a{A, W, C, M, N, K, stamps, group_m};
     const int tiles = ((M + 255) / 256) * (N / 256);
     switch (variant) {
         case 0: hipLaunchKernelGGL(lab_pp<0>, dim3(tiles), dim3(512), 0, s, a); break;

@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--shapes", default="qkv,o,fc1,fc2")
     ap.add_argument("--images", type=int, default=256)
+    ap.add_argument("--groups", default="", help="tile-order sweep for variant 0: group_m values, e.g. 0,2,4,8,16")
     args = ap.parse_args()
     lib = C.CDLL(os.path.join(HERE, "liblab.so"))
-    lib.lab_gemm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    lib.lab_gemm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                             C.c_int]
     dev = torch.device("cuda", 0)
     M = args.images * 197
     Mp = (M + 255) // 256 * 256
@@ -42,12 +44,14 @@ def main():
         Cs = {v: torch.zeros(M, N, dtype=torch.bfloat16, device=dev) for v in variants}
         s = torch.cuda.current_stream().cuda_stream
 
-        def run(v):
-            rc = lib.lab_gemm(v, A.data_ptr(), W.data_ptr(), Cs[v].data_ptr(), M, N, K, stamps.data_ptr(), s)
+        def run(v, grp=-1):
+            rc = lib.lab_gemm(v, A.data_ptr(), W.data_ptr(), Cs[v].data_ptr(), M, N, K, stamps.data_ptr(), s, grp)
             assert rc == 0, rc
 
         Am = A[:M]
         legs = {f"v{v}": (lambda v=v: run(v)) for v in variants}
+        for grp in [int(x) for x in args.groups.split(",") if x.strip()]:
+            legs[f"v{variants[0]}_g{grp}"] = lambda grp=grp: run(variants[0], grp)
         legs["vendor_mm"] = lambda: torch.mm(Am, W.t())
         times = {k: [] for k in legs}
         for _ in range(args.rounds):
@@ -72,7 +76,7 @@ def main():
         print(name, json.dumps(res), flush=True)
         out[name] = res
         if args.stamps:
-            lib.lab_gemm(1, A.data_ptr(), W.data_ptr(), Cs[v0].data_ptr(), M, N, K, stamps.data_ptr(), s)
+            lib.lab_gemm(1, A.data_ptr(), W.data_ptr(), Cs[v0].data_ptr(), M, N, K, stamps.data_ptr(), s, -1)
             torch.cuda.synchronize()
             st = stamps.view(16, 512).cpu()
             nk = K // 64

@@ -6,7 +6,7 @@ TAG=$1
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 300 python -u tools/gemm_lab/lab.py --stamps --rounds 3 > $O/lab.log 2>&1
+timeout -k 10 300 python -u tools/gemm_lab/lab.py --stamps --rounds 3 --groups 0,2,4,16 > $O/lab.log 2>&1
 echo "lab rc=$?"; tail -2 $O/lab.log | cut -c1-200
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
