@@ -421,9 +421,14 @@ __device__ __forceinline__ void pp_tile_coords(const GemmArgs &a, int tile, int 
 // described above gemm_pp_kernel.  smem: the 2-stage ring (2 * PP_STAGE) then, for the
 // LayerNorm-fold consumers, the tile rows' (rstd, -rstd*mu) at 2 * PP_STAGE.  On return
 // every wave has passed the loop's last barrier (the ring is free for the epilogue).
-template <int EPI, int ABL>
+// KL (K-loop form, bit-identical results): bit 0 = the wave's W fragments of a K-step are read
+// once and kept for both of its halves (24 LDS reads per wave per K-step instead of 32); bit 1 =
+// the LDS-DMA as buffer loads (one lane offset for all 8 pieces, the piece's rows in the scalar
+// offset, the K-step in the descriptor: no per-piece 64-bit address arithmetic).
+template <int EPI, int ABL, int KL = 0>
 __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m0, int n0, int kb, int ke,
                                          f32x4 (&acc)[2][2][4][2], int tid, int64_t sb = -1) {
+    constexpr bool WKEEP = (KL & 1) != 0, BUF = (KL & 2) != 0;
     constexpr int BM = PP_BM, BK = PP_BK, A_BYTES = BM * BK * 2, STAGE = PP_STAGE;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -433,17 +438,29 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
     const uint16_t *Ag = a.A + (int64_t)m0 * K;
     const uint16_t *Wg = a.W + (int64_t)n0 * K;
 
-    // 64 pieces of 1 KB per K-tile (A: 0-31, W: 32-63); wave w owns pieces w + 8 i.
+    // 64 pieces of 1 KB per K-tile (A: 0-31, W: 32-63); wave w owns pieces w + 8 i.  Piece rows
+    // r = 8 w + 64 (i % 4) + lane / 8: the chunk swizzle (r >> 1) & 7 does not depend on i.
+    const int lr = wave * 8 + (lane >> 3);
+    const uint32_t voff = (uint32_t)(lr * K + (((lane & 7) ^ ((lr >> 1) & 7)) << 3)) * 2u;
     auto stage4 = [&](int buf, int k0, int i0) {
         uint8_t *base = smem + buf * STAGE;
+        if constexpr (BUF) {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void *)((i0 < 4 ? Ag : Wg) + k0), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-        for (int i = i0; i < i0 + 4; ++i) {
-            const int piece = wave + 8 * i;
-            const bool is_a = i < 4;
-            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+            for (int i = i0; i < i0 + 4; ++i)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(base + (wave + 8 * i) * 1024), 16, voff,
+                                                         (i & 3) * 64 * K * 2, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i) {
+                const int piece = wave + 8 * i;
+                const bool is_a = i < 4;
+                const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
+                const int c = (lane & 7) ^ ((r >> 1) & 7);
+                const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
+                __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+            }
         }
     };
     auto bar = [] {
@@ -464,7 +481,7 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
     if (sb >= 0) RC_STAMP(sb, RC_NOW());
     if (grp == 1) bar();  // stagger: G1 one segment behind
 
-    bf16x8 af[4][2], wf[2][2];  // [mi][s], [ni][s]
+    bf16x8 af[4][2], wf[WKEEP ? 2 : 1][2][2];  // [mi][s], [nq (W kept) or 0][ni][s]
 #pragma nounroll
     for (int kt = kb; kt < ke; ++kt) {
         const int cur = (kt - kb) & 1;
@@ -486,14 +503,16 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
                         af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                     }
             }
+            if (!WKEEP || p < 2) {
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
+                for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const int r = wc * 64 + nq * 32 + ni * 16 + li;
-                    const int c = s * 4 + g;
-                    wf[ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                }
+                    for (int s = 0; s < 2; ++s) {
+                        const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                        const int c = s * 4 + g;
+                        wf[WKEEP ? nq : 0][ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
             if (!(ABL & 1) && more && p < 2) stage4(cur ^ 1, kofs(kt + 1), p * 4);
             if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -507,10 +526,10 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
 #pragma unroll
                     for (int ni = 0; ni < 2; ++ni)
                         if constexpr (!(ABL & 2))
-                            acc[mq][nq][mi][ni] =
-                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s], af[mi][s], acc[mq][nq][mi][ni], 0, 0, 0);
+                            acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[WKEEP ? nq : 0][ni][s], af[mi][s],
+                                                                                         acc[mq][nq][mi][ni], 0, 0, 0);
                         else
-                            asm volatile("" ::"v"(wf[ni][s]), "v"(af[mi][s]));
+                            asm volatile("" ::"v"(wf[WKEEP ? nq : 0][ni][s]), "v"(af[mi][s]));
             __builtin_amdgcn_s_setprio(0);
             bar();
         }
@@ -534,7 +553,7 @@ __device__ __forceinline__ void pp_bias_regs(const GemmArgs &a, int n0, float4 (
     }
 }
 
-template <int EPI, int ABL = 0, int NKT = 0>
+template <int EPI, int ABL = 0, int NKT = 0, int KL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     // LayerNorm-fold consumers keep the tile rows' (rstd, -rstd*mu) behind the ring (one
     // __shared__ array: a second one would make hipcc drain the LDS-DMA queue every K-step)
@@ -559,7 +578,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     RC_STAMP(sb + 5, (uint64_t)(m0 / PP_BM) | ((uint64_t)(n0 / PP_BM) << 32));
     float4 biasr[2][2];
     pp_bias_regs<EPI>(a, n0, biasr, threadIdx.x);
-    pp_kloop<EPI, ABL>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, threadIdx.x, sb + 1);
+    pp_kloop<EPI, ABL, KL>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, threadIdx.x, sb + 1);
     if constexpr ((ABL & 4) != 0) {
 #pragma unroll
         for (int a0 = 0; a0 < 2; ++a0)
@@ -1241,9 +1260,18 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 // (Rounds 1-2 also measured a 128x128 4-wave kernel, a 256x256 / 128x256 single-
 // barrier kernel, a persistent kernel, Stream-K and a deferred-store persistent
 // kernel: each lost on every shape and was removed.)
-enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9 };
+enum GemmVariant {
+    GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9,
+    // ping-pong with an explicit K-loop form KL = variant - 10 (A/B; GEMM_PINGPONG = the default form)
+    GEMM_PP_KL0 = 10, GEMM_PP_KL1 = 11, GEMM_PP_KL2 = 12, GEMM_PP_KL3 = 13
+};
+constexpr int GEMM_PP_KL_DEFAULT = 0;  // the ping-pong K-loop form the product runs
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
+    if (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) {  // a K-loop form where auto runs the ping-pong kernel
+        const int p = gemm_pick(a, GEMM_AUTO, patch_epilogue, pair_epilogue);
+        return p == GEMM_PINGPONG ? variant : p;
+    }
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
     // Short square projections (O-proj, patch embed: N = K = 768) finish in
@@ -1294,7 +1322,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        RC_REQUIRE((pick == GEMM_PINGPONG || pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
+        RC_REQUIRE((pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING4 ||
+                    pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
                        a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
     }
     switch (pick) {
@@ -1337,14 +1366,27 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
-        case GEMM_PINGPONG: {
+        case GEMM_PINGPONG:
+        case GEMM_PP_KL1:
+        case GEMM_PP_KL2:
+        case GEMM_PP_KL3: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             a.group_m = gemm_group_m(a);
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
-            if (a.K == 768) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 12>), gr, bl, 0, s, a);
-            else if (a.K == 3072) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 48>), gr, bl, 0, s, a);
-            else hipLaunchKernelGGL((gemm_pp_kernel<EPI>), gr, bl, 0, s, a);
+            const int kl = pick == GEMM_PINGPONG ? GEMM_PP_KL_DEFAULT : pick - GEMM_PP_KL0;
+            auto go = [&](auto klc) {
+                constexpr int KLV = decltype(klc)::value;
+                if (a.K == 768) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 12, KLV>), gr, bl, 0, s, a);
+                else if (a.K == 3072) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 48, KLV>), gr, bl, 0, s, a);
+                else hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 0, KLV>), gr, bl, 0, s, a);
+            };
+            switch (kl) {
+                case 1: go(std::integral_constant<int, 1>{}); break;
+                case 2: go(std::integral_constant<int, 2>{}); break;
+                case 3: go(std::integral_constant<int, 3>{}); break;
+                default: go(std::integral_constant<int, 0>{}); break;
+            }
             break;
         }
 #if defined(RC_GEMM_ABLATION)

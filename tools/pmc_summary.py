@@ -89,8 +89,10 @@ def main():
             except (OSError, ValueError):
                 latest = {}
         for key, knames in keys.items():
-            kname = next((k for k in knames if any(r["kernel"] == k for r in out.values())), knames[0])
-            recs = [r for r in out.values() if r["kernel"] == kname]
+            # prefix match: "gemm_pp_kernel<5, 0, 12" also names the K-loop forms <5, 0, 12, KL>
+            kname = next((k for k in knames if any(r["kernel"].startswith(k.rstrip(">")) for r in out.values())),
+                         knames[0])
+            recs = [r for r in out.values() if r["kernel"].startswith(kname.rstrip(">"))]
             if recs:  # bench prices the full-size launches (unsplit fc1, 125M-row scan / filter): the longest grid
                 gmax = max(recs, key=lambda r: r["dur_us"])["grid"]
                 recs = [r for r in recs if r["grid"] == gmax]
