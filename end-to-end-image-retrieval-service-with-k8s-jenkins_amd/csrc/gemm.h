@@ -1265,7 +1265,10 @@ enum GemmVariant {
     // ping-pong with an explicit K-loop form KL = variant - 10 (A/B; GEMM_PINGPONG = the default form)
     GEMM_PP_KL0 = 10, GEMM_PP_KL1 = 11, GEMM_PP_KL2 = 12, GEMM_PP_KL3 = 13
 };
-constexpr int GEMM_PP_KL_DEFAULT = 0;  // the ping-pong K-loop form the product runs
+// the ping-pong K-loop form the product runs: W kept (r04b in-model A/B, tools/gemm_ab.py, median of
+// 3 interleaved rounds: QKV 178.0 -> 175.3, fc1 274.5 -> 269.9, fc2 297.7 -> 294.4 us per launch,
+// step 10.08 -> 10.02 ms; the buffer-load DMA (KL 2) lost on fc2, 297.7 -> 313.1)
+constexpr int GEMM_PP_KL_DEFAULT = 1;
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
     if (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) {  // a K-loop form where auto runs the ping-pong kernel

@@ -174,7 +174,7 @@ def test_pool_decodes_per_member(vitmod, sd2, cuda):
     ref = single.decode_jpeg_for_embed(datas)
     assert len(ims) == 9 and all(torch.equal(a, b) for a, b in zip(ims, ref.unbind(0)))
     raw, _ = pool.embed_images(ims, assign=pool.assign_by_location(ims))
-    want, _ = single.embed(ref, normalized=False)
+    want, _ = single.embed_images(list(ref.unbind(0)))
     assert torch.equal(raw, want)
     assert pool.embed_jpeg(datas) == single.embed_jpeg(datas)
     pool.close()

@@ -11,6 +11,7 @@
 //  variant 4: 0 with the LDS-DMA as buffer loads (one lane offset, scalar row offsets)
 //  variant 5: 3 at BK = 32 in a 4-slot ring, three steps in flight, one barrier per step
 //  variant 6: ping-pong with 2 phases per K-step (32-MFMA segments, 4 barriers per step), W kept
+//  variants 7 / 8: ping-pong over a BK = 32 ring of 4 / 5 slots (64 / 96 KB of DMA in flight)
 //  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
 //             wrong results, timing only)
 // Every variant accumulates each output over K in the same order (chunks of 32, k
@@ -471,6 +472,111 @@ __global__ __launch_bounds__(512, 1) void lab_pp2(LabArgs a) {
             }
 }
 
+
+// ---------------------------------------------- ping-pong over a deep ring (BK = 32)
+// gemm_ring_kernel's schedule (2 phases per 32-deep step, W kept for both, 4 DMA pieces per wave
+// per step) with NS slots of 32 KB and NS - 2 steps in flight across every barrier: NS = 4 keeps
+// the 64 KB the 2 x 64 KB ping-pong keeps in flight, NS = 5 (all 160 KB of LDS) keeps 96 KB.
+// Every step is issued (past the end: the last step again, into the slot of a finished one), so
+// the counted wait is the same constant on every path.
+template <int NS>
+__global__ __launch_bounds__(512, 1) void lab_ring(LabArgs a) {
+    constexpr int BK = 32, A_BYTES = 256 * BK * 2, SLOT = 2 * A_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NS * SLOT];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / BK;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+    // 32 pieces of 1 KB (16 rows x 64 B) per slot: A rows = pieces 0-15, W = 16-31; wave w issues
+    // pieces w + 8 i, i = 0..3.  Lane l writes row l >> 2, stored chunk l & 3 = source chunk
+    // (l & 3) ^ (((l >> 5) & 1) << 1)
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    auto issue = [&](int t) {
+        const int tc = t < nk ? t : nk - 1;
+        uint8_t *base = smem + (t % NS) * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = piece < 16;
+            const uint16_t *src = is_a ? Ag + (int64_t)(piece * 16 + prow) * K : Wg + (int64_t)((piece - 16) * 16 + prow) * K;
+            __builtin_amdgcn_global_load_lds((const void *)(src + tc * BK + pchunk * 8), (lds_void_t *)(base + piece * 1024),
+                                             16, 0, 0);
+        }
+    };
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 2; ++l) acc[i][j][k][l] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) issue(t);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
+    bar();
+    if (grp == 1) bar();
+    bf16x8 af[4], wf[2][2];
+#pragma nounroll
+    for (int t = 0; t < nk; ++t) {
+        const uint8_t *As = smem + (t % NS) * SLOT;
+        const uint8_t *Ws = As + A_BYTES;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+                af[mi] = *reinterpret_cast<const bf16x8 *>(As + (grp * 128 + p * 64 + mi * 16 + li) * 64 + fchunk);
+            if (p == 0) {
+#pragma unroll
+                for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        wf[nq][ni] = *reinterpret_cast<const bf16x8 *>(Ws + (wc * 64 + nq * 32 + ni * 16 + li) * 64 + fchunk);
+                issue(t + NS - 1);  // into the slot step t - 1 used (every wave's reads of it closed)
+            } else {
+                // this wave's pieces of step t + 1 landed; steps t + 2 .. t + NS - 1 may fly
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        acc[p][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nq][ni], af[mi], acc[p][nq][mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+    }
+    if (grp == 0) bar();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's re-issued steps
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                    const int col = n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                    const f32x4 v = acc[mq][nq][mi][ni];
+                    if (row < a.M)
+                        *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                }
+}
+
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
                         uint64_t *stamps, hipStream_t s, int group_m) {
     if (N % 256 || K % 64) return 1;
@@ -484,6 +590,8 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 4: hipLaunchKernelGGL(lab_pp<4>, dim3(tiles), dim3(512), 0, s, a); break;
         case 5: hipLaunchKernelGGL(lab_w4r, dim3(tiles), dim3(256), 0, s, a); break;
         case 6: hipLaunchKernelGGL(lab_pp2, dim3(tiles), dim3(512), 0, s, a); break;
+        case 7: hipLaunchKernelGGL(lab_ring<4>, dim3(tiles), dim3(512), 0, s, a); break;
+        case 8: hipLaunchKernelGGL(lab_ring<5>, dim3(tiles), dim3(512), 0, s, a); break;
         case 16: hipLaunchKernelGGL(lab_pp<16>, dim3(tiles), dim3(512), 0, s, a); break;   // ablation: no DMA in the loop
         case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
         case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers

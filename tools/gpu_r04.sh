@@ -6,9 +6,9 @@ TAG=$1
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 300 python -u tools/gemm_lab/lab.py --stamps --rounds 3 --groups 0,2,4,16 > $O/lab.log 2>&1
+timeout -k 10 300 python -u tools/gemm_lab/lab.py --rounds 3 --variants ${LABV:-0,2,7,8,48} > $O/lab.log 2>&1
 echo "lab rc=$?"; tail -2 $O/lab.log | cut -c1-200
-VARIANTS=0,11,12,13 ROUNDS=3 STEPS=8 timeout -k 10 300 python -u tools/gemm_ab.py > $O/gemm_ab.log 2>&1
+VARIANTS=${ABV:-0,10} ROUNDS=3 STEPS=8 timeout -k 10 300 python -u tools/gemm_ab.py > $O/gemm_ab.log 2>&1
 echo "gemm_ab rc=$?"; tail -1 $O/gemm_ab.log | cut -c1-600
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
