@@ -614,15 +614,19 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // wave waits for its own pieces of step t + 1 (vmcnt(4 (NS - 3)) after issuing step
 // t + NS - 1's last pieces) in its (t, 1) M segment, and the barrier closing G1's (t, 1)
 // M segment precedes G0's (t + 1, 0) M segment.
+// NS = 5 (round 4): the ring takes all 160 KB and keeps 3 K-steps (96 KB) in flight; the LayerNorm
+// row scales then wait in a register (tid < 256: its row) through the K loop and go to LDS at
+// 128 KB once the loop is over (the epilogue stages at most 128 KB from offset 0).
 template <int EPI, int NS, int NKS = 0>
 __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
     constexpr int BM = 256, BN = 256, BK = 32;
     constexpr int A_BYTES = BM * BK * 2, SLOT = 2 * A_BYTES;  // 16 KB + 16 KB
     constexpr int LN_LDS = epi_ln(EPI) ? BM * 8 : 0;
+    constexpr bool LN_REG = NS * SLOT > 128 * 1024;  // no room past the ring: scales in registers
     // the epilogue stages up to 128 KB from offset 0: the LayerNorm row scales live past both
-    constexpr int LN_OFF = NS * SLOT > 128 * 1024 ? NS * SLOT : 128 * 1024;
-    constexpr int SMEM = LN_OFF + LN_LDS;
-    static_assert(NS >= 3 && NS <= 4 && SMEM <= 160 * 1024, "ring of 3..4 slots");
+    constexpr int LN_OFF = LN_REG ? 128 * 1024 : (NS * SLOT > 128 * 1024 ? NS * SLOT : 128 * 1024);
+    constexpr int SMEM = LN_REG ? NS * SLOT : LN_OFF + LN_LDS;
+    static_assert(NS >= 3 && NS <= 5 && SMEM <= 160 * 1024 && (!LN_REG || LN_OFF + LN_LDS <= SMEM), "ring of 3..5 slots");
     __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -698,10 +702,12 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
             stage2(t, t * BK, 2);
         }
     }
+    float2 ln_scale = make_float2(0.f, 0.f);
     if constexpr (epi_ln(EPI)) {
-        if (tid < BM)
-            *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) =
-                ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * LN_STRIDE, a.ln_eps);
+        if (tid < BM) {
+            ln_scale = ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * LN_STRIDE, a.ln_eps);
+            if constexpr (!LN_REG) *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) = ln_scale;
+        }
     }
     if (nk >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -735,8 +741,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
             }
             if (tn_ < nk) stage2(nslot, tn_ * BK, 2 * p);
             if (p == 1) {  // this wave's pieces of step t + 1 have landed (the younger steps may fly)
-                if (t + NS - 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
-                else if (t + NS - 2 < nk && NS >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 3)) : "memory");
+                const int younger = min(NS - 2, max(0, nk - t - 2));  // steps issued after t + 1
+                if (younger >= 3 && NS >= 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * 3) : "memory");
+                else if (younger == 2 && NS >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * 2) : "memory");
+                else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * 1) : "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -755,6 +763,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
         }
     }
     if (grp == 0) bar();  // balance the stagger barrier
+    if constexpr (LN_REG && epi_ln(EPI)) {  // the ring is free (every DMA waited for, every read retired)
+        if (tid < BM) *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) = ln_scale;
+        __syncthreads();
+    }
     pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr, threadIdx.x);
 }
 
@@ -1263,7 +1275,8 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 enum GemmVariant {
     GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9,
     // ping-pong with an explicit K-loop form KL = variant - 10 (A/B; GEMM_PINGPONG = the default form)
-    GEMM_PP_KL0 = 10, GEMM_PP_KL1 = 11, GEMM_PP_KL2 = 12, GEMM_PP_KL3 = 13
+    GEMM_PP_KL0 = 10, GEMM_PP_KL1 = 11, GEMM_PP_KL2 = 12, GEMM_PP_KL3 = 13,
+    GEMM_RING5 = 7  // the ring kernel with 5 slots (3 K-steps, 96 KB, in flight)
 };
 // the ping-pong K-loop form the product runs: W kept (r04b in-model A/B, tools/gemm_ab.py, median of
 // 3 interleaved rounds: QKV 178.0 -> 175.3, fc1 274.5 -> 269.9, fc2 297.7 -> 294.4 us per launch,
@@ -1271,7 +1284,8 @@ enum GemmVariant {
 constexpr int GEMM_PP_KL_DEFAULT = 1;
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
-    if (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) {  // a K-loop form where auto runs the ping-pong kernel
+    if ((variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) || variant == GEMM_RING5 || variant == GEMM_RING4) {
+        // a K-loop form / ring, applied where auto runs the ping-pong kernel
         const int p = gemm_pick(a, GEMM_AUTO, patch_epilogue, pair_epilogue);
         return p == GEMM_PINGPONG ? variant : p;
     }
@@ -1325,18 +1339,23 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        RC_REQUIRE((pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING4 ||
-                    pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
+        RC_REQUIRE((pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING5 ||
+                    pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
                        a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
     }
     switch (pick) {
+        case GEMM_RING5:
         case GEMM_RING4:
         case GEMM_RING3: {
             RC_REQUIRE(a.N % 256 == 0 && a.K % 32 == 0, RC_ERR_UNSUPPORTED, "ring GEMM: N % 256 == 0, K % 32 == 0");
             a.group_m = gemm_group_m(a);
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
-            if (pick == GEMM_RING4) {
+            if (pick == GEMM_RING5) {
+                if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 5, 24>), gr, bl, 0, s, a);
+                else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 5, 96>), gr, bl, 0, s, a);
+                else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 5>), gr, bl, 0, s, a);
+            } else if (pick == GEMM_RING4) {
                 if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 24>), gr, bl, 0, s, a);
                 else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 96>), gr, bl, 0, s, a);
                 else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4>), gr, bl, 0, s, a);
