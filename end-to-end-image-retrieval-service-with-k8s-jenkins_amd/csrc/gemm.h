@@ -1284,11 +1284,6 @@ enum GemmVariant {
 constexpr int GEMM_PP_KL_DEFAULT = 1;
 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
-    if ((variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) || variant == GEMM_RING5 || variant == GEMM_RING4) {
-        // a K-loop form / ring, applied where auto runs the ping-pong kernel
-        const int p = gemm_pick(a, GEMM_AUTO, patch_epilogue, pair_epilogue);
-        return p == GEMM_PINGPONG ? variant : p;
-    }
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
     // Short square projections (O-proj, patch embed: N = K = 768) finish in
@@ -1303,6 +1298,17 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool p
     (void)pair_epilogue;
     if (a.N <= 768 && a.K <= 768) return GEMM_W2;
     return GEMM_PINGPONG;
+}
+
+// The model's A/B knob (rc_model_set_gemm_variant): 4 / 5 / 6 force that kernel on every full-batch
+// projection; the ring of 5 slots (7) and the ping-pong K-loop forms (10-13) replace the ping-pong
+// kernel only where auto picks it (O-proj keeps its two-workgroup kernel, small batches the skinny)
+inline int gemm_model_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue) {
+    if (variant == GEMM_RING5 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3)) {
+        const int p = gemm_pick(a, GEMM_AUTO, patch_epilogue, pair_epilogue);
+        return p == GEMM_PINGPONG ? variant : p;
+    }
+    return variant;
 }
 
 // Ping-pong tile order: groups of 8 row tiles (column-major inside a group) when

@@ -347,7 +347,7 @@ void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = role >= 0 ? m->timers[role].begin(s) : -1;
-    launch_gemm<EPI>(a, m->gemm_variant, s);
+    launch_gemm<EPI>(a, gemm_model_variant(a, m->gemm_variant, epi_patch(EPI), epi_hl(EPI)), s);
     if (role >= 0) m->timers[role].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }

@@ -297,17 +297,18 @@ def test_from_pretrained_v5_layout_matches_golden(vitmod, cuda, tmp_path):
     direct.close()
 
 
-@pytest.mark.parametrize("variant", [5, 6])
-def test_ring_gemm_variant_bit_identical(vitmod, weights12, cuda, variant):
-    """The ring GEMM kernels (deeper LDS-DMA pipeline) accumulate K in the ping-pong kernel's
-    order: the 12-layer embedding of a batch is the same bits under either (all four
-    projection epilogues: LN-fold consumers, GELU, bf16-pair residual producers)."""
+@pytest.mark.parametrize("base,variant", [(4, 5), (4, 6), (0, 7), (0, 10), (0, 11), (0, 12), (0, 13)])
+def test_ring_gemm_variant_bit_identical(vitmod, weights12, cuda, base, variant):
+    """The ring GEMM kernels (deeper LDS-DMA pipeline, 3 / 4 / 5 slots) and the ping-pong K-loop
+    forms (W kept, buffer-load DMA) accumulate K in the ping-pong kernel's order: the 12-layer
+    embedding of a batch is the same bits under each (all four projection epilogues: LN-fold
+    consumers, GELU, bf16-pair residual producers)."""
     import torch
 
     rng = np.random.default_rng(21)
     imgs = torch.from_numpy(rng.integers(0, 256, (300, 224, 224, 3), dtype=np.uint8))
     m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=300)
-    m.set_gemm_variant(4)
+    m.set_gemm_variant(base)
     a, an = m.embed(imgs)
     m.set_gemm_variant(variant)
     b, bn = m.embed(imgs)
