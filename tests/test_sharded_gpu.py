@@ -296,7 +296,7 @@ def test_query_host_equals_search_plus_fetch(cuda, shards, n):
     import torch
 
     idxmod = import_pkg("index")
-    ss = idxmod.ShardSet(96, dtype="float16", capacity_per_shard=512, devices=[0] * shards)
+    ss = idxmod.ShardSet(96, dtype="float16", capacity_per_shard=1024, devices=[0] * shards)
     g = torch.Generator().manual_seed(n + shards)
     X = torch.randn(n, 96, generator=g)
     ss.upsert_rows(X, torch.arange(n))

@@ -12,6 +12,7 @@
 //  variant 5: 3 at BK = 32 in a 4-slot ring, three steps in flight, one barrier per step
 //  variant 6: ping-pong with 2 phases per K-step (32-MFMA segments, 4 barriers per step), W kept
 //  variants 7 / 8: ping-pong over a BK = 32 ring of 4 / 5 slots (64 / 96 KB of DMA in flight)
+//  variant 9: ping-pong with A through LDS-DMA and W loaded straight into registers one K-step ahead
 //  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
 //             wrong results, timing only)
 // Every variant accumulates each output over K in the same order (chunks of 32, k
@@ -577,6 +578,144 @@ __global__ __launch_bounds__(512, 1) void lab_ring(LabArgs a) {
                 }
 }
 
+
+// ------------------------------- ping-pong, A through LDS, W straight into registers
+// lab_pp's schedule with the weight tile never staged in LDS: each wave loads its own 64 W rows
+// (4 fragments x 2 k-halves, 16 B per lane each) from global memory (L2: the weights are <= 4.7 MB)
+// one K-step ahead into a second register set, while the LDS-DMA carries only the A tile (32 KB
+// per K-step instead of 64).  The W loads are inline asm (hipcc would drain every LDS-DMA before
+// their first use); the phase-3 vmcnt(0) that retires the A DMA of step t+1 also retires them.
+// Two K-steps per loop iteration so the two W register sets keep fixed names.
+__global__ __launch_bounds__(512, 1) void lab_ppw(LabArgs a) {
+    constexpr int A_BYTES = 256 * 64 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * A_BYTES];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 64;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    // A pieces: 32 per K-step (8 rows x 128 B), wave w issues pieces w + 8 i, i = 0..3
+    auto stageA = [&](int buf, int k0, int i0) {
+        uint8_t *base = smem + buf * A_BYTES;
+#pragma unroll
+        for (int i = i0; i < i0 + 2; ++i) {
+            const int piece = wave + 8 * i;
+            const int r = piece * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            __builtin_amdgcn_global_load_lds((const void *)(Ag + (int64_t)r * K + k0 + c * 8), (lds_void_t *)(base + piece * 1024),
+                                             16, 0, 0);
+        }
+    };
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 2; ++l) acc[i][j][k][l] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // three register slots of W fragments: nq = 1 always lives in Y (its next-step copy is loaded at
+    // phase 3, after phase 2 retired it, and waited for at phase 1 of the next step); nq = 0
+    // alternates between X and Z (next step's copy loaded at phase 0 into the idle slot)
+    bf16x8 wX[2][2], wY[2][2], wZ[2][2], af[4][2];
+    // saddr form: the wave-uniform row block + K-step in SGPRs, one 32-bit VGPR offset per (nq, ni)
+    uint32_t woff[2][2];
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) woff[nq][ni] = (uint32_t)(((nq * 32 + ni * 16 + li) * K + 8 * g) * 2);
+    const uint8_t *wblk = reinterpret_cast<const uint8_t *>(a.W) + (int64_t)(n0 + wc * 64) * K * 2;
+    auto loadW1 = [&](bf16x8 (&w)[2][2], int t, int nq) {
+        const uint8_t *base = wblk + t * 128;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+            asm volatile("global_load_dwordx4 %0, %2, %3\n\tglobal_load_dwordx4 %1, %2, %3 offset:64"
+                         : "=&v"(w[ni][0]), "=&v"(w[ni][1])
+                         : "v"(woff[nq][ni]), "s"(base)
+                         : "memory");
+    };
+    stageA(0, 0, 0);
+    stageA(0, 0, 2);
+    loadW1(wX, 0, 0);
+    loadW1(wY, 0, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp == 1) bar();
+    auto step = [&](int kt, bf16x8 (&w0)[2][2], bf16x8 (&w0n)[2][2]) {
+        const int cur = kt & 1;
+        const uint8_t *As = smem + cur * A_BYTES;
+        const bool more = kt + 1 < nk;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mq = p >> 1;
+            const int nq = (p == 1 || p == 2);
+            if (p == 0 || p == 2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        const int c = s2 * 4 + g;
+                        af[mi][s2] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+            }
+            if (more && p < 2) stageA(cur ^ 1, (kt + 1) * 64, p * 2);
+            if (more && p == 0) loadW1(w0n, kt + 1, 0);
+            if (p == 1) {
+                // this step's Y loads (issued at the previous step's phase 3) must have landed;
+                // younger: phase 0's 2 DMA + 4 loads and phase 1's 2 DMA
+                if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (p == 3) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // phase 2 was Y's last use this step: refill it for the next step
+                if (more) loadW1(wY, kt + 1, 1);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+                        acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nq ? wY[ni][s2] : w0[ni][s2], af[mi][s2],
+                                                                                    acc[mq][nq][mi][ni], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            bar();
+        }
+    };
+#pragma nounroll
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, wX, wZ);
+        step(kt + 1, wZ, wX);
+    }
+    if (grp == 0) bar();
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                    const int col = n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g;
+                    const f32x4 v = acc[mq][nq][mi][ni];
+                    if (row < a.M)
+                        *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                }
+}
+
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
                         uint64_t *stamps, hipStream_t s, int group_m) {
     if (N % 256 || K % 64) return 1;
@@ -592,6 +731,7 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 6: hipLaunchKernelGGL(lab_pp2, dim3(tiles), dim3(512), 0, s, a); break;
         case 7: hipLaunchKernelGGL(lab_ring<4>, dim3(tiles), dim3(512), 0, s, a); break;
         case 8: hipLaunchKernelGGL(lab_ring<5>, dim3(tiles), dim3(512), 0, s, a); break;
+        case 9: hipLaunchKernelGGL(lab_ppw, dim3(tiles), dim3(512), 0, s, a); break;
         case 16: hipLaunchKernelGGL(lab_pp<16>, dim3(tiles), dim3(512), 0, s, a); break;   // ablation: no DMA in the loop
         case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
         case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers
