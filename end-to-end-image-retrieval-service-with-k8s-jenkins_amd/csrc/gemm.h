@@ -1395,6 +1395,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case GEMM_PINGPONG:
+        case GEMM_PP_KL0:
         case GEMM_PP_KL1:
         case GEMM_PP_KL2:
         case GEMM_PP_KL3: {
