@@ -13,6 +13,8 @@
 //  variant 6: ping-pong with 2 phases per K-step (32-MFMA segments, 4 barriers per step), W kept
 //  variants 7 / 8: ping-pong over a BK = 32 ring of 4 / 5 slots (64 / 96 KB of DMA in flight)
 //  variant 9: ping-pong with A through LDS-DMA and W loaded straight into registers one K-step ahead
+//  variant 10: 5 software-pipelined: the next step's fragments read under this step's MFMAs
+//  variant 11: 10 with MFMA / ds_read as inline asm (program order, accumulators pinned in AGPRs)
 //  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
 //             wrong results, timing only)
 // Every variant accumulates each output over K in the same order (chunks of 32, k
@@ -716,6 +718,186 @@ __global__ __launch_bounds__(512, 1) void lab_ppw(LabArgs a) {
                 }
 }
 
+
+// ---------------------- 4 waves, 128x128 per wave, BK = 32 ring, fragments prefetched
+// lab_w4r's tile and ring (4 slots of A[256][32] + W[256][32], one barrier per 32-deep step),
+// but software-pipelined the way a one-wave-per-SIMD kernel has to be: step t's 64 MFMAs run on
+// fragments read during step t-1, while the wave reads step t+1's 16 fragments (4 after each of
+// the first four 8-MFMA rows) and issues its 8 DMA pieces of step t+3 (one per row).  Accumulators
+// live in AGPRs (256), two fragment sets in VGPRs (128).  Per step and CU: 64 KB of ds_read_b128
+// (256 LDS cycles) and 32 KB of DMA against 1024 MFMA cycles per SIMD — the 8-wave ping-pong
+// spends 192 KB of reads per 64-deep step.
+__global__ __launch_bounds__(256, 1) void lab_w4p(LabArgs a) {
+    constexpr int NS = 4, SLOT = 2 * 256 * 32 * 2, A_BYTES = 256 * 32 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NS * SLOT];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 32;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    const uint32_t voff = (uint32_t)((16 * wave + prow) * K + pchunk * 8) * 2u;
+    auto piece = [&](int t, int i) {
+        const int tc = t < nk ? t : nk - 1;
+        uint8_t *base = smem + (t % NS) * SLOT;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)((i < 4 ? Ag : Wg) + tc * 32), (short)0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(base + (wave + 4 * i) * 1024), 16, voff, (i & 3) * 64 * K * 2, 0, 0);
+    };
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+    auto frag = [&](int t, int j) -> bf16x8 {  // j < 8: W rows wc*128 + 16j; else A rows wr*128 + 16(j-8)
+        const uint8_t *base = smem + (t % NS) * SLOT + (j < 8 ? A_BYTES : 0);
+        const int r = (j < 8 ? wc : wr) * 128 + (j & 7) * 16 + li;
+        return *reinterpret_cast<const bf16x8 *>(base + r * 64 + fchunk);
+    };
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) piece(t, i);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    bar();
+    bf16x8 f0[16], f1[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) f0[j] = frag(0, j);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    auto step = [&](int t, bf16x8 (&cur)[16], bf16x8 (&nxt)[16]) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step t+1 landed
+        bar();                                              // ... and everyone's; slot (t+3)%4 free
+        __builtin_amdgcn_sched_barrier(0);
+        const bool rd = t + 1 < nk;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[ni], cur[8 + mi], acc[mi][ni], 0, 0, 0);
+            if (mi < 4 && rd) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) nxt[4 * mi + j] = frag(t + 1, 4 * mi + j);
+            }
+            piece(t + 3, mi);
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            if (mi < 4) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma nounroll
+    for (int t = 0; t < nk; t += 2) {
+        step(t, f0, f1);
+        step(t + 1, f1, f0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail re-reads
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int row = m0 + wr * 128 + mi * 16 + li;
+            const int col = n0 + wc * 128 + ni * 16 + 4 * g;
+            const f32x4 v = acc[mi][ni];
+            if (row < a.M)
+                *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+}
+
+
+// ------------------------- 10 with the loop in program order: MFMA and ds_read as inline asm
+// (accumulators pinned to AGPRs with "+a"; hipcc rotated accumulator tiles through a spare
+// AGPR quad every step in lab_w4p).  The compiler does not see these MFMAs: the epilogue's
+// first AGPR read waits out the last MFMA's passes with explicit s_nops.
+__device__ __forceinline__ void mfma_a(f32x4 &c, const bf16x8 &w, const bf16x8 &x) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(x));
+}
+__device__ __forceinline__ void ds_read16(bf16x8 &d, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(addr) : "memory");
+}
+__global__ __launch_bounds__(256, 1) void lab_w4a(LabArgs a) {
+    constexpr int NS = 4, SLOT = 2 * 256 * 32 * 2, A_BYTES = 256 * 32 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NS * SLOT];
+    int tm, tn;
+    tile_coords(a, 256, 256, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 32;
+    const uint16_t *Ag = a.A + (int64_t)m0 * K;
+    const uint16_t *Wg = a.W + (int64_t)n0 * K;
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    const uint32_t voff = (uint32_t)((16 * wave + prow) * K + pchunk * 8) * 2u;
+    auto piece = [&](int t, int i) {
+        const int tc = t < nk ? t : nk - 1;
+        uint8_t *base = smem + (t % NS) * SLOT;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)((i < 4 ? Ag : Wg) + tc * 32), (short)0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(base + (wave + 4 * i) * 1024), 16, voff, (i & 3) * 64 * K * 2, 0, 0);
+    };
+    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
+    const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+    const uint32_t waddr = sbase + A_BYTES + (wc * 128 + li) * 64 + fchunk;  // + slot, + 1024 j
+    const uint32_t aaddr = sbase + (wr * 128 + li) * 64 + fchunk;
+    auto frag = [&](bf16x8 &d, int t, int j) {
+        ds_read16(d, (j < 8 ? waddr : aaddr) + (t % NS) * SLOT + (j & 7) * 1024);
+    };
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) piece(t, i);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    bar();
+    bf16x8 f0[16], f1[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) frag(f0[j], 0, j);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    auto step = [&](int t, bf16x8 (&cur)[16], bf16x8 (&nxt)[16]) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step t+1 landed
+        bar();                                              // ... and everyone's; slot (t+3)%4 free
+        const int tn1 = t + 1 < nk ? t + 1 : t;             // last step: a harmless re-read
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) {
+                mfma_a(acc[mi][ni], cur[ni], cur[8 + mi]);
+                if (mi < 4 && (ni & 1)) frag(nxt[4 * mi + (ni >> 1)], tn1, 4 * mi + (ni >> 1));
+                if (ni == 3) piece(t + 3, mi);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+#pragma nounroll
+    for (int t = 0; t < nk; t += 2) {
+        step(t, f0, f1);
+        step(t + 1, f1, f0);
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int row = m0 + wr * 128 + mi * 16 + li;
+            const int col = n0 + wc * 128 + ni * 16 + 4 * g;
+            const f32x4 v = acc[mi][ni];
+            if (row < a.M)
+                *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+}
+
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
                         uint64_t *stamps, hipStream_t s, int group_m) {
     if (N % 256 || K % 64) return 1;
@@ -732,6 +914,8 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 7: hipLaunchKernelGGL(lab_ring<4>, dim3(tiles), dim3(512), 0, s, a); break;
         case 8: hipLaunchKernelGGL(lab_ring<5>, dim3(tiles), dim3(512), 0, s, a); break;
         case 9: hipLaunchKernelGGL(lab_ppw, dim3(tiles), dim3(512), 0, s, a); break;
+        case 10: hipLaunchKernelGGL(lab_w4p, dim3(tiles), dim3(256), 0, s, a); break;
+        case 11: hipLaunchKernelGGL(lab_w4a, dim3(tiles), dim3(256), 0, s, a); break;
         case 16: hipLaunchKernelGGL(lab_pp<16>, dim3(tiles), dim3(512), 0, s, a); break;   // ablation: no DMA in the loop
         case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
         case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers
