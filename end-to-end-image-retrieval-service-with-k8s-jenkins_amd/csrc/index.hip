@@ -13,6 +13,7 @@
 //   merge_partials_kernel: per query, top-k over all blocks' partial lists.
 // Algorithmic HBM bytes per query pass: n_rows * ld * sizeof(T).
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "index_common.h"
@@ -158,38 +159,8 @@ __global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__r
     const int qi = blockIdx.x;
     if (flags != nullptr && flags[qi] == 0) return;  // block-uniform
     WaveTopK<CAP> tk;
-    tk.init(as_lds(&lds[wave][0]), k);
-    const int64_t total = (int64_t)nlist * k;
-    // MERGE_U independent loads in flight per lane before any is consumed: the
-    // loop is latency-bound otherwise (one dependent HBM/L2 round trip per 64 keys)
-    constexpr int MERGE_U = 8;
-    for (int64_t j0 = (int64_t)wave * 64 * MERGE_U; j0 < total; j0 += 256 * MERGE_U) {
-        uint64_t key[MERGE_U];
-#pragma unroll
-        for (int u = 0; u < MERGE_U; ++u) {
-            const int64_t j = j0 + u * 64 + lane;
-            key[u] = KEY_EMPTY;
-            if (j < total) {
-                const int64_t l = j / k, t = j - l * k;
-                key[u] = partial[(l * nq_total + qi) * k + t];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < MERGE_U; ++u) {
-            tk.reserve(64);
-            tk.push(key[u] != KEY_EMPTY, key[u]);
-        }
-    }
-    tk.compact();
-    __syncthreads();
+    merge_partial_lists<CAP>(partial, nlist, nq_total, qi, k, lds, tk);
     if (wave == 0) {
-        for (int w = 1; w < 4; ++w)
-            for (int j = 0; j < k; j += 64) {
-                const uint64_t key = (j + lane < k) ? as_lds(&lds[w][0])[j + lane] : KEY_EMPTY;
-                tk.reserve(64);
-                tk.push(key != KEY_EMPTY, key);
-            }
-        tk.compact();
         for (int j = lane; j < k; j += 64) {
             const uint64_t key = tk.buf[j];
             const bool ok = key != KEY_EMPTY;
@@ -280,6 +251,7 @@ struct rc_index {
     int ws_nq = 0, ws_k = 0, ws_nblk = 0;
     float *qn = nullptr;
     uint64_t *partial = nullptr;
+    unsigned *q1_ticket = nullptr;  // query1_kernel's last-block ticket (0 between launches)
     BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
     KernelTimer timer;   // scan_topk_kernel launches (bytes)
     KernelTimer gtimer;  // filter_gemm_kernel launches (flops)
@@ -469,6 +441,52 @@ void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx,
     DeviceScope ds(h->device);
     dispatch_dtype(h->dtype, [&](auto t) { launch_upsert<decltype(t)>(h, vecs, src_idx, n, rows, s); });
 }
+
+// Internal (sharded.hip, rc_sharded_query_host): one query as ONE launch (query1_kernel) —
+// normalise, scan, merge, gather values — writing scores [k], rows [k] and (with_values)
+// values [k][dim] to out_* (host-mapped memory is fine: nothing is copied back).  Returns
+// false, enqueuing nothing, when the shape is outside the kernel's range (the caller takes
+// the multi-kernel path).  n_rows >= 1.
+bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int with_values, float *out_scores,
+                  int64_t *out_rows, float *out_values, hipStream_t s) {
+    if (h->dim > QUERY1_MAX_DIM || h->nch > 6 || topk_cap(k) > 256 || n_rows < 1 || n_rows > QUERY1_MAX_ROWS) return false;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceScope ds(h->device);
+    ensure_workspace(h, 1, k);
+    if (h->q1_ticket == nullptr) {
+        h->q1_ticket = (unsigned *)dmalloc(sizeof(unsigned));
+        RC_HIP(hipMemsetAsync(h->q1_ticket, 0, sizeof(unsigned), s));
+    }
+    Query1Args a{};
+    a.rows = h->rows;
+    a.norms = h->norms;
+    a.ld = h->ld;
+    a.dim = h->dim;
+    a.nch = h->nch;
+    a.n_rows = n_rows;
+    // >= 64 rows a block (two passes of the block's 32-row step), at most QUERY1_MAX_BLOCKS lists
+    int64_t rpb = std::max<int64_t>(64, (n_rows + QUERY1_MAX_BLOCKS - 1) / QUERY1_MAX_BLOCKS);
+    rpb = (rpb + 31) / 32 * 32;
+    a.rows_per_block = rpb;
+    a.nblk = (int)((n_rows + rpb - 1) / rpb);
+    a.k = k;
+    a.with_values = with_values;
+    a.row_base = h->row_base;
+    a.row_stride = h->row_stride;
+    a.partial = h->partial;
+    a.ticket = h->q1_ticket;
+    a.out_scores = out_scores;
+    a.out_rows = out_rows;
+    a.out_values = out_values;
+    std::memcpy(a.q, query, (size_t)h->dim * sizeof(float));
+    switch (h->dtype) {
+        case RC_F32: launch_query1_f32(a, s); break;
+        case RC_F16: launch_query1_f16(a, s); break;
+        case RC_BF16: launch_query1_bf16(a, s); break;
+        default: throw Error(RC_ERR_INVALID, "unknown dtype");
+    }
+    return true;
+}
 }  // namespace rc
 
 namespace {
@@ -532,6 +550,7 @@ int rc_index_destroy(rc_index *h) {
         dfree(h->norms);
         dfree(h->qn);
         dfree(h->partial);
+        dfree(h->q1_ticket);
         delete h;
     });
 }

@@ -94,6 +94,77 @@ void launch_scan_f32(const ScanArgs &a);
 void launch_scan_f16(const ScanArgs &a);
 void launch_scan_bf16(const ScanArgs &a);
 
+// One query, one launch (rc_sharded_query_host's request path): query1_kernel normalises the
+// query (carried in the kernel arguments: no copy), scans its block's rows, and the last block
+// to finish merges every block's partial list and gathers the matched rows' values, writing
+// scores / rows / values straight into (host-mapped) output memory.
+constexpr int QUERY1_MAX_DIM = 768;       // the query rides in the kernarg segment (< 4 KB)
+constexpr int QUERY1_MAX_BLOCKS = 256;    // partial lists the last block merges, at most
+constexpr int64_t QUERY1_MAX_ROWS = 1 << 20;  // beyond this the multi-kernel scan has more blocks in flight
+struct Query1Args {
+    const void *rows;
+    const float *norms;
+    int64_t ld;
+    int dim;
+    int nch;
+    int64_t n_rows;
+    int64_t rows_per_block;
+    int nblk;
+    int k;
+    int with_values;
+    int64_t row_base, row_stride;
+    uint64_t *partial;      // [nblk][k]
+    unsigned *ticket;       // 0 before the launch; the last block resets it
+    float *out_scores;      // [k]
+    int64_t *out_rows;      // [k]
+    float *out_values;      // [k][dim] (with_values)
+    float q[QUERY1_MAX_DIM];
+};
+void launch_query1_f32(const Query1Args &a, hipStream_t s);
+void launch_query1_f16(const Query1Args &a, hipStream_t s);
+void launch_query1_bf16(const Query1Args &a, hipStream_t s);
+
+// Merge nlist sorted partial lists of k keys (query qi of nq_total) into wave 0's tk: the body
+// of merge_partials_kernel, shared with query1_kernel's last block.  Block-collective.
+template <int CAP>
+__device__ __forceinline__ void merge_partial_lists(const uint64_t *__restrict__ partial, int nlist, int nq_total, int qi, int k,
+                                                    uint64_t (&lds)[4][CAP], WaveTopK<CAP> &tk) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    tk.init(as_lds(&lds[wave][0]), k);
+    const int64_t total = (int64_t)nlist * k;
+    // MERGE_U independent loads in flight per lane before any is consumed: the
+    // loop is latency-bound otherwise (one dependent HBM/L2 round trip per 64 keys)
+    constexpr int MERGE_U = 8;
+    for (int64_t j0 = (int64_t)wave * 64 * MERGE_U; j0 < total; j0 += 256 * MERGE_U) {
+        uint64_t key[MERGE_U];
+#pragma unroll
+        for (int u = 0; u < MERGE_U; ++u) {
+            const int64_t j = j0 + u * 64 + lane;
+            key[u] = KEY_EMPTY;
+            if (j < total) {
+                const int64_t l = j / k, t = j - l * k;
+                key[u] = partial[(l * nq_total + qi) * k + t];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < MERGE_U; ++u) {
+            tk.reserve(64);
+            tk.push(key[u] != KEY_EMPTY, key[u]);
+        }
+    }
+    tk.compact();
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < 4; ++w)
+            for (int j = 0; j < k; j += 64) {
+                const uint64_t key = (j + lane < k) ? as_lds(&lds[w][0])[j + lane] : KEY_EMPTY;
+                tk.reserve(64);
+                tk.push(key != KEY_EMPTY, key);
+            }
+        tk.compact();
+    }
+}
+
 // ------------------------------------------- batched MFMA search (search_mfma.hip)
 constexpr int BATCH_CAND_CAP = 4096;  // candidate slots per query per stage
 constexpr int INDEX_ROW_PAD = 256;    // row storage is allocated in whole 256-row tiles
@@ -164,25 +235,23 @@ int batch_stage_ratio(int k, int cap, int inflation = 1);
 constexpr int SCAN_U = 2;
 
 // One block's pass over its row range for queries [q0, q0 + QB): partial top-k keys.
+template <typename T, int NCH>
+struct ScanShape {
+    static constexpr int EPC = 16 / sizeof(T);           // values per 16-B chunk
+    static constexpr int CPL = NCH * 128 / (16 * EPC);   // chunks per lane
+};
+
+// One block's pass over its row range for the QB queries held in registers q (lane sub's
+// chunks sub + 16 i): partial top-k keys of queries q0 .. q0 + QB.
 template <typename T, int NCH, int QB, int CAP>
-__device__ __forceinline__ void scan_rows(const T *__restrict__ rows, int64_t ld, int64_t n_rows, int64_t rows_per_block,
-                                          const float *__restrict__ qn, int q0, int nq_total, int k,
-                                          uint64_t *__restrict__ partial) {
-    constexpr int EPC = 16 / sizeof(T);
-    constexpr int CPL = NCH * 128 / (16 * EPC);
+__device__ __forceinline__ void scan_rows_q(const T *__restrict__ rows, int64_t ld, int64_t n_rows, int64_t rows_per_block,
+                                            const float (&q)[QB][ScanShape<T, NCH>::CPL][ScanShape<T, NCH>::EPC], int q0,
+                                            int nq_total, int k, uint64_t *__restrict__ partial) {
+    constexpr int EPC = ScanShape<T, NCH>::EPC;
+    constexpr int CPL = ScanShape<T, NCH>::CPL;
     __shared__ uint64_t lds[4][QB][CAP];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 15, rg = lane >> 4;
-
-    float q[QB][CPL][EPC];
-#pragma unroll
-    for (int b = 0; b < QB; ++b)
-#pragma unroll
-        for (int i = 0; i < CPL; ++i)
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-                q[b][i][e] = qn[(int64_t)(q0 + b) * ld + (sub + 16 * i) * EPC + e];
-            }
 
     WaveTopK<CAP> tk[QB];
     static_for<QB>([&](auto bc) { tk[bc.value].init(as_lds(&lds[wave][bc.value][0]), k); });
@@ -248,6 +317,23 @@ __device__ __forceinline__ void scan_rows(const T *__restrict__ rows, int64_t ld
 }
 
 template <typename T, int NCH, int QB, int CAP>
+__device__ __forceinline__ void scan_rows(const T *__restrict__ rows, int64_t ld, int64_t n_rows, int64_t rows_per_block,
+                                          const float *__restrict__ qn, int q0, int nq_total, int k,
+                                          uint64_t *__restrict__ partial) {
+    constexpr int EPC = ScanShape<T, NCH>::EPC;
+    constexpr int CPL = ScanShape<T, NCH>::CPL;
+    const int sub = threadIdx.x & 15;
+    float q[QB][CPL][EPC];
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int i = 0; i < CPL; ++i)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) q[b][i][e] = qn[(int64_t)(q0 + b) * ld + (sub + 16 * i) * EPC + e];
+    scan_rows_q<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, q, q0, nq_total, k, partial);
+}
+
+template <typename T, int NCH, int QB, int CAP>
 __global__ __launch_bounds__(256) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
                                                        int64_t rows_per_block, const float *__restrict__ qn, int q0,
                                                        int nq_total, int k, uint64_t *__restrict__ partial,
@@ -303,6 +389,89 @@ void launch_scan_dtype(const ScanArgs &a) {
         case 12: return launch_scan_qb<T, 12>(a);
         case 16: return launch_scan_qb<T, 16>(a);
         default: throw Error(RC_ERR_UNSUPPORTED, "unsupported row width");
+    }
+}
+
+// rc_sharded_query_host's single-query launch (see Query1Args).  Every wave normalises the
+// query exactly as normalize_queries_kernel does (same lane partition of the sum of squares,
+// same wave_sum, same products), so scores are bit-identical to the multi-kernel path; the
+// top-k of a total order does not depend on how rows are split over blocks.  Ticket: each
+// block publishes its partial list (release fence, then one atomic); the block that takes the
+// last ticket acquires and finishes — every block reaches the exit.
+template <typename T, int NCH, int CAP>
+__global__ __launch_bounds__(256) void query1_kernel(const Query1Args a) {
+    constexpr int EPC = ScanShape<T, NCH>::EPC;
+    constexpr int CPL = ScanShape<T, NCH>::CPL;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane & 15;
+    float ss = 0.f;
+    for (int c = lane; c < a.dim; c += 64) ss = fmaf(a.q[c], a.q[c], ss);
+    ss = wave_sum(ss);
+    const float inv = ss > 0.f ? 1.0f / sqrtf(ss) : 0.f;
+    float q[1][CPL][EPC];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+            const int c = (sub + 16 * i) * EPC + e;
+            q[0][i][e] = c < a.dim ? a.q[c] * inv : 0.f;
+        }
+    scan_rows_q<T, NCH, 1, CAP>((const T *)a.rows, a.ld, a.n_rows, a.rows_per_block, q, 0, 1, a.k, a.partial);
+    __shared__ int last;
+    __threadfence();  // this block's partial list, visible device-wide before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(a.ticket, 1u) == (unsigned)(a.nblk - 1);
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // acquire: every other block's list
+    __shared__ uint64_t lds[4][CAP];
+    WaveTopK<CAP> tk;
+    merge_partial_lists<CAP>(a.partial, a.nblk, 1, 0, a.k, lds, tk);
+    __shared__ uint64_t best[CAP];
+    if (wave == 0) {
+        for (int j = lane; j < a.k; j += 64) {
+            const uint64_t key = tk.buf[j];
+            const bool ok = key != KEY_EMPTY;
+            best[j] = key;
+            a.out_scores[j] = ok ? key_score(key) : -INFINITY;
+            a.out_rows[j] = ok ? a.row_base + (int64_t)key_idx(key) * a.row_stride : -1;
+        }
+    }
+    __syncthreads();
+    if (a.with_values) {  // fetch_kernel's arithmetic: stored row x norm, NaN for an empty slot
+        const T *rows = (const T *)a.rows;
+        for (int j = wave; j < a.k; j += 4) {
+            const uint64_t key = best[j];
+            float *dst = a.out_values + (int64_t)j * a.dim;
+            if (key == KEY_EMPTY) {
+                for (int c = lane; c < a.dim; c += 64) dst[c] = __builtin_nanf("");
+            } else {
+                const int64_t r = key_idx(key);
+                const float nrm = a.norms[r];
+                for (int c = lane; c < a.dim; c += 64) dst[c] = Elem<T>::load(rows, r * a.ld + c) * nrm;
+            }
+        }
+    }
+    if (threadIdx.x == 0) *a.ticket = 0u;  // ready for the next launch (stream-ordered)
+}
+
+template <typename T, int NCH>
+void launch_query1_cap(const Query1Args &a, hipStream_t s) {
+    const int cap = topk_cap(a.k);
+    if (cap <= 128) hipLaunchKernelGGL((query1_kernel<T, NCH, 128>), dim3(a.nblk), dim3(256), 0, s, a);
+    else if (cap <= 256) hipLaunchKernelGGL((query1_kernel<T, NCH, 256>), dim3(a.nblk), dim3(256), 0, s, a);
+    else throw Error(RC_ERR_UNSUPPORTED, "single-query launch needs k <= 128");
+    RC_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_query1_dtype(const Query1Args &a, hipStream_t s) {
+    switch (a.nch) {
+        case 1: return launch_query1_cap<T, 1>(a, s);
+        case 2: return launch_query1_cap<T, 2>(a, s);
+        case 3: return launch_query1_cap<T, 3>(a, s);
+        case 4: return launch_query1_cap<T, 4>(a, s);
+        case 6: return launch_query1_cap<T, 6>(a, s);
+        default: throw Error(RC_ERR_UNSUPPORTED, "single-query launch: row width beyond 768");
     }
 }
 #endif  // SCAN_INSTANTIATE

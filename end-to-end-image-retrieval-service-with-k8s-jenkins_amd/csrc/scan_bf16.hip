@@ -4,4 +4,5 @@
 
 namespace rc {
 void launch_scan_bf16(const ScanArgs &a) { launch_scan_dtype<bf16_t>(a); }
+void launch_query1_bf16(const Query1Args &a, hipStream_t s) { launch_query1_dtype<bf16_t>(a, s); }
 }  // namespace rc

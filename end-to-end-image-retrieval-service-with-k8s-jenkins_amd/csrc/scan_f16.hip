@@ -4,4 +4,5 @@
 
 namespace rc {
 void launch_scan_f16(const ScanArgs &a) { launch_scan_dtype<f16_t>(a); }
+void launch_query1_f16(const Query1Args &a, hipStream_t s) { launch_query1_dtype<f16_t>(a, s); }
 }  // namespace rc

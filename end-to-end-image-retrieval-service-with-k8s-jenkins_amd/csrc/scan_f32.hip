@@ -4,4 +4,5 @@
 
 namespace rc {
 void launch_scan_f32(const ScanArgs &a) { launch_scan_dtype<float>(a); }
+void launch_query1_f32(const Query1Args &a, hipStream_t s) { launch_query1_dtype<float>(a, s); }
 }  // namespace rc

@@ -18,6 +18,7 @@
 // with an RCCL all-gather instead (sharded.py).
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "index_common.h"
@@ -25,6 +26,8 @@
 namespace rc {
 void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *rows,
                          hipStream_t s);
+bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int with_values, float *out_scores,
+                  int64_t *out_rows, float *out_values, hipStream_t s);
 
 // dst[i][:] = src[idx[i]][:] (one wave per row): a remote shard's subset of an upsert
 // batch, made contiguous on the leader so only those rows cross xGMI.
@@ -533,6 +536,20 @@ int rc_sharded_query_host(rc_sharded *h, const float *queries, int nq, int64_t n
         const QueryLayout L = query_layout(h, nq, k, dev_values);
         ensure_query(h, L.total);
         DeviceScope dl(h->dev[0]);
+        if (h->n == 1 && nq == 1) {
+            // the request path: ONE launch (query in its arguments, results written straight
+            // into the pinned block), one synchronisation, no copies
+            float *hs = (float *)(h->qh + L.sc);
+            int64_t *hr = (int64_t *)(h->qh + L.rw);
+            float *hv = (float *)(h->qh + L.val);
+            if (index_query1(h->shard[0], queries, n_rows, k, with_values, hs, hr, hv, h->qs)) {
+                RC_HIP(hipStreamSynchronize(h->qs));
+                std::memcpy(scores, hs, (size_t)k * sizeof(float));
+                std::memcpy(out_rows, hr, (size_t)k * sizeof(int64_t));
+                if (with_values) std::memcpy(values, hv, (size_t)k * h->dim * sizeof(float));
+                return;
+            }
+        }
         std::memcpy(h->qh + L.q, queries, (size_t)nq * h->dim * sizeof(float));
         RC_HIP(hipMemcpyAsync(h->qd + L.q, h->qh + L.q, (size_t)nq * h->dim * sizeof(float), hipMemcpyHostToDevice, h->qs));
         float *dsc = (float *)(h->qd + L.sc);

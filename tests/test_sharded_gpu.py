@@ -317,3 +317,38 @@ def test_query_host_equals_search_plus_fetch(cuda, shards, n):
     e_s, e_r, _ = ss.query_host(q.numpy().copy(), 3, 0, True)
     assert np.isneginf(e_s).all() and (e_r == -1).all()
     ss.close()
+
+
+@pytest.mark.parametrize("dtype,dim,n", [("float32", 768, 10000), ("float16", 96, 700), ("bfloat16", 300, 70000),
+                                         ("float32", 768, 1), ("float16", 512, 33)])
+def test_single_query_launch_equals_multi_kernel(cuda, dtype, dim, n):
+    """One query through rc_sharded_query_host is ONE launch (query1_kernel: the query in its
+    arguments, normalise + scan + last-block merge + value gather, results written into pinned
+    memory); it returns the multi-kernel path's scores, rows and values bit for bit (search +
+    fetch), for every storage dtype, indexes smaller than k, and back-to-back calls (the
+    last-block ticket resets itself)."""
+    import torch
+
+    idxmod = import_pkg("index")
+    ss = idxmod.ShardSet(dim, dtype=dtype, capacity_per_shard=max(n, 64), devices=[0])
+    g = torch.Generator().manual_seed(dim + n)
+    X = torch.randn(n, dim, generator=g)
+    ss.upsert_rows(X, torch.arange(n))
+    q = torch.randn(3, dim, generator=g)
+    q[1] = X[n // 2]
+    for k in (1, 5, 100):
+        for qi in range(3):
+            for rep in range(2):
+                sc, rw, val = (a.copy() for a in ss.query_host(q[qi:qi + 1].numpy().copy(), k, n, True))
+                s_ref, r_ref = ss.search(q[qi:qi + 1], k, n)
+                assert np.array_equal(sc, s_ref.cpu().numpy()), (k, qi, rep)
+                assert np.array_equal(rw, r_ref.cpu().numpy()), (k, qi, rep)
+                live = rw[0] >= 0
+                assert live.sum() == min(k, n)
+                if live.any():
+                    want = ss.fetch_rows([int(r) for r in rw[0][live]]).numpy()
+                    assert np.array_equal(val[0][live], want)
+                assert np.isnan(val[0][~live]).all()
+    sc1, rw1, v1 = ss.query_host(q[1:2].numpy().copy(), 5, n, False)
+    assert rw1[0, 0] == n // 2 and v1 is None
+    ss.close()
