@@ -251,7 +251,9 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
                         u[1][h] = r2[1];
                     }
                     const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
-                    if (row < a.M) {
+                    if constexpr ((ABL & 8) != 0) {  // diagnostic: no C stores
+                        asm volatile("" ::"v"(u[0][0]), "v"(u[0][1]), "v"(u[1][0]), "v"(u[1][1]));
+                    } else if (row < a.M) {
                         uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + col);
                         const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
                         if constexpr ((ABL & 32) != 0) nt_store16(dst, val);
@@ -1304,7 +1306,11 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool p
 // projection; the ring of 5 slots (7) and the ping-pong K-loop forms (10-13) replace the ping-pong
 // kernel only where auto picks it (O-proj keeps its two-workgroup kernel, small batches the skinny)
 inline int gemm_model_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue) {
-    if (variant == GEMM_RING5 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3)) {
+    bool pp_only = variant == GEMM_RING5 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3);
+#if defined(RC_GEMM_ABLATION)
+    pp_only = pp_only || variant >= 100;  // ping-pong ablations (diagnostic builds) on ping-pong shapes only
+#endif
+    if (pp_only) {
         const int p = gemm_pick(a, GEMM_AUTO, patch_epilogue, pair_epilogue);
         return p == GEMM_PINGPONG ? variant : p;
     }
@@ -1345,8 +1351,12 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        RC_REQUIRE((pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING5 ||
-                    pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY) && a.ln_c &&
+        bool ln_ok = pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING5 ||
+                     pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY;
+#if defined(RC_GEMM_ABLATION)
+        ln_ok = ln_ok || (pick >= 100 && pick < 200);  // gemm_pp_kernel<EPI, ABL>
+#endif
+        RC_REQUIRE(ln_ok && a.ln_c &&
                        a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
     }
     switch (pick) {
@@ -1430,12 +1440,13 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
-        case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
+        case 100 + 0: case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
         case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: {
             a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
             switch (variant - 100) {
+                case 0: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0>), gr, bl, 0, s, a); break;
                 case 1: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1>), gr, bl, 0, s, a); break;
                 case 2: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 2>), gr, bl, 0, s, a); break;
                 case 3: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 3>), gr, bl, 0, s, a); break;

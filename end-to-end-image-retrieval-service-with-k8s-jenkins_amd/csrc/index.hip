@@ -13,6 +13,7 @@
 //   merge_partials_kernel: per query, top-k over all blocks' partial lists.
 // Algorithmic HBM bytes per query pass: n_rows * ld * sizeof(T).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -471,6 +472,9 @@ bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int wi
     a.nblk = (int)((n_rows + rpb - 1) / rpb);
     a.k = k;
     a.with_values = with_values;
+    // RC_QUERY1_LAUNCHES=2 (A/B): scan and finish as two launches instead of the ticket
+    const char *ql = std::getenv("RC_QUERY1_LAUNCHES");
+    a.launches = (ql && ql[0] == '2') ? 2 : 1;
     a.row_base = h->row_base;
     a.row_stride = h->row_stride;
     a.partial = h->partial;

@@ -98,7 +98,7 @@ void launch_scan_bf16(const ScanArgs &a);
 // query (carried in the kernel arguments: no copy), scans its block's rows, and the last block
 // to finish merges every block's partial list and gathers the matched rows' values, writing
 // scores / rows / values straight into (host-mapped) output memory.
-constexpr int QUERY1_MAX_DIM = 768;       // the query rides in the kernarg segment (< 4 KB)
+constexpr int QUERY1_MAX_DIM = 768;       // the query rides in the kernarg segment (< 4 KB); a multiple of 256
 constexpr int QUERY1_MAX_BLOCKS = 256;    // partial lists the last block merges, at most
 constexpr int64_t QUERY1_MAX_ROWS = 1 << 20;  // beyond this the multi-kernel scan has more blocks in flight
 struct Query1Args {
@@ -112,6 +112,7 @@ struct Query1Args {
     int nblk;
     int k;
     int with_values;
+    int launches;           // 1: one launch (last-block ticket); 2: scan launch + finishing launch
     int64_t row_base, row_stride;
     uint64_t *partial;      // [nblk][k]
     unsigned *ticket;       // 0 before the launch; the last block resets it
@@ -395,16 +396,30 @@ void launch_scan_dtype(const ScanArgs &a) {
 // rc_sharded_query_host's single-query launch (see Query1Args).  Every wave normalises the
 // query exactly as normalize_queries_kernel does (same lane partition of the sum of squares,
 // same wave_sum, same products), so scores are bit-identical to the multi-kernel path; the
-// top-k of a total order does not depend on how rows are split over blocks.  Ticket: each
-// block publishes its partial list (release fence, then one atomic); the block that takes the
-// last ticket acquires and finishes — every block reaches the exit.
+// top-k of a total order does not depend on how rows are split over blocks.
+// PHASE 0: one launch — each block publishes its partial list (release fence, then one
+// atomic ticket); the block that takes the last ticket acquires and finishes (every block
+// reaches the exit).  PHASE 1 / 2: the same work as two launches (scan blocks; one finishing
+// block), the kernel boundary ordering the lists instead of the fences.
 template <typename T, int NCH, int CAP>
-__global__ __launch_bounds__(256) void query1_kernel(const Query1Args a) {
+__device__ __forceinline__ void query1_scan(const Query1Args &a) {
     constexpr int EPC = ScanShape<T, NCH>::EPC;
     constexpr int CPL = ScanShape<T, NCH>::CPL;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane & 15;
+    const int lane = threadIdx.x & 63, sub = lane & 15;
+    // the kernarg segment may sit in host memory: one round of independent loads into LDS
+    // (no branches), then every read is local
+    __shared__ float qs[QUERY1_MAX_DIM];
+    {
+        constexpr int PER = QUERY1_MAX_DIM / 256;
+        float v[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) v[i] = a.q[threadIdx.x + 256 * i];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) qs[threadIdx.x + 256 * i] = v[i];
+    }
+    __syncthreads();
     float ss = 0.f;
-    for (int c = lane; c < a.dim; c += 64) ss = fmaf(a.q[c], a.q[c], ss);
+    for (int c = lane; c < a.dim; c += 64) ss = fmaf(qs[c], qs[c], ss);
     ss = wave_sum(ss);
     const float inv = ss > 0.f ? 1.0f / sqrtf(ss) : 0.f;
     float q[1][CPL][EPC];
@@ -413,16 +428,14 @@ __global__ __launch_bounds__(256) void query1_kernel(const Query1Args a) {
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
             const int c = (sub + 16 * i) * EPC + e;
-            q[0][i][e] = c < a.dim ? a.q[c] * inv : 0.f;
+            q[0][i][e] = c < a.dim ? qs[c] * inv : 0.f;
         }
     scan_rows_q<T, NCH, 1, CAP>((const T *)a.rows, a.ld, a.n_rows, a.rows_per_block, q, 0, 1, a.k, a.partial);
-    __shared__ int last;
-    __threadfence();  // this block's partial list, visible device-wide before its ticket
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(a.ticket, 1u) == (unsigned)(a.nblk - 1);
-    __syncthreads();
-    if (!last) return;
-    __threadfence();  // acquire: every other block's list
+}
+
+template <typename T, int CAP>
+__device__ __forceinline__ void query1_finish(const Query1Args &a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ uint64_t lds[4][CAP];
     WaveTopK<CAP> tk;
     merge_partial_lists<CAP>(a.partial, a.nblk, 1, 0, a.k, lds, tk);
@@ -451,16 +464,47 @@ __global__ __launch_bounds__(256) void query1_kernel(const Query1Args a) {
             }
         }
     }
-    if (threadIdx.x == 0) *a.ticket = 0u;  // ready for the next launch (stream-ordered)
+}
+
+template <typename T, int NCH, int CAP, int PHASE>
+__global__ __launch_bounds__(256) void query1_kernel(const Query1Args a) {
+    if constexpr (PHASE == 2) {
+        query1_finish<T, CAP>(a);
+        return;
+    } else {
+        query1_scan<T, NCH, CAP>(a);
+        if constexpr (PHASE == 0) {
+            __shared__ int last;
+            __threadfence();  // this block's partial list, visible device-wide before its ticket
+            __syncthreads();
+            if (threadIdx.x == 0) last = atomicAdd(a.ticket, 1u) == (unsigned)(a.nblk - 1);
+            __syncthreads();
+            if (!last) return;
+            __threadfence();  // acquire: every other block's list
+            query1_finish<T, CAP>(a);
+            if (threadIdx.x == 0) *a.ticket = 0u;  // ready for the next launch (stream-ordered)
+        }
+    }
+}
+
+template <typename T, int NCH, int CAP>
+void launch_query1_phases(const Query1Args &a, hipStream_t s) {
+    if (a.launches == 1) {
+        hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 0>), dim3(a.nblk), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 1>), dim3(a.nblk), dim3(256), 0, s, a);
+        RC_LAUNCH_CHECK();
+        hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 2>), dim3(1), dim3(256), 0, s, a);
+    }
+    RC_LAUNCH_CHECK();
 }
 
 template <typename T, int NCH>
 void launch_query1_cap(const Query1Args &a, hipStream_t s) {
     const int cap = topk_cap(a.k);
-    if (cap <= 128) hipLaunchKernelGGL((query1_kernel<T, NCH, 128>), dim3(a.nblk), dim3(256), 0, s, a);
-    else if (cap <= 256) hipLaunchKernelGGL((query1_kernel<T, NCH, 256>), dim3(a.nblk), dim3(256), 0, s, a);
+    if (cap <= 128) launch_query1_phases<T, NCH, 128>(a, s);
+    else if (cap <= 256) launch_query1_phases<T, NCH, 256>(a, s);
     else throw Error(RC_ERR_UNSUPPORTED, "single-query launch needs k <= 128");
-    RC_LAUNCH_CHECK();
 }
 
 template <typename T>

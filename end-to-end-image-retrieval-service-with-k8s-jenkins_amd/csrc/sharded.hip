@@ -18,6 +18,7 @@
 // with an RCCL all-gather instead (sharded.py).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -536,7 +537,8 @@ int rc_sharded_query_host(rc_sharded *h, const float *queries, int nq, int64_t n
         const QueryLayout L = query_layout(h, nq, k, dev_values);
         ensure_query(h, L.total);
         DeviceScope dl(h->dev[0]);
-        if (h->n == 1 && nq == 1) {
+        const char *q1 = std::getenv("RC_QUERY1");  // "0": the multi-kernel path (A/B)
+        if (h->n == 1 && nq == 1 && !(q1 && q1[0] == '0')) {
             // the request path: ONE launch (query in its arguments, results written straight
             // into the pinned block), one synchronisation, no copies
             float *hs = (float *)(h->qh + L.sc);

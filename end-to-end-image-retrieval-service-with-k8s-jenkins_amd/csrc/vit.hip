@@ -812,7 +812,11 @@ int rc_model_set_parts(rc_model *m, int parts) {
 int rc_model_set_gemm_variant(rc_model *m, int variant) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
-        RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING5 || variant == GEMM_RING4 ||
+        bool diag = false;
+#if defined(RC_GEMM_ABLATION)
+        diag = variant >= 100 && variant < 200;  // ping-pong ablations (tools/build_diag.sh builds only)
+#endif
+        RC_REQUIRE(diag || variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING5 || variant == GEMM_RING4 ||
                        variant == GEMM_RING3 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3),
                    RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 / 6 / 7 (ring of 4 / 3 / 5 slots), "
                    "10-13 (ping-pong K-loop forms)");

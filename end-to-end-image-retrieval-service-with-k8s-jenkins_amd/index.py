@@ -733,14 +733,15 @@ class Index:
         recent: dict[str, list[float]] = {}
         ids, meta = self._ids, self._meta
         for qi in range(q.shape[0]):
+            rows = rw[qi].tolist()
+            live = k - rows.count(-1)  # the lists are sorted: empty slots (-1) come last
+            vals = val[qi, :live].tolist() if include_values else None  # one conversion per query
             matches = []
-            for j, (s, r) in enumerate(zip(sc[qi].tolist(), rw[qi].tolist())):
-                if r < 0:
-                    continue
+            for j, (s, r) in enumerate(zip(sc[qi, :live].tolist(), rows[:live])):
                 vid = ids[r]
                 m = {"id": vid, "score": s}
                 if include_values:
-                    m["values"] = v = val[qi, j].tolist()
+                    m["values"] = v = vals[j]
                     recent[vid] = v
                 if include_metadata:
                     m["metadata"] = dict(meta.get(vid, {}))

@@ -44,7 +44,8 @@ for r in range(rounds):
         res[v]["step_ms"].append((time.perf_counter() - t0) / steps * 1e3)
         if ref is None:
             ref = raw.clone()
-        assert torch.equal(raw, ref), f"variant {v} changed the embedding bits"
+        if os.environ.get("NOCHECK") != "1":  # ablation builds change the bits on purpose
+            assert torch.equal(raw, ref), f"variant {v} changed the embedding bits"
         m.set_parts(1)
         m.timing(roles)
         m.timing_reset()

@@ -15,6 +15,7 @@
 //  variant 9: ping-pong with A through LDS-DMA and W loaded straight into registers one K-step ahead
 //  variant 10: 5 software-pipelined: the next step's fragments read under this step's MFMAs
 //  variant 11: 10 with MFMA / ds_read as inline asm (program order, accumulators pinned in AGPRs)
+//  variants 128 / 176: 0 / 48 without the C stores (the epilogue's HBM write burst)
 //  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
 //             wrong results, timing only)
 // Every variant accumulates each output over K in the same order (chunks of 32, k
@@ -71,6 +72,7 @@ template <int VAR>
 __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
     constexpr bool STAMP = VAR == 1, WKEEP = VAR == 2, BUF = VAR == 4;
     constexpr bool NO_DMA = (VAR & 16) != 0, NO_READ = (VAR & 32) != 0, NO_MFMA = (VAR & 64) != 0;
+    constexpr bool NO_STORE = (VAR & 128) != 0;
     constexpr int A_BYTES = 256 * 64 * 2;
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + (STAMP ? 8192 : 0)];
     int tm, tn;
@@ -198,7 +200,9 @@ __global__ __launch_bounds__(512, 1) void lab_pp(LabArgs a) {
                     const int row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
                     const int col = n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g;
                     const f32x4 v = acc[mq][nq][mi][ni];
-                    if (row < a.M)
+                    if constexpr (NO_STORE)
+                        asm volatile("" ::"v"(v));
+                    else if (row < a.M)
                         *reinterpret_cast<uint2 *>(a.C + (int64_t)row * a.N + col) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
                 }
     if constexpr (STAMP) {
@@ -920,6 +924,8 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
         case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers
         case 64: hipLaunchKernelGGL(lab_pp<64>, dim3(tiles), dim3(512), 0, s, a); break;   // no MFMA
+        case 128: hipLaunchKernelGGL(lab_pp<128>, dim3(tiles), dim3(512), 0, s, a); break;  // no C stores
+        case 176: hipLaunchKernelGGL(lab_pp<176>, dim3(tiles), dim3(512), 0, s, a); break;  // MFMA + barriers only
         default: return 2;
     }
     return hipGetLastError() == hipSuccess ? 0 : 3;

@@ -35,12 +35,27 @@ ix = ing.get_index("lat-probe", dimension=768, dtype="float32", capacity=len(X))
 ix.upsert_tensor([f"r{i}" for i in range(len(X))], torch.from_numpy(X).cuda(), None)
 q = np.ascontiguousarray(np.asarray(vec, np.float32)[None])
 ss = ix._set
-out = {
+out = {}
+for mode, env in (("multi_kernel", {"RC_QUERY1": "0"}), ("two_launch", {"RC_QUERY1_LAUNCHES": "2"})):
+    os.environ.update(env)
+    out[f"lib_novalues_{mode}"] = lat(lambda: ss.query_host(q, 5, len(X), False))
+    for key in env:
+        del os.environ[key]
+out.update({
     "lib_values": lat(lambda: ss.query_host(q, 5, len(X), True)),
     "lib_novalues": lat(lambda: ss.query_host(q, 5, len(X), False)),
     "index_query_values": lat(lambda: ix.query(vector=vec, top_k=5, include_values=True)),
     "index_query_novalues": lat(lambda: ix.query(vector=vec, top_k=5)),
     "search": lat(lambda: ret.search(ix, vec, top_k=5)),
     "asarray": lat(lambda: np.asarray(vec, np.float32)),
-}
+})
+idxmod = importlib.import_module(f"{PKG}.index")
+for n in (1, 1000, 100000):
+    s2 = idxmod.ShardSet(768, dtype="float32", capacity_per_shard=n, devices=[0])
+    s2.upsert_rows(torch.randn(n, 768), torch.arange(n))
+    out[f"lib_novalues_n{n}"] = lat(lambda: s2.query_host(q, 5, n, False))
+    s2.close()
+t1 = torch.zeros(1, device="cuda")
+out["torch_tiny_kernel_sync"] = lat(lambda: (t1.add_(1), torch.cuda.synchronize()))
+out["torch_sync_only"] = lat(lambda: torch.cuda.synchronize())
 print(json.dumps(out), flush=True)
