@@ -472,9 +472,11 @@ bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int wi
     a.nblk = (int)((n_rows + rpb - 1) / rpb);
     a.k = k;
     a.with_values = with_values;
-    // RC_QUERY1_LAUNCHES=2 (A/B): scan and finish as two launches instead of the ticket
+    // scan and finish as two launches: the kernel boundary orders the partial lists for less than
+    // the one-launch ticket's device-scope fences cost (35.3 vs 40.9 us per 10k-row call,
+    // profiles/r04/r04_query1_ab.json); RC_QUERY1_LAUNCHES=1 keeps the ticket form (A/B)
     const char *ql = std::getenv("RC_QUERY1_LAUNCHES");
-    a.launches = (ql && ql[0] == '2') ? 2 : 1;
+    a.launches = (ql && ql[0] == '1') ? 1 : 2;
     a.row_base = h->row_base;
     a.row_stride = h->row_stride;
     a.partial = h->partial;
