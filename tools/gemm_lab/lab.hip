@@ -15,6 +15,8 @@
 //  variant 9: ping-pong with A through LDS-DMA and W loaded straight into registers one K-step ahead
 //  variant 10: 5 software-pipelined: the next step's fragments read under this step's MFMAs
 //  variant 11: 10 with MFMA / ds_read as inline asm (program order, accumulators pinned in AGPRs)
+//  variants 12 / 13 / 14 / 15: persistent ping-pong, LDS-staged epilogue, 0 / 4 / 6 / 8 of each thread's
+//             16 C chunks stored during the next tile's first K-steps instead of at once
 //  variants 128 / 176: 0 / 48 without the C stores (the epilogue's HBM write burst)
 //  variants 16 / 32 / 48 / 64: 0 without the loop's DMA / LDS reads / both / MFMAs (ablations:
 //             wrong results, timing only)
@@ -22,6 +24,8 @@
 // ascending), so their results are bit-identical.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <utility>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -902,6 +906,171 @@ __global__ __launch_bounds__(256, 1) void lab_w4a(LabArgs a) {
         }
 }
 
+
+// ------------------------------ persistent ping-pong with the C stores spread over the next tile
+// lab_pp's K loop (variant 0 form) in a persistent grid (one workgroup per CU walks the tiles
+// t = i * grid + remap(block)).  Epilogue as the product's bf16 path: the 256 x 256 bf16 tile
+// staged in LDS (512-B rows, 16-B chunk XOR (row & 31)), then 16 row-chunk stores of 16 B per
+// thread.  DEF of them (0, 8 or 16) are held in registers and issued during the NEXT tile's
+// first K-steps (one per M segment of phases 0 and 2), so the CUs' write bursts overlap MFMA
+// work instead of stalling every CU at once; the last tile stores everything at once.
+template <int DEF>
+__global__ __launch_bounds__(512, 1) void lab_ppd(LabArgs a) {
+    constexpr int A_BYTES = 256 * 64 * 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int g = lane >> 4, li = lane & 15;
+    const int K = a.K, nk = K / 64;
+    const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
+    const int lr = wave * 8 + (lane >> 3);
+    const uint32_t voff = (uint32_t)(lr * K + (((lane & 7) ^ ((lr >> 1) & 7)) << 3)) * 2u;
+    uint4 pend[DEF > 0 ? DEF : 1];
+    int pm0 = -1, pn0 = 0;  // the previous tile (whose last DEF chunks per thread are pending)
+    const int rb = xcd_remap(blockIdx.x, gridDim.x);
+    // pending chunk i of this thread: epilogue iteration it = 16 - DEF + i, row (it*512+tid)>>5
+    auto store_pending = [&](int i) {
+        int ptid;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(ptid) : "v"(tid));  // recompute, do not hoist
+        const int id = (16 - DEF + i) * 512 + ptid;
+        const int rl = id >> 5, ch = id & 31;
+        if (pm0 + rl < a.M) *reinterpret_cast<uint4 *>(a.C + (int64_t)(pm0 + rl) * a.N + pn0 + ch * 8) = pend[i];
+    };
+#pragma nounroll
+    for (int tile = rb; tile < ntiles; tile += gridDim.x) {
+        int tm, tn;
+        tile_coords(a, 256, 256, tile, tm, tn);
+        const int m0 = tm * 256, n0 = tn * 256;
+        const uint16_t *Ag = a.A + (int64_t)m0 * K;
+        const uint16_t *Wg = a.W + (int64_t)n0 * K;
+        auto stage4 = [&](int buf, int k0, int i0) {  // buffer-load DMA (lab variant 4's form)
+            uint8_t *base = smem + buf * PP_STAGE;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void *)((i0 < 4 ? Ag : Wg) + k0), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(base + (wave + 8 * i) * 1024), 16, voff,
+                                                         (i & 3) * 64 * K * 2, 0, 0);
+        };
+        f32x4 acc[2][2][4][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int l = 0; l < 2; ++l) acc[i][j][k][l] = f32x4{0.f, 0.f, 0.f, 0.f};
+        stage4(0, 0, 0);
+        stage4(0, 0, 4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (grp == 1) bar();
+        bf16x8 af[4][2], wf[2][2];
+        int np = 0;
+        // one K-step; PS: this step issues pending chunks 2 PS and 2 PS + 1 (static indices)
+        auto kstep = [&](int kt, auto psc) {
+            constexpr int PS = decltype(psc)::value;
+            const int cur = kt & 1;
+            const uint8_t *As = smem + cur * PP_STAGE;
+            const uint8_t *Ws = As + A_BYTES;
+            const bool more = kt + 1 < nk;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int mq = p >> 1;
+                const int nq = (p == 1 || p == 2);
+                if (p == 0 || p == 2) {
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2) {
+                            const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                            const int c = s2 * 4 + g;
+                            af[mi][s2] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                        }
+                }
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int r = wc * 64 + nq * 32 + ni * 16 + li;
+                        const int c = s2 * 4 + g;
+                        wf[ni][s2] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                    }
+                if constexpr (PS >= 0) {  // one deferred C chunk of the previous tile per phase 0 / 2
+                    if (p == 0 && pm0 >= 0) store_pending(2 * PS);
+                    if (p == 2 && pm0 >= 0) store_pending(2 * PS + 1);
+                }
+                if (more && p < 2) stage4(cur ^ 1, (kt + 1) * 64, p * 4);
+                if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                bar();
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < 2; ++ni)
+                            acc[mq][nq][mi][ni] =
+                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni][s2], af[mi][s2], acc[mq][nq][mi][ni], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+                bar();
+            }
+        };
+        // the first DEF / 2 K-steps unrolled (each issues two pending chunks), then the rest
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            ((I < nk ? kstep(I, std::integral_constant<int, I>{}) : void()), ...);
+        }(std::make_integer_sequence<int, DEF / 2>{});
+#pragma nounroll
+        for (int kt = DEF / 2; kt < nk; ++kt) kstep(kt, std::integral_constant<int, -1>{});
+        (void)np;
+        if (grp == 0) bar();
+        if constexpr (DEF > 0) {  // pending chunks the loop did not reach (K shorter than the spread)
+            if (pm0 >= 0)
+#pragma unroll
+                for (int i = 0; i < DEF; ++i)
+                    if (i >= 2 * nk) store_pending(i);
+        }
+        // epilogue: stage the bf16 tile (every read and DMA of the loop retired by its last barrier).
+        // Its addresses derive from a laundered copy of the lane id, so hipcc recomputes them per
+        // tile instead of hoisting ~48 loop-invariant offsets into registers across the K loop.
+        int ltid;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(ltid) : "v"(tid));
+        const int eli = ltid & 15, eg = (ltid >> 4) & 3;
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+            for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const int rl = grp * 128 + mq * 64 + mi * 16 + eli;
+                        const int cl = wc * 64 + nq * 32 + ni * 16 + 4 * eg;
+                        const f32x4 v = acc[mq][nq][mi][ni];
+                        const int off = rl * 512 + ((((cl >> 3) ^ (rl & 31))) << 4) + (cl & 7) * 2;
+                        *reinterpret_cast<uint2 *>(smem + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                    }
+        __syncthreads();
+        const bool last = tile + (int)gridDim.x >= ntiles;
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int id = it * 512 + ltid;
+            const int rl = id >> 5, ch = id & 31;
+            const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
+            if (it >= 16 - DEF && !last)
+                pend[it - (16 - DEF)] = v;
+            else if (m0 + rl < a.M)
+                *reinterpret_cast<uint4 *>(a.C + (int64_t)(m0 + rl) * a.N + n0 + ch * 8) = v;
+        }
+        pm0 = m0;
+        pn0 = n0;
+        __syncthreads();  // LDS free for the next tile's prologue
+    }
+}
+
 extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint16_t *C, int M, int N, int K,
                         uint64_t *stamps, hipStream_t s, int group_m) {
     if (N % 256 || K % 64) return 1;
@@ -920,6 +1089,10 @@ extern "C" int lab_gemm(int variant, const uint16_t *A, const uint16_t *W, uint1
         case 9: hipLaunchKernelGGL(lab_ppw, dim3(tiles), dim3(512), 0, s, a); break;
         case 10: hipLaunchKernelGGL(lab_w4p, dim3(tiles), dim3(256), 0, s, a); break;
         case 11: hipLaunchKernelGGL(lab_w4a, dim3(tiles), dim3(256), 0, s, a); break;
+        case 12: hipLaunchKernelGGL(lab_ppd<0>, dim3(tiles < 256 ? tiles : 256), dim3(512), 0, s, a); break;
+        case 13: hipLaunchKernelGGL(lab_ppd<4>, dim3(tiles < 256 ? tiles : 256), dim3(512), 0, s, a); break;
+        case 14: hipLaunchKernelGGL(lab_ppd<6>, dim3(tiles < 256 ? tiles : 256), dim3(512), 0, s, a); break;
+        case 15: hipLaunchKernelGGL(lab_ppd<8>, dim3(tiles < 256 ? tiles : 256), dim3(512), 0, s, a); break;
         case 16: hipLaunchKernelGGL(lab_pp<16>, dim3(tiles), dim3(512), 0, s, a); break;   // ablation: no DMA in the loop
         case 32: hipLaunchKernelGGL(lab_pp<32>, dim3(tiles), dim3(512), 0, s, a); break;   // no LDS reads after step 0
         case 48: hipLaunchKernelGGL(lab_pp<48>, dim3(tiles), dim3(512), 0, s, a); break;   // neither: MFMA + barriers

@@ -4,7 +4,7 @@ yardstick; check every variant bit-identical to variant 0 and variant 0 against 
 Variant 1's per-barrier s_memtime stamps are summarised per segment.
 
 usage: python tools/gemm_lab/lab.py [--variants 0,2,3,4] [--rounds 5] [--stamps]
-(build: hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -shared lab.hip -o liblab.so)
+(build: hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -shared lab.hip -o liblab.so)
 """
 import argparse
 import ctypes as C
