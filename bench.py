@@ -315,6 +315,16 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
                               what="retriever.utils.search(index, emb, top_k=5) over 10,000 x 768 f32 rows "
                                    "(index.query with include_values=True, as the reference calls it)",
                               planted_found=sorted(got) == sorted(f"r{r}" for r in planted))
+    # where a request's time goes: the library call alone (one launch pair + sync, results as host
+    # arrays) and the Python list building the Pinecone-shaped response needs on top
+    qv = np.ascontiguousarray(np.asarray(vec, np.float32)[None])
+    out["search_top5"]["library_call"] = dict(
+        _lat(lambda: ix._set.query_host(qv, 5, len(X), True), reps * 5),
+        what="rc_sharded_query_host alone (query in, scores + rows + 5 x 768 values out as host arrays)")
+    vals = np.zeros((5, 768), np.float32)
+    out["search_top5"]["python_lists"] = dict(
+        _lat(lambda: (np.asarray(vec, np.float32), vals.tolist()), reps * 5),
+        what="the response's Python side alone: the 768-float query list to an array, 5 x 768 values to lists")
     from fastapi.testclient import TestClient
 
     log("bench: latency /search_image")

@@ -1509,7 +1509,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     }
     if constexpr (epi_ln(EPI)) {
         bool ln_ok = pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING5 ||
-                     pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY;
+                     pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY || gemm_is_ppd(pick);
 #if defined(RC_GEMM_ABLATION)
         ln_ok = ln_ok || (pick >= 100 && pick < 200);  // gemm_pp_kernel<EPI, ABL>
 #endif
