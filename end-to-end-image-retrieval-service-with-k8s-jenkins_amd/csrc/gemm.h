@@ -1565,6 +1565,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         case GEMM_PPD_3_4:
         case GEMM_PPD_2_6:
         case GEMM_PPD_4_4:
+        case GEMM_PPD_P_4:
+        case GEMM_PPD_P_0:
             if constexpr (epi_bf16_out(EPI) && !epi_patch(EPI)) {
                 RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
                 a.group_m = gemm_group_m(a);
