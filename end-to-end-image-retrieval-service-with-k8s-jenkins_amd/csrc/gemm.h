@@ -20,7 +20,6 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "topk.h"
 #include "vit_kernels.h"
 
 namespace rc {
@@ -186,30 +185,9 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
 // wc*64 + nq*32 + ni*16 + 4g + j).  smem: the ring (>= 128 KB, every read and DMA of the
 // K loop retired by its final barrier); ln_off: the LayerNorm-fold row scales (EPI_*_LN);
 // biasr: the bf16 epilogues' bias, loaded before the K loop.
-// Deferred C chunks held in named registers (no array: hipcc kept an array of them in scratch
-// under the fc1 epilogue's register pressure).  Indices are constants after unrolling.
-struct PendChunks {
-    uint4 v0, v1, v2, v3, v4, v5;
-    __device__ __forceinline__ void set(int i, const uint4 &v) {
-        if (i == 0) v0 = v;
-        else if (i == 1) v1 = v;
-        else if (i == 2) v2 = v;
-        else if (i == 3) v3 = v;
-        else if (i == 4) v4 = v;
-        else v5 = v;
-    }
-    __device__ __forceinline__ uint4 get(int i) const {
-        return i == 0 ? v0 : i == 1 ? v1 : i == 2 ? v2 : i == 3 ? v3 : i == 4 ? v4 : v5;
-    }
-};
-
-// DEF > 0 (gemm_ppd_kernel, bf16 epilogues): when defer is set, the thread's last DEF 16-B chunks
-// (staged path: iterations 16 - DEF .. 15; direct path: (mq, mi, nq) in loop order) go to pend
-// instead of memory — the next tile's K loop stores them (ppd_chunk_addr recomputes the address).
-template <int EPI, int ABL, int NR = 4, int DEF = 0>
+template <int EPI, int ABL, int NR = 4>
 __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2][4][2], uint8_t *smem, int ln_off,
-                                            int m0, int n0, const float4 (&biasr)[2][2], int tid,
-                                            PendChunks &pend, bool defer) {
+                                            int m0, int n0, const float4 (&biasr)[2][2], int tid) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wave >> 2, wc = wave & 3;
@@ -273,11 +251,8 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
                         u[1][h] = r2[1];
                     }
                     const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
-                    const int L = (mq * 4 + mi) * 2 + nq;  // this chunk's place in the direct path's order (unrolled: static)
                     if constexpr ((ABL & 8) != 0) {  // diagnostic: no C stores
                         asm volatile("" ::"v"(u[0][0]), "v"(u[0][1]), "v"(u[1][0]), "v"(u[1][1]));
-                    } else if (DEF > 0 && L >= 16 - DEF && defer) {
-                        pend.set(L - (16 - DEF), make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]));
                     } else if (row < a.M) {
                         uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + col);
                         const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
@@ -347,8 +322,6 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
             const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
             if constexpr ((ABL & 8) != 0) {
                 asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-            } else if (DEF > 0 && it >= 16 - DEF && defer) {
-                pend.set(it - (16 - DEF), v);
             } else if (m0 + rl < a.M) {
                 uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8);
                 if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
@@ -454,15 +427,9 @@ __device__ __forceinline__ void pp_tile_coords(const GemmArgs &a, int tile, int 
 // once and kept for both of its halves (24 LDS reads per wave per K-step instead of 32); bit 1 =
 // the LDS-DMA as buffer loads (one lane offset for all 8 pieces, the piece's rows in the scalar
 // offset, the K-step in the descriptor: no per-piece 64-bit address arithmetic).
-// DEF > 0 (gemm_ppd_kernel): the previous tile's DEF deferred C chunks go out during the first
-// DEF / 2 K-steps, one per phase-0 / phase-2 M segment (pend(i), i = 0 .. DEF - 1; those K-steps
-// are peeled so every index is static), and any the loop did not reach right after it.
-struct NoPending {
-    __device__ void operator()(int) const {}
-};
-template <int EPI, int ABL, int KL = 0, int DEF = 0, typename PEND = NoPending>
+template <int EPI, int ABL, int KL = 0>
 __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m0, int n0, int kb, int ke,
-                                         f32x4 (&acc)[2][2][4][2], int tid, int64_t sb = -1, const PEND &pend = PEND{}) {
+                                         f32x4 (&acc)[2][2][4][2], int tid, int64_t sb = -1) {
     constexpr bool WKEEP = (KL & 1) != 0, BUF = (KL & 2) != 0;
     constexpr int BM = PP_BM, BK = PP_BK, A_BYTES = BM * BK * 2, STAGE = PP_STAGE;
     const int lane = tid & 63;
@@ -517,8 +484,8 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
     if (grp == 1) bar();  // stagger: G1 one segment behind
 
     bf16x8 af[4][2], wf[WKEEP ? 2 : 1][2][2];  // [mi][s], [nq (W kept) or 0][ni][s]
-    auto kstep = [&](int kt, auto psc) __attribute__((always_inline)) {
-        constexpr int PSI = decltype(psc)::value;  // >= 0: this step issues pending chunks 2 PSI, 2 PSI + 1
+#pragma nounroll
+    for (int kt = kb; kt < ke; ++kt) {
         const int cur = (kt - kb) & 1;
         const uint8_t *As = smem + cur * STAGE;
         const uint8_t *Ws = As + A_BYTES;
@@ -548,10 +515,6 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
                         wf[WKEEP ? nq : 0][ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                     }
             }
-            if constexpr (PSI >= 0) {
-                if (p == 0) pend(2 * PSI);
-                if (p == 2) pend(2 * PSI + 1);
-            }
             if (!(ABL & 1) && more && p < 2) stage4(cur ^ 1, kofs(kt + 1), p * 4);
             if (p == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -572,23 +535,8 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
             __builtin_amdgcn_s_setprio(0);
             bar();
         }
-    };
-    if constexpr (DEF > 0) {
-        static_for<DEF / 2>([&](auto ic) {
-            if (kb + ic.value < ke) kstep(kb + ic.value, ic);
-        });
     }
-#pragma nounroll
-    for (int kt = kb + DEF / 2; kt < ke; ++kt) kstep(kt, std::integral_constant<int, -1>{});
     if (grp == 0) bar();  // balance the stagger barrier
-    if constexpr (DEF > 0) {  // pending chunks of K-steps the loop did not have
-        static_for<DEF / 2>([&](auto ic) {
-            if (kb + ic.value >= ke) {
-                pend(2 * ic.value);
-                pend(2 * ic.value + 1);
-            }
-        });
-    }
     if (sb >= 0) RC_STAMP(sb + 1, RC_NOW());
 }
 
@@ -644,93 +592,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                     for (int a3 = 0; a3 < 2; ++a3) asm volatile("" ::"v"(acc[a0][a1][a2][a3]));
         return;
     }
-    PendChunks nopend;
-    pp_epilogue<EPI, ABL>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, threadIdx.x, nopend, false);
+    pp_epilogue<EPI, ABL>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, threadIdx.x);
     RC_STAMP(sb + 3, RC_NOW());
-}
-
-// ------------------------------------------------ ping-pong, C stores deferred --
-// gemm_pp_kernel's tile, K loop and epilogue, TPB consecutive tiles per workgroup (tile order as
-// gemm_pp_kernel's, the XCD remap on workgroups).  The bf16 epilogue of every tile but the
-// workgroup's last holds DEF of each thread's 16 output chunks in registers and the next
-// tile's first DEF / 2 K-steps store them, one per phase-0 / phase-2 M segment — so the
-// chunks leave while MFMAs run instead of in the all-CU write burst at every tile boundary
-// that stalls gemm_pp_kernel (no-store ablation: QKV 212 -> 151 us in tools/gemm_lab;
-// -0.8 ms per batch in the model).  Results bit-identical (same arithmetic, same stores).
-template <int EPI>
-__device__ __forceinline__ uint4 *ppd_chunk_addr(const GemmArgs &a, int m0, int n0, int i, int DEF, int tid, bool &ok) {
-    // chunk i of DEF of the tile at (m0, n0): epilogue position 16 - DEF + i of this thread
-    int ltid;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(ltid) : "v"(tid));  // recomputed per use, not hoisted
-    const int pos = 16 - DEF + i;
-    const int ldc = a.ldc ? a.ldc : a.N;
-    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN;
-    int row, col;
-    if constexpr (DIRECT) {  // (mq, mi, nq) = pos in loop order; lane (g, li) of wave (grp, wc)
-        const int lane = ltid & 63, g = lane >> 4, li = lane & 15;
-        const int wave = ltid >> 6, grp = wave >> 2, wc = wave & 3;
-        const int nq = pos & 1, mi = (pos >> 1) & 3, mq = pos >> 3;
-        row = m0 + grp * 128 + mq * 64 + mi * 16 + li;
-        col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
-    } else {  // staged: iteration pos of the row-chunk store loop
-        const int id = pos * 512 + ltid;
-        row = m0 + (id >> 5);
-        col = n0 + (id & 31) * 8;
-    }
-    ok = row < a.M;
-    return reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * ldc + col);
-}
-
-template <int EPI, int NKT, int KL, int TPB, int DEF>
-__global__ __launch_bounds__(512, 1) void gemm_ppd_kernel(GemmArgs a) {
-    static_assert(epi_bf16_out(EPI) && !epi_patch(EPI) && DEF % 2 == 0, "bf16 epilogues");
-    constexpr int LN_LDS = epi_ln(EPI) ? PP_BM * 8 : 0;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + LN_LDS];
-    const int ntiles = ((a.M + PP_BM - 1) / PP_BM) * (a.N / PP_BM);
-    // TPB > 0: tiles [TPB b, TPB b + TPB) of workgroup b (remapped); TPB = 0: persistent, one
-    // workgroup per CU walking tiles b, b + grid, ... (the grid's rounds in gemm_pp_kernel's order)
-    const int rb = xcd_remap(blockIdx.x, gridDim.x);
-    const int t0 = TPB > 0 ? rb * TPB : rb, tstep = TPB > 0 ? 1 : (int)gridDim.x;
-    const int nmine = TPB > 0 ? TPB : (ntiles - rb + tstep - 1) / tstep;
-    static_assert(DEF <= 6, "PendChunks holds 6");
-    PendChunks pend;
-    int pm0 = 0, pn0 = 0;
-    bool have = false;  // pend holds the previous tile's chunks
-    for (int j = 0; j < nmine; ++j) {
-        const int tile = t0 + j * tstep;
-        if (tile >= ntiles) break;  // block-uniform
-        int tm, tn;
-        pp_tile_coords(a, tile, tm, tn);
-        const int m0 = tm * PP_BM, n0 = tn * PP_BM;
-        f32x4 acc[2][2][4][2];
-#pragma unroll
-        for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-            for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-                for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                    for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // the lane id laundered per tile: hipcc would otherwise hoist every tid-derived address of
-        // the K loop and epilogue out of the tile loop and keep them all live (spills)
-        int ltid;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(ltid) : "v"((int)threadIdx.x));
-        float4 biasr[2][2];
-        pp_bias_regs<EPI>(a, n0, biasr, ltid);
-        auto store_pending = [&](int i) __attribute__((always_inline)) {  // inlined: pend stays in registers
-            if (!have) return;
-            bool ok;
-            uint4 *dst = ppd_chunk_addr<EPI>(a, pm0, pn0, i, DEF, ltid, ok);
-            if (ok) *dst = pend.get(i);
-        };
-        pp_kloop<EPI, 0, KL, DEF>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, ltid, -1, store_pending);
-        const bool defer = DEF > 0 && j + 1 < nmine && tile + tstep < ntiles;
-        pp_epilogue<EPI, 0, 4, DEF>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, ltid, pend, defer);
-        have = defer;
-        pm0 = m0;
-        pn0 = n0;
-        __syncthreads();  // the epilogue's LDS reads are done before the next prologue's DMA
-    }
 }
 
 // --------------------------------------------------------------- ring GEMM --
@@ -906,8 +769,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
         if (tid < BM) *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) = ln_scale;
         __syncthreads();
     }
-    PendChunks nopend;
-    pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr, threadIdx.x, nopend, false);
+    pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr, threadIdx.x);
 }
 
 // Epilogue of a 128 x 256 tile held as acc[mi][ni] by 4 waves (wave w: columns
@@ -1406,20 +1268,6 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
     if (ok && g == 0) *reinterpret_cast<float2 *>(ln_stats + (int64_t)row * LN_STRIDE + 2 * blk) = st;
 }
 
-// compute units of the current device (cached per device): the persistent kernels' grid
-inline int gemm_cu_count() {
-    static int cache[64] = {0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) dev = 0;
-    if (cache[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cache[dev] = n;
-    }
-    return cache[dev];
-}
-
 // Kernel choice: 4 = ping-pong 256x256, 8 = two-workgroup 128x256, 9 = skinny
 // (M <= 256), 0 = auto.  Auto follows interleaved A/B timings on the batch-256 shapes
 // (tools/gemm_calib.py): ping-pong everywhere except the short square projections.
@@ -1430,13 +1278,8 @@ enum GemmVariant {
     GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9,
     // ping-pong with an explicit K-loop form KL = variant - 10 (A/B; GEMM_PINGPONG = the default form)
     GEMM_PP_KL0 = 10, GEMM_PP_KL1 = 11, GEMM_PP_KL2 = 12, GEMM_PP_KL3 = 13,
-    GEMM_RING5 = 7,  // the ring kernel with 5 slots (3 K-steps, 96 KB, in flight)
-    // ping-pong with deferred C stores (gemm_ppd_kernel), bf16 epilogues only:
-    // 14: 2 tiles per workgroup, 4 deferred chunks; 15: 3 / 4; 16: 2 / 6; 17: 4 / 4
-    // 18: persistent (one workgroup per CU), 4 deferred; 19: persistent, none
-    GEMM_PPD_2_4 = 14, GEMM_PPD_3_4 = 15, GEMM_PPD_2_6 = 16, GEMM_PPD_4_4 = 17, GEMM_PPD_P_4 = 18, GEMM_PPD_P_0 = 19
+    GEMM_RING5 = 7  // the ring kernel with 5 slots (3 K-steps, 96 KB, in flight)
 };
-inline bool gemm_is_ppd(int v) { return v >= GEMM_PPD_2_4 && v <= GEMM_PPD_P_0; }
 // the ping-pong K-loop form the product runs: W kept (r04b in-model A/B, tools/gemm_ab.py, median of
 // 3 interleaved rounds: QKV 178.0 -> 175.3, fc1 274.5 -> 269.9, fc2 297.7 -> 294.4 us per launch,
 // step 10.08 -> 10.02 ms; the buffer-load DMA (KL 2) lost on fc2, 297.7 -> 313.1)
@@ -1463,7 +1306,7 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool p
 // projection; the ring of 5 slots (7) and the ping-pong K-loop forms (10-13) replace the ping-pong
 // kernel only where auto picks it (O-proj keeps its two-workgroup kernel, small batches the skinny)
 inline int gemm_model_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue) {
-    bool pp_only = variant == GEMM_RING5 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) || gemm_is_ppd(variant);
+    bool pp_only = variant == GEMM_RING5 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3);
 #if defined(RC_GEMM_ABLATION)
     pp_only = pp_only || variant >= 100;  // ping-pong ablations (diagnostic builds) on ping-pong shapes only
 #endif
@@ -1509,7 +1352,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     }
     if constexpr (epi_ln(EPI)) {
         bool ln_ok = pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING5 ||
-                     pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY || gemm_is_ppd(pick);
+                     pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY;
 #if defined(RC_GEMM_ABLATION)
         ln_ok = ln_ok || (pick >= 100 && pick < 200);  // gemm_pp_kernel<EPI, ABL>
 #endif
@@ -1561,39 +1404,6 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
-        case GEMM_PPD_2_4:
-        case GEMM_PPD_3_4:
-        case GEMM_PPD_2_6:
-        case GEMM_PPD_4_4:
-        case GEMM_PPD_P_4:
-        case GEMM_PPD_P_0:
-            if constexpr (epi_bf16_out(EPI) && !epi_patch(EPI)) {
-                RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
-                a.group_m = gemm_group_m(a);
-                const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
-                constexpr int KLD = GEMM_PP_KL_DEFAULT;
-                auto go = [&](auto tpbc, auto defc) {
-                    constexpr int TPB = decltype(tpbc)::value, DEF = decltype(defc)::value;
-                    const dim3 gr(TPB > 0 ? (ntiles + TPB - 1) / TPB : std::min(ntiles, gemm_cu_count())), bl(512);
-                    if (a.K == 768) hipLaunchKernelGGL((gemm_ppd_kernel<EPI, 12, KLD, TPB, DEF>), gr, bl, 0, s, a);
-                    else hipLaunchKernelGGL((gemm_ppd_kernel<EPI, 0, KLD, TPB, DEF>), gr, bl, 0, s, a);
-                };
-                using I2 = std::integral_constant<int, 2>;
-                using I3 = std::integral_constant<int, 3>;
-                using I4 = std::integral_constant<int, 4>;
-                using I6 = std::integral_constant<int, 6>;
-                using I0 = std::integral_constant<int, 0>;
-                switch (pick) {
-                    case GEMM_PPD_2_4: go(I2{}, I4{}); break;
-                    case GEMM_PPD_3_4: go(I3{}, I4{}); break;
-                    case GEMM_PPD_2_6: go(I2{}, I6{}); break;
-                    case GEMM_PPD_P_4: go(I0{}, I4{}); break;
-                    case GEMM_PPD_P_0: go(I0{}, I0{}); break;
-                    default: go(I4{}, I4{}); break;
-                }
-                break;
-            }
-            [[fallthrough]];  // other epilogues: the ping-pong kernel
         case GEMM_PINGPONG:
         case GEMM_PP_KL0:
         case GEMM_PP_KL1:
@@ -1603,7 +1413,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             a.group_m = gemm_group_m(a);
             const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(512);
-            const int kl = (pick == GEMM_PINGPONG || gemm_is_ppd(pick)) ? GEMM_PP_KL_DEFAULT : pick - GEMM_PP_KL0;
+            const int kl = pick == GEMM_PINGPONG ? GEMM_PP_KL_DEFAULT : pick - GEMM_PP_KL0;
             auto go = [&](auto klc) {
                 constexpr int KLV = decltype(klc)::value;
                 if (a.K == 768) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 12, KLV>), gr, bl, 0, s, a);

@@ -817,7 +817,7 @@ int rc_model_set_gemm_variant(rc_model *m, int variant) {
         diag = variant >= 100 && variant < 200;  // ping-pong ablations (tools/build_diag.sh builds only)
 #endif
         RC_REQUIRE(diag || variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING5 || variant == GEMM_RING4 ||
-                       variant == GEMM_RING3 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3) || gemm_is_ppd(variant),
+                       variant == GEMM_RING3 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3),
                    RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 / 6 / 7 (ring of 4 / 3 / 5 slots), "
                    "10-13 (ping-pong K-loop forms)");
         std::lock_guard<std::mutex> lk(m->mu);

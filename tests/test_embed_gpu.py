@@ -297,14 +297,12 @@ def test_from_pretrained_v5_layout_matches_golden(vitmod, cuda, tmp_path):
     direct.close()
 
 
-@pytest.mark.parametrize("base,variant", [(4, 5), (4, 6), (0, 7), (0, 10), (0, 11), (0, 12), (0, 13), (0, 14), (0, 15),
-                                          (0, 16), (0, 17), (0, 18), (0, 19)])
+@pytest.mark.parametrize("base,variant", [(4, 5), (4, 6), (0, 7), (0, 10), (0, 11), (0, 12), (0, 13)])
 def test_ring_gemm_variant_bit_identical(vitmod, weights12, cuda, base, variant):
-    """The ring GEMM kernels (deeper LDS-DMA pipeline, 3 / 4 / 5 slots), the ping-pong K-loop
-    forms (W kept, buffer-load DMA) and the deferred-store forms (several tiles per workgroup or
-    persistent; C chunks stored under the next tile's K loop) accumulate K in the ping-pong
-    kernel's order: the 12-layer embedding of a batch is the same bits under each (all four
-    projection epilogues: LN-fold consumers, GELU, bf16-pair residual producers)."""
+    """The ring GEMM kernels (deeper LDS-DMA pipeline, 3 / 4 / 5 slots) and the ping-pong K-loop
+    forms (W kept, buffer-load DMA) accumulate K in the ping-pong kernel's order: the 12-layer
+    embedding of a batch is the same bits under each (all four projection epilogues: LN-fold
+    consumers, GELU, bf16-pair residual producers)."""
     import torch
 
     rng = np.random.default_rng(21)

@@ -24,7 +24,7 @@ def run(epi, variant, A, W, bias, M, out, pos=None, tokens=0):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 10, 11, 12, 13])
 @pytest.mark.parametrize("M,N,K", [(300, 768, 768), (1000, 2304, 768), (513, 3072, 768), (257, 768, 3072), (64, 256, 64)])
 @pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
 def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
