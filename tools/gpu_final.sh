@@ -7,8 +7,10 @@ set -u
 TAG=$1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+if [ "${SKIP_BENCH:-0}" != "1" ]; then
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?; cat gpurun_out/bench_$TAG.json; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench_$TAG.err; exit $rc; }
+fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python -u bench.py --no-cpu --no-latency --steps 5 --warmup 2 --parts 1 --ingest-images 32768 > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
 find gpurun_out/prof_$TAG -name '*kernel_trace.csv' -delete
