@@ -407,10 +407,15 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 // TOK > 0: the token count as a compile-time constant (197 for ViT-B/16 at 224),
 // so only the last key tile carries the padding mask; TOK = 0 reads `tokens`.
-template <int TOK>
-__global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                          int tokens_rt, int heads, float scale_log2e) {
-    constexpr int HD = 64, PPW = ATT2_TILES * 2 / 2;  // 13 DMA pieces per wave
+// W (waves per block): 4 — query tiles w, w + 4, ...; waves 0-1 stage K, 2-3 V (13 pieces each),
+// 3 blocks per CU; 8 — tiles w, w + 8 (the block's critical path 2 tiles, not 4), waves 0-3 stage K
+// and 4-7 V (7 pieces each, the 2 past the 26 re-load the last piece), 2 blocks per CU.
+template <int TOK, int W = 4>
+__global__ __launch_bounds__(64 * W, W == 4 ? 3 : 2) void attention_v2_kernel(const uint16_t *__restrict__ qkv,
+                                                                            uint16_t *__restrict__ out, int tokens_rt,
+                                                                            int heads, float scale_log2e) {
+    static_assert(W == 4 || W == 8, "4 or 8 waves");
+    constexpr int HD = 64, HALF = W / 2, PPW = (ATT2_TILES * 2 + HALF - 1) / HALF;  // DMA pieces per wave
     const int tokens = TOK > 0 ? TOK : tokens_rt;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];
     uint8_t *Ks = lds, *Vs = lds + ATT2_ROWS * 128;
@@ -441,9 +446,11 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     load_q(wave < nqt ? wave : 0, qf);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-        const int piece = wave * PPW + i;
-        const bool isv = piece >= ATT2_TILES * 2;
-        const int r = (isv ? piece - ATT2_TILES * 2 : piece) * 8 + (lane >> 3);
+        // wave w < HALF stages K pieces (w PPW + i), the others V; indices past 25 re-load piece 25
+        const bool isv = wave >= HALF;
+        const int kp = min((wave - (isv ? HALF : 0)) * PPW + i, ATT2_TILES * 2 - 1);
+        const int piece = isv ? ATT2_TILES * 2 + kp : kp;
+        const int r = kp * 8 + (lane >> 3);
         const int pc = lane & 7;
         const int c = isv ? (pc ^ (((r >> 1) & 3) << 1)) : (pc ^ ((r >> 1) & 7));
         const int rr = r < tokens ? r : tokens - 1;
@@ -455,8 +462,8 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    if (wave < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K staged (and Q)
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");  // Q only: V may fly
+    if (wave < HALF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K staged (and Q)
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");     // Q only: V may fly
     bar();
     __builtin_amdgcn_sched_barrier(0);  // nothing that reads qf moves above the wait
 
@@ -559,19 +566,19 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     // first tile: scores while V lands, then every wave waits for V once
     const bool first = wave < nqt;
     bf16x8 qn[2];
-    if (first && wave + 4 < nqt) load_q(wave + 4, qn);  // the next tile's queries, under the scores
+    if (first && wave + W < nqt) load_q(wave + W, qn);  // the next tile's queries, under the scores
     if (first) scores(qf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V staged (waves 2-3), qn landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V staged (waves HALF..), qn landed
     bar();
     __builtin_amdgcn_sched_barrier(0);
     if (first) pv_store(wave);
-    for (int qt = wave + 4; qt < nqt; qt += 4) {
+    for (int qt = wave + W; qt < nqt; qt += W) {
         // qn (issued a tile ago) has landed; the previous tile's 4 output stores may still fly
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         qf[0] = qn[0];
         qf[1] = qn[1];
-        if (qt + 4 < nqt) load_q(qt + 4, qn);  // prefetch the next tile's queries
+        if (qt + W < nqt) load_q(qt + W, qn);  // prefetch the next tile's queries
         scores(qf);
         pv_store(qt);
     }

@@ -287,6 +287,9 @@ int rc_model_set_ln_fold(rc_model *m, int on);
  * bit-identical across variants: every kernel accumulates K in the same order):
  * 0 auto, 4 ping-pong (one 64-deep K-tile in flight), 5 ring (4 slots of 32-deep
  * K-steps, 2 in flight), 6 ring (3 slots, 1 in flight). */
+// Attention kernel shape (A/B knob): 4 waves per (image, head) block, 3 blocks per CU (default),
+// or 8 waves, 2 blocks per CU.  Bit-identical results.
+int rc_model_set_attention_waves(rc_model *m, int waves);
 int rc_model_set_gemm_variant(rc_model *m, int variant);
 
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
