@@ -33,7 +33,7 @@ ref = None
 for r in range(rounds):
     for v in variants:
         if os.environ.get("KNOB") == "attn":  # A/B of the attention kernel shape instead
-            m.set_attention_waves(v)
+            m.set_attention_form(v)
         else:
             m.set_gemm_variant(v)
         m.set_parts(parts)
