@@ -672,23 +672,38 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
 #pragma unroll
             for (int j = QS_NS - SPS; j < QS_NS; ++j) issue(t + j);
             constexpr int NG = SPS * 2 * RH;
+            // row-fragment group gi: 4 rows-of-16 x (k-step kl, half sh) — read into cur, then 4 x QT
+            // MFMAs.  Rolling schedule: each fragment of group gi + 1 is read as soon as the MFMAs
+            // of the same slot of group gi have issued, so a group's LDS latency runs under the
+            // previous group's MFMAs instead of in front of its own (no extra registers: the new
+            // fragment takes the slot just freed).
+            auto frag_addr = [&](int gi) {
+                const int kl = gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
+                return smem + ((t + kl) % QS_NS) * STEP_BYTES + li * 128 + (((sh * 4 + g) ^ ((li >> 1) & 7)) << 4) +
+                       rh * 4 * 2048;
+            };
+            i32x4_t cur[4];
+            {
+                const uint8_t *Sr = frag_addr(0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cur[i] = *reinterpret_cast<const i32x4_t *>(Sr + i * 2048);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // group 0's reads go out together, ahead of the pattern
 #pragma unroll
             for (int gi = 0; gi < NG; ++gi) {
                 const int kl = gi / (2 * RH), sh = (gi / RH) % 2, rh = gi % RH;
                 const int ks = SPS * kp + kl;
-                const uint8_t *Sr = smem + ((t + kl) % QS_NS) * STEP_BYTES + li * 128 +
-                                    (((sh * 4 + g) ^ ((li >> 1) & 7)) << 4) + rh * 4 * 2048;
-                i32x4_t cur[4];
+                const uint8_t *Sn = frag_addr(gi + 1 < NG ? gi + 1 : gi);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) cur[i] = *reinterpret_cast<const i32x4_t *>(Sr + i * 2048);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i) {
 #pragma unroll
                     for (int qt = 0; qt < QT; ++qt)
                         acc[rh * 4 + i][qt] =
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(qf[qt][ks * 2 + sh], cur[i], acc[rh * 4 + i][qt], 0, 0, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                    if (gi + 1 < NG) cur[i] = *reinterpret_cast<const i32x4_t *>(Sn + i * 2048);
+                    __builtin_amdgcn_sched_group_barrier(0x008, QT, 0);
+                    if (gi + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
             }
         }
         // ---- epilogue: keep (q, row) iff sq·(sx·D) + ex·aq >= thr[q]
