@@ -14,6 +14,7 @@ the C ABI (``include/retrieval_core.h``).
 """
 from __future__ import annotations
 
+import array
 import json
 import os
 import threading
@@ -238,6 +239,11 @@ def _as_vector_np(values: Any, dim: int) -> np.ndarray:
     Python loop)."""
     if isinstance(values, torch.Tensor):
         a = values.detach().to(device="cpu", dtype=torch.float32).reshape(-1).numpy()
+    elif isinstance(values, (list, tuple)):
+        try:  # a JSON list of floats: array('f') converts it ~4x faster than np.asarray (same f32 rounding)
+            a = np.frombuffer(array.array("f", values), dtype=np.float32)
+        except TypeError:
+            a = np.asarray(values, dtype=np.float32).reshape(-1)
     else:
         a = np.asarray(values, dtype=np.float32).reshape(-1)
     if a.shape[0] != dim:
@@ -735,7 +741,8 @@ class Index:
         for qi in range(q.shape[0]):
             rows = rw[qi].tolist()
             live = k - rows.count(-1)  # the lists are sorted: empty slots (-1) come last
-            vals = val[qi, :live].tolist() if include_values else None  # one conversion per query
+            # one conversion per query, through f64 (exact for f32; numpy's f64 tolist is the faster one)
+            vals = val[qi, :live].astype(np.float64).tolist() if include_values else None
             matches = []
             for j, (s, r) in enumerate(zip(sc[qi, :live].tolist(), rows[:live])):
                 vid = ids[r]
