@@ -322,9 +322,11 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
         _lat(lambda: ix._set.query_host(qv, 5, len(X), True), reps * 5),
         what="rc_sharded_query_host alone (query in, scores + rows + 5 x 768 values out as host arrays)")
     vals = np.zeros((5, 768), np.float32)
+    idxmod = importlib.import_module(f"{pkg}.index")
     out["search_top5"]["python_lists"] = dict(
-        _lat(lambda: (np.asarray(vec, np.float32), vals.tolist()), reps * 5),
-        what="the response's Python side alone: the 768-float query list to an array, 5 x 768 values to lists")
+        _lat(lambda: (idxmod._as_vector_np(vec, 768), vals.astype(np.float64).tolist()), reps * 5),
+        what="the response's Python side alone (as Index.query does it): the 768-float query list to an "
+             "array, 5 x 768 values to lists")
     from fastapi.testclient import TestClient
 
     log("bench: latency /search_image")
