@@ -270,3 +270,28 @@ def test_index_devices_spec(monkeypatch):
     utils = import_pkg("ingesting.utils")
     assert utils.index_devices("0,2,4") == [0, 2, 4]
     assert utils.index_devices("", shards=3) == [None, None, None]
+
+
+def test_query_vector_parsing_matches_numpy():
+    """Index.query's request path turns the JSON list into f32 through array('f'); it must give
+    numpy's f32 rounding bit for bit for floats, ints, numpy scalars and tuples, and keep the
+    reference's errors (wrong dimension, all-zero vector) — no GPU needed."""
+    import numpy as np
+    import torch
+
+    idx = import_pkg("index")
+    rng = np.random.default_rng(5)
+    vals = (rng.standard_normal(768) * 10.0 ** rng.integers(-8, 8, 768)).tolist()
+    ref = np.asarray(vals, dtype=np.float32)
+    for v in (vals, tuple(vals), [np.float64(x) for x in vals], np.asarray(vals), torch.tensor(vals, dtype=torch.float64)):
+        got = idx._as_vector_np(v, 768)
+        assert got.shape == (1, 768) and got.dtype == np.float32 and got.flags.c_contiguous
+        assert np.array_equal(got[0], ref)
+    ints = list(range(1, 769))
+    assert np.array_equal(idx._as_vector_np(ints, 768)[0], np.arange(1, 769, dtype=np.float32))
+    with pytest.raises(ValueError):
+        idx._as_vector_np(vals[:10], 768)
+    with pytest.raises(ValueError):
+        idx._as_vector_np([0.0] * 768, 768)
+    with pytest.raises((ValueError, TypeError)):
+        idx._as_vector_np(["a"] * 768, 768)
