@@ -131,7 +131,6 @@ SIGNATURES = {
     "rc_model_set_last_layer": (C.c_int, [_vp, _i32]),
     "rc_model_set_ln_fold": (C.c_int, [_vp, _i32]),
     "rc_model_set_gemm_variant": (C.c_int, [_vp, _i32]),
-    "rc_model_set_attention_form": (C.c_int, [_vp, _i32]),
     "rc_model_timing": (C.c_int, [_vp, _i32]),
     "rc_model_timing_read": (C.c_int, [_vp, _i32, _pd, _pi64, _pd]),
     "rc_model_timing_reset": (C.c_int, [_vp]),

@@ -89,7 +89,6 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // diagnostic builds: RC_GEMM_VARIANT (ablation variants)
-    int attn_form = 0;             // attention kernel form (rc_model_set_attention_form)
     int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -495,21 +494,11 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             break;
         }
         const int ta = m->timers[T_ATTN].begin(s);
-        const float sl2e = scale * 1.4426950408889634f;
-        const int form = (T == 197 && c.heads % 12 == 0) ? m->attn_form : 0;  // v3 forms: 12-head groups divide heads
-        if (form == 1)
-            hipLaunchKernelGGL((attention_v2_kernel<197, 8>), dim3(n * c.heads), dim3(512), 0, s, qkv, attn, T, c.heads, sl2e);
-        else if (form == 2)
-            hipLaunchKernelGGL((attention_v3_kernel<197, 12>), dim3(n * c.heads / 12), dim3(512), 0, s, qkv, attn, T, c.heads, sl2e);
-        else if (form == 3)
-            hipLaunchKernelGGL((attention_v3_kernel<197, 6>), dim3(n * c.heads / 6), dim3(512), 0, s, qkv, attn, T, c.heads, sl2e);
-        else if (form == 4)
-            hipLaunchKernelGGL((attention_v3_kernel<197, 4>), dim3(n * c.heads / 4), dim3(512), 0, s, qkv, attn, T, c.heads, sl2e);
-        else if (T == 197)
-            hipLaunchKernelGGL((attention_v2_kernel<197, 4>), dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+        if (T == 197)
+            hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
         else
-            hipLaunchKernelGGL((attention_v2_kernel<0, 4>), dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+            hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
@@ -833,15 +822,6 @@ int rc_model_set_gemm_variant(rc_model *m, int variant) {
                    "10-13 (ping-pong K-loop forms)");
         std::lock_guard<std::mutex> lk(m->mu);
         m->gemm_variant = variant;
-    });
-}
-
-int rc_model_set_attention_form(rc_model *m, int form) {
-    return guard([&] {
-        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
-        RC_REQUIRE(form >= 0 && form <= 4, RC_ERR_INVALID, "attention form must be 0-4");
-        std::lock_guard<std::mutex> lk(m->mu);
-        m->attn_form = form;
     });
 }
 

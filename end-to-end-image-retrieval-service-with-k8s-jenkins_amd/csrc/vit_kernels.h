@@ -452,11 +452,7 @@ __device__ __forceinline__ void att_scores(const uint8_t *Ks, const bf16x8 (&qf)
 }
 
 // O = P·V of query tile qt (V of the head in LDS), normalised and stored to obase (the image's
-// output rows at this head's columns, row stride H).  ASM_TR (attention_v3): the transposed V
-// reads as inline asm with an explicit lgkmcnt wait per key pair — as builtins, hipcc puts a
-// vmcnt(0) before them while the next head's LDS-DMA is in flight (it cannot tell the buffers
-// apart), which would drain that prefetch.
-template <bool ASM_TR = false>
+// output rows at this head's columns, row stride H)
 __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st)[ATT2_TILES], float sum, int qt,
                                              int tokens, uint16_t *obase, int H) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
@@ -478,28 +474,12 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
             pf[j] = (__bf16)st[t][j];
             pf[j + 4] = (__bf16)st[t + 1][j];
         }
-        if constexpr (ASM_TR) {
-            s16x4 lo[4], hi[4];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[d]) : "v"((uint32_t)(uintptr_t)vrow_addr(t * 16 + g * 4 + qq, d)) : "memory");
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi[d]) : "v"((uint32_t)(uintptr_t)vrow_addr(t * 16 + 16 + g * 4 + qq, d)) : "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const s16x8 vv = {lo[d][0], lo[d][1], lo[d][2], lo[d][3], hi[d][0], hi[d][1], hi[d][2], hi[d][3]};
-                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + g * 4 + qq, d));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + 16 + g * 4 + qq, d));
-                const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
-            }
+        for (int d = 0; d < 4; ++d) {
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + g * 4 + qq, d));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + 16 + g * 4 + qq, d));
+            const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[d], 0, 0, 0);
         }
         asm volatile("" ::: "memory");  // cap the V transposed reads in flight (VGPRs)
     }
@@ -510,16 +490,7 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
         for (int j = 0; j < 4; ++j) pf4[j] = __builtin_bit_cast(short, (__bf16)st[t][j]);
         s16x4 v4[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            if constexpr (ASM_TR)
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v4[d]) : "v"((uint32_t)(uintptr_t)vrow_addr(t * 16 + g * 4 + qq, d)) : "memory");
-            else
-                v4[d] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + g * 4 + qq, d));
-        }
-        if constexpr (ASM_TR) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        for (int d = 0; d < 4; ++d) v4[d] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(vrow_addr(t * 16 + g * 4 + qq, d));
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(v4[d], pf4, o[d], 0, 0, 0);
     }
@@ -536,15 +507,10 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
 
 // TOK > 0: the token count as a compile-time constant (197 for ViT-B/16 at 224),
 // so only the last key tile carries the padding mask; TOK = 0 reads `tokens`.
-// W (waves per block): 4 — query tiles w, w + 4, ...; waves 0-1 stage K, 2-3 V (13 pieces each),
-// 3 blocks per CU; 8 — tiles w, w + 8 (the block's critical path 2 tiles, not 4), waves 0-3 stage K
-// and 4-7 V (7 pieces each, the 2 past the 26 re-load the last piece), 2 blocks per CU.
-template <int TOK, int W = 4>
-__global__ __launch_bounds__(64 * W, W == 4 ? 3 : 2) void attention_v2_kernel(const uint16_t *__restrict__ qkv,
-                                                                            uint16_t *__restrict__ out, int tokens_rt,
-                                                                            int heads, float scale_log2e) {
-    static_assert(W == 4 || W == 8, "4 or 8 waves");
-    constexpr int HD = 64, HALF = W / 2, PPW = (ATT2_TILES * 2 + HALF - 1) / HALF;  // DMA pieces per wave
+template <int TOK>
+__global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+                                                          int tokens_rt, int heads, float scale_log2e) {
+    constexpr int W = 4, HALF = W / 2, HD = 64, PPW = ATT2_TILES * 2 / HALF;  // 13 DMA pieces per wave
     const int tokens = TOK > 0 ? TOK : tokens_rt;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];
     uint8_t *Ks = lds, *Vs = lds + ATT2_ROWS * 128;
@@ -575,7 +541,7 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 3 : 2) void attention_v2_kernel(co
     load_q(wave < nqt ? wave : 0, qf);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-        // wave w < HALF stages K pieces (w PPW + i), the others V; indices past 25 re-load piece 25
+        // waves 0-1 stage K pieces w PPW + i, waves 2-3 the V pieces
         const bool isv = wave >= HALF;
         const int kp = min((wave - (isv ? HALF : 0)) * PPW + i, ATT2_TILES * 2 - 1);
         const int piece = isv ? ATT2_TILES * 2 + kp : kp;
@@ -619,93 +585,6 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 3 : 2) void attention_v2_kernel(co
         if (qt + W < nqt) load_q(qt + W, qn);  // prefetch the next tile's queries
         scores(qf);
         pv_store(qt);
-    }
-}
-
-// Self-attention v3: one block of 8 waves walks HPB consecutive heads of one image, with the
-// head's K / V double-buffered in LDS (2 × 52 KB): while the waves compute head i out of one
-// buffer, the LDS-DMA of head i + 1 lands in the other, so each CU streams K / V under its own
-// MFMA / softmax work instead of alternating load and compute phases block by block (v2: 76 µs
-// per batch-256 launch = 4.1 TB/s for 310 MB, the load and compute phases adding up).  Per head
-// the math is att_scores / att_pv_store on the same tiles as v2 (bit-identical results); wave w
-// takes query tiles w and w + 8.  Per head and wave the loads go in this order: its query tiles'
-// Q (2 × 16 B each), then its 7 DMA pieces of the NEXT head (waves 0-3: K, 4-7: V; indices past
-// the 26 pieces re-load piece 25); one counted wait (vmcnt(7): all but the next head's pieces)
-// and a barrier make head i's K, V and Q visible.  A barrier after the head's last P·V frees its
-// buffer for head i + 2.
-constexpr int ATT3_WAVES = 8, ATT3_PPW = 7;
-template <int TOK, int HPB>
-__global__ __launch_bounds__(512, 1) void attention_v3_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                          int tokens_rt, int heads, float scale_log2e) {
-    constexpr int HD = 64, BUF = 2 * ATT2_ROWS * 128;
-    const int tokens = TOK > 0 ? TOK : tokens_rt;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * BUF];
-    const int H = heads * HD, H3 = 3 * H;
-    const int groups = heads / HPB;
-    const int img = blockIdx.x / groups, h0 = (blockIdx.x % groups) * HPB;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, li = lane & 15;
-    const int nqt = (tokens + 15) / 16;
-    const uint16_t *ibase = qkv + (int64_t)img * tokens * H3;
-    uint16_t *obase_img = out + (int64_t)img * tokens * H;
-    auto bar = [] {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    auto load_q = [&](int h, int qt, bf16x8 (&qv)[2]) {
-        const int q = qt * 16 + li;
-        const uint16_t *qp = ibase + h * HD + (int64_t)(q < tokens ? q : tokens - 1) * H3 + g * 8;
-        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:64"
-                     : "=&v"(qv[0]), "=&v"(qv[1])
-                     : "v"(qp)
-                     : "memory");
-    };
-    auto stage = [&](int h, int b) {  // this wave's 7 DMA pieces of head h into buffer b
-        const uint16_t *base = ibase + h * HD;
-        const bool isv = wave >= ATT3_WAVES / 2;
-#pragma unroll
-        for (int i = 0; i < ATT3_PPW; ++i) {
-            const int kp = min((wave - (isv ? ATT3_WAVES / 2 : 0)) * ATT3_PPW + i, ATT2_TILES * 2 - 1);
-            const int piece = isv ? ATT2_TILES * 2 + kp : kp;
-            const int r = kp * 8 + (lane >> 3);
-            const int pc = lane & 7;
-            const int c = isv ? (pc ^ (((r >> 1) & 3) << 1)) : (pc ^ ((r >> 1) & 7));
-            const int rr = r < tokens ? r : tokens - 1;
-            const uint16_t *src = base + (int64_t)rr * H3 + (isv ? 2 * H : H) + c * 8;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(lds + b * BUF + piece * 1024), 16, 0, 0);
-        }
-    };
-    stage(h0, 0);
-    f32x4 st[ATT2_TILES];
-    float sum = 0.f;
-    for (int i = 0; i < HPB; ++i) {
-        const int h = h0 + i, b = i & 1;
-        const uint8_t *Ks = lds + b * BUF, *Vs = Ks + ATT2_ROWS * 128;
-        const int qt0 = wave, qt1 = wave + ATT3_WAVES;
-        const bool has0 = qt0 < nqt, has1 = qt1 < nqt;
-        bf16x8 q0[2], q1[2];
-        load_q(h, has0 ? qt0 : 0, q0);
-        load_q(h, has1 ? qt1 : 0, q1);
-        if (i + 1 < HPB) {
-            stage(h + 1, b ^ 1);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ATT3_PPW) : "memory");  // all but head h+1's pieces
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        bar();
-        __builtin_amdgcn_sched_barrier(0);
-        uint16_t *ob = obase_img + h * HD;
-        if (has0) {
-            att_scores<TOK>(Ks, q0, tokens, scale_log2e, st, sum);
-            att_pv_store<true>(Vs, st, sum, qt0, tokens, ob, H);
-        }
-        if (has1) {
-            att_scores<TOK>(Ks, q1, tokens, scale_log2e, st, sum);
-            att_pv_store<true>(Vs, st, sum, qt1, tokens, ob, H);
-        }
-        bar();  // every wave is done with buffer b: head i + 2 may land there
     }
 }
 

@@ -364,11 +364,6 @@ class VitMsnEmbedder:
         """Full-batch projection GEMM kernel: 0 auto, 4 ping-pong, 5 / 6 ring (A/B; same bits)."""
         check(self.lib.rc_model_set_gemm_variant(self._h, int(variant)))
 
-    def set_attention_form(self, form: int) -> None:
-        """Attention kernel form (A/B; same bits): 0 one (image, head) per 4-wave block, 1 the same
-        with 8 waves, 2 / 3 / 4 one 8-wave block per 12 / 6 / 4 heads, K / V double-buffered."""
-        check(self.lib.rc_model_set_attention_form(self._h, int(form)))
-
     def timing_reset(self) -> None:
         check(self.lib.rc_model_timing_reset(self._h))
 

@@ -287,10 +287,6 @@ int rc_model_set_ln_fold(rc_model *m, int on);
  * bit-identical across variants: every kernel accumulates K in the same order):
  * 0 auto, 4 ping-pong (one 64-deep K-tile in flight), 5 ring (4 slots of 32-deep
  * K-steps, 2 in flight), 6 ring (3 slots, 1 in flight). */
-// Attention kernel form (A/B knob; bit-identical results): 0 = one (image, head) per block of 4
-// waves, 3 blocks per CU (default); 1 = the same with 8 waves, 2 blocks per CU; 2 / 3 / 4 = one
-// block of 8 waves walks 12 / 6 / 4 heads of an image with K / V double-buffered (ViT-B shapes).
-int rc_model_set_attention_form(rc_model *m, int form);
 int rc_model_set_gemm_variant(rc_model *m, int variant);
 
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).

@@ -315,25 +315,3 @@ def test_ring_gemm_variant_bit_identical(vitmod, weights12, cuda, base, variant)
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(an, bn)
     m.close()
-
-
-
-
-@pytest.mark.parametrize("form", [1, 2, 3, 4])
-def test_attention_forms_bit_identical(vitmod, weights12, cuda, form):
-    """Every attention form — 8 waves per (image, head) block; one 8-wave block walking 12 / 6 / 4
-    heads with K / V double-buffered — computes each query tile exactly as the default form: the
-    same embedding bits (odd batch: the last block's heads, every image's 13 query tiles)."""
-    import torch
-
-    rng = np.random.default_rng(22)
-    imgs = torch.from_numpy(rng.integers(0, 256, (37, 224, 224, 3), dtype=np.uint8))
-    m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=37)
-    a, an = m.embed(imgs)
-    m.set_attention_form(form)
-    b, bn = m.embed(imgs)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b) and torch.equal(an, bn)
-    with pytest.raises(Exception):
-        m.set_attention_form(5)
-    m.close()

@@ -32,10 +32,7 @@ res = {v: {"step_ms": [], **{r: [] for r in roles}} for v in variants}
 ref = None
 for r in range(rounds):
     for v in variants:
-        if os.environ.get("KNOB") == "attn":  # A/B of the attention kernel shape instead
-            m.set_attention_form(v)
-        else:
-            m.set_gemm_variant(v)
+        m.set_gemm_variant(v)
         m.set_parts(parts)
         for _ in range(2):
             m.embed(imgs, out=(raw, nrm))
