@@ -565,9 +565,12 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     // candidate rows, appended with LDS atomics (lgkmcnt only) and flushed to the global lists
     // once at the block's end — a returning global atomic per append would wait for every
     // older vector-memory op, i.e. drain the DMA ring (vmcnt(0)) in the middle of the K loop
-    __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES + SB_TILE * 4 * (1 + I8_SL)];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[QS_NS * STEP_BYTES + SB_TILE * 4 * (1 + I8_SL) + SB_TILE * 12];
     uint32_t *lcnt = reinterpret_cast<uint32_t *>(smem + QS_NS * STEP_BYTES);
     uint32_t *lbuf = lcnt + SB_TILE;
+    // the block's per-query thr, sq, aq: read by each epilogue instead of held in 24 VGPRs, which
+    // the K loop needs (in registers the kernel spilled; from LDS it is 0.7 % faster)
+    float *lq = reinterpret_cast<float *>(lbuf + SB_TILE * I8_SL);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -585,7 +588,13 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     const int nsteps = ntiles * NKT;
     const int64_t row0 = a.r_begin + rt0 * RT;  // a multiple of RT (host check)
     const uint8_t *Rg = (const uint8_t *)a.rows + row0 * ldb;
-    if (tid < SB_TILE) lcnt[tid] = 0u;  // visible to every wave after the K loop's first barrier
+    if (tid < SB_TILE) {  // visible to every wave after the K loop's first barrier
+        const int q = qb * SB_TILE + tid;
+        lcnt[tid] = 0u;
+        lq[tid] = a.thr[q];
+        lq[SB_TILE + tid] = a.sq[q];
+        lq[2 * SB_TILE + tid] = a.aq[q];
+    }
 
     i32x4_t qf[QT][2 * NKT];  // bytes [64 kk + 16 g, +16) of query q0 + 16 qt + li
     const int q0 = qb * SB_TILE + wave * 16 * QT;
@@ -595,23 +604,33 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
         for (int kk = 0; kk < 2 * NKT; ++kk)
             qf[qt][kk] = *reinterpret_cast<const i32x4_t *>((const uint8_t *)a.qh + (int64_t)(q0 + qt * 16 + li) * ldb +
                                                             kk * 64 + g * 16);
-    float thr[QT][4], sq[QT][4], aq[QT][4];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int q = q0 + qt * 16 + 4 * g + j;
-            thr[qt][j] = a.thr[q];
-            sq[qt][j] = a.sq[q];
-            aq[qt][j] = a.aq[q];
-        }
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(thr[qt][j]), "v"(sq[qt][j]), "v"(aq[qt][j]));
-#pragma unroll
         for (int kk = 0; kk < 2 * NKT; ++kk) asm volatile("" ::"v"(qf[qt][kk]));
-    }
+    // an epilogue's per-query operands: 3·QT LDS reads (inline asm: as C++, hipcc would wait for
+    // the whole DMA ring first), retired together
+    auto epi_params = [&](float (&thr)[QT][4], float (&sq)[QT][4], float (&aq)[QT][4]) __attribute__((always_inline)) {
+        f32x4_t v[3][QT];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                asm volatile("ds_read_b128 %0, %1"
+                             : "=v"(v[c][qt])
+                             : "v"((uint32_t)(uintptr_t)(lq + c * SB_TILE + wave * 16 * QT + qt * 16 + 4 * g)));
+        static_assert(QT == 2, "the wait below ties 3 x 2 values");
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[2][0]), "+v"(v[2][1]));
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                thr[qt][j] = v[0][qt][j];
+                sq[qt][j] = v[1][qt][j];
+                aq[qt][j] = v[2][qt][j];
+            }
+    };
 
     uint32_t loff[PPW];
 #pragma unroll
@@ -716,6 +735,8 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
         float exm = ex[0];
 #pragma unroll
         for (int rf = 1; rf < RF; ++rf) exm = fmaxf(exm, ex[rf]);
+        float thr[QT][4], sq[QT][4], aq[QT][4];
+        epi_params(thr, sq, aq);
         bool hit = false;
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
