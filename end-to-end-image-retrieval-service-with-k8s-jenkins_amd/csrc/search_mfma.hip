@@ -732,20 +732,30 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
             sx[rf] = sxv[rf >> 2][rf & 3];
             ex[rf] = exv[rf >> 2][rf & 3];
         }
-        float exm = ex[0];
+        float exm = ex[0], sxmax = sx[0], sxmin = sx[0];
 #pragma unroll
-        for (int rf = 1; rf < RF; ++rf) exm = fmaxf(exm, ex[rf]);
+        for (int rf = 1; rf < RF; ++rf) {
+            exm = fmaxf(exm, ex[rf]);
+            sxmax = fmaxf(sxmax, sx[rf]);
+            sxmin = fminf(sxmin, sx[rf]);
+        }
         float thr[QT][4], sq[QT][4], aq[QT][4];
         epi_params(thr, sq, aq);
-        bool hit = false;
+        // the gate: for every rf, sx[rf]·D[rf] <= sxb·Dmax with Dmax = max_rf D[rf] and sxb = sxmax
+        // (Dmax >= 0) or sxmin (Dmax < 0); f32 products and the fma are monotonic, so the gate
+        // passes whenever one of the lane's 8 per-element conditions below holds (the appends are
+        // decided by those alone): an integer max per accumulator instead of cvt + mul + max
+        bool hit = false, hq[QT][4];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                float m = -INFINITY;
+                int dm = acc[0][qt][j];
 #pragma unroll
-                for (int rf = 0; rf < RF; ++rf) m = fmaxf(m, sx[rf] * (float)acc[rf][qt][j]);
-                hit |= fmaf(exm, aq[qt][j], sq[qt][j] * m) >= thr[qt][j];
+                for (int rf = 1; rf < RF; ++rf) dm = max(dm, acc[rf][qt][j]);
+                const float m = (dm >= 0 ? sxmax : sxmin) * (float)dm;
+                hq[qt][j] = fmaf(exm, aq[qt][j], sq[qt][j] * m) >= thr[qt][j];
+                hit |= hq[qt][j];
             }
         if (__ballot(hit) != 0 && hit) {
             const int64_t rbase = row0 + (int64_t)tile * RT + li;
@@ -753,6 +763,9 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+                    // only the (qt, j) whose gate passed walk their 8 rows (the looser int8 bound
+                    // sends about a quarter of the wave-tiles here)
+                    if (!hq[qt][j]) continue;
                     const int q = q0 + qt * 16 + 4 * g + j;
 #pragma unroll
                     for (int rf = 0; rf < RF; ++rf) {
