@@ -253,6 +253,8 @@ struct rc_index {
     float *qn = nullptr;
     uint64_t *partial = nullptr;
     unsigned *q1_ticket = nullptr;  // query1_kernel's last-block ticket (0 between launches)
+    unsigned *q1_done = nullptr;    // host-coherent completion word of the polled query1 path
+    unsigned q1_seq = 0;
     BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
     KernelTimer timer;   // scan_topk_kernel launches (bytes)
     KernelTimer gtimer;  // filter_gemm_kernel launches (flops)
@@ -449,7 +451,7 @@ void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx,
 // false, enqueuing nothing, when the shape is outside the kernel's range (the caller takes
 // the multi-kernel path).  n_rows >= 1.
 bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int with_values, float *out_scores,
-                  int64_t *out_rows, float *out_values, hipStream_t s) {
+                  int64_t *out_rows, float *out_values, hipStream_t s, volatile unsigned **done, unsigned *seq) {
     if (h->dim > QUERY1_MAX_DIM || h->nch > 6 || topk_cap(k) > 256 || n_rows < 1 || n_rows > QUERY1_MAX_ROWS) return false;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceScope ds(h->device);
@@ -484,6 +486,17 @@ bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int wi
     a.out_scores = out_scores;
     a.out_rows = out_rows;
     a.out_values = out_values;
+    if (done != nullptr) {  // the caller polls a host-coherent completion word (see spin_until)
+        if (h->q1_done == nullptr) {
+            RC_HIP(hipHostMalloc((void **)&h->q1_done, 64, hipHostMallocCoherent));
+            *h->q1_done = 0u;
+        }
+        a.done = h->q1_done;
+        a.seq = ++h->q1_seq;
+        if (a.seq == 0u) a.seq = ++h->q1_seq;  // 0 is the initial word
+        *done = h->q1_done;
+        *seq = a.seq;
+    }
     std::memcpy(a.q, query, (size_t)h->dim * sizeof(float));
     switch (h->dtype) {
         case RC_F32: launch_query1_f32(a, s); break;
@@ -557,6 +570,7 @@ int rc_index_destroy(rc_index *h) {
         dfree(h->qn);
         dfree(h->partial);
         dfree(h->q1_ticket);
+        if (h->q1_done != nullptr) (void)hipHostFree(h->q1_done);
         delete h;
     });
 }

@@ -119,6 +119,8 @@ struct Query1Args {
     float *out_scores;      // [k]
     int64_t *out_rows;      // [k]
     float *out_values;      // [k][dim] (with_values)
+    unsigned *done;         // optional host-coherent word: the finishing block stores seq there last
+    unsigned seq;
     float q[QUERY1_MAX_DIM];
 };
 void launch_query1_f32(const Query1Args &a, hipStream_t s);
@@ -462,6 +464,13 @@ __device__ __forceinline__ void query1_finish(const Query1Args &a) {
                 const float nrm = a.norms[r];
                 for (int c = lane; c < a.dim; c += 64) dst[c] = Elem<T>::load(rows, r * a.ld + c) * nrm;
             }
+        }
+    }
+    if (a.done != nullptr) {  // completion word for a host that polls instead of synchronising
+        __syncthreads();      // every wave's result stores issued and retired
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }

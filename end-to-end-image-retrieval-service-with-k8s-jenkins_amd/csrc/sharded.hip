@@ -16,6 +16,7 @@
 // (score desc, global row asc) — the same order a single rc_index gives.
 // A multi-PROCESS deployment (one process per GPU) uses the same shard row map
 // with an RCCL all-gather instead (sharded.py).
+#include <atomic>
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -28,7 +29,28 @@ namespace rc {
 void index_upsert_gather(rc_index *h, const float *vecs, const int64_t *src_idx, int64_t n, const int64_t *rows,
                          hipStream_t s);
 bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int with_values, float *out_scores,
-                  int64_t *out_rows, float *out_values, hipStream_t s);
+                  int64_t *out_rows, float *out_values, hipStream_t s, volatile unsigned **done = nullptr,
+                  unsigned *seq = nullptr);
+
+// Wait for query1's completion word instead of the stream: the word is stored after the results
+// (system-scope release), so the host can read them the moment it changes, without the
+// end-of-kernel signal round trip.  Every 256 polls the stream is queried, so a faulted or
+// finished launch ends the wait too (a fault surfaces as the stream's error).
+static void spin_until(volatile unsigned *word, unsigned want, hipStream_t s) {
+    for (uint32_t it = 1;; ++it) {
+        if (*word == want) return;
+        if ((it & 255u) == 0u) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) {
+                if (*word == want) return;
+                RC_HIP(hipStreamSynchronize(s));
+                return;
+            }
+            if (e != hipErrorNotReady) RC_HIP(e);
+        }
+        __builtin_ia32_pause();
+    }
+}
 
 // dst[i][:] = src[idx[i]][:] (one wave per row): a remote shard's subset of an upsert
 // batch, made contiguous on the leader so only those rows cross xGMI.
@@ -544,8 +566,18 @@ int rc_sharded_query_host(rc_sharded *h, const float *queries, int nq, int64_t n
             float *hs = (float *)(h->qh + L.sc);
             int64_t *hr = (int64_t *)(h->qh + L.rw);
             float *hv = (float *)(h->qh + L.val);
-            if (index_query1(h->shard[0], queries, n_rows, k, with_values, hs, hr, hv, h->qs)) {
-                RC_HIP(hipStreamSynchronize(h->qs));
+            const char *sp = std::getenv("RC_QUERY1_SPIN");  // "0": synchronise the stream (A/B)
+            const bool spin = !(sp && sp[0] == '0');
+            volatile unsigned *word = nullptr;
+            unsigned want = 0;
+            if (index_query1(h->shard[0], queries, n_rows, k, with_values, hs, hr, hv, h->qs, spin ? &word : nullptr,
+                             &want)) {
+                if (spin) {
+                    spin_until(word, want, h->qs);
+                    std::atomic_thread_fence(std::memory_order_acquire);  // the result reads stay below
+                } else {
+                    RC_HIP(hipStreamSynchronize(h->qs));
+                }
                 std::memcpy(scores, hs, (size_t)k * sizeof(float));
                 std::memcpy(out_rows, hr, (size_t)k * sizeof(int64_t));
                 if (with_values) std::memcpy(values, hv, (size_t)k * h->dim * sizeof(float));

@@ -36,7 +36,8 @@ ix.upsert_tensor([f"r{i}" for i in range(len(X))], torch.from_numpy(X).cuda(), N
 q = np.ascontiguousarray(np.asarray(vec, np.float32)[None])
 ss = ix._set
 out = {}
-for mode, env in (("multi_kernel", {"RC_QUERY1": "0"}), ("one_launch", {"RC_QUERY1_LAUNCHES": "1"})):
+for mode, env in (("multi_kernel", {"RC_QUERY1": "0"}), ("one_launch", {"RC_QUERY1_LAUNCHES": "1"}),
+                  ("stream_sync", {"RC_QUERY1_SPIN": "0"})):
     os.environ.update(env)
     out[f"lib_novalues_{mode}"] = lat(lambda: ss.query_host(q, 5, len(X), False))
     for key in env:
@@ -47,6 +48,7 @@ out.update({
     "index_query_values": lat(lambda: ix.query(vector=vec, top_k=5, include_values=True)),
     "index_query_novalues": lat(lambda: ix.query(vector=vec, top_k=5)),
     "search": lat(lambda: ret.search(ix, vec, top_k=5)),
+    "lib_values_again": lat(lambda: ss.query_host(q, 5, len(X), True)),
     "asarray": lat(lambda: np.asarray(vec, np.float32)),
     "tolist_5x768": lat(lambda: np.zeros((5, 768), np.float32).tolist()),
 })
