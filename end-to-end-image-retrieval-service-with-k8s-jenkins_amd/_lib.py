@@ -111,6 +111,7 @@ SIGNATURES = {
     "rc_sharded_set_filter": (C.c_int, [_vp, _i32]),
     "rc_sharded_create": (C.c_int, [_i32, _pi32, _i32, _i32, _i64, C.POINTER(_vp)]),
     "rc_sharded_destroy": (C.c_int, [_vp]),
+    "rc_sharded_force_remote": (C.c_int, [_vp]),
     "rc_sharded_info": (C.c_int, [_vp, _pi32, _pi64, _pi64]),
     "rc_sharded_shard": (C.c_int, [_vp, _i32, C.POINTER(_vp)]),
     "rc_sharded_grow": (C.c_int, [_vp, _i64]),
@@ -130,7 +131,6 @@ SIGNATURES = {
     "rc_model_set_parts": (C.c_int, [_vp, _i32]),
     "rc_model_set_last_layer": (C.c_int, [_vp, _i32]),
     "rc_model_set_ln_fold": (C.c_int, [_vp, _i32]),
-    "rc_model_set_gemm_variant": (C.c_int, [_vp, _i32]),
     "rc_model_timing": (C.c_int, [_vp, _i32]),
     "rc_model_timing_read": (C.c_int, [_vp, _i32, _pd, _pi64, _pd]),
     "rc_model_timing_reset": (C.c_int, [_vp]),
@@ -141,6 +141,13 @@ SIGNATURES = {
     "rc_jpeg_decoder_destroy": (C.c_int, [_vp]),
     "rc_jpeg_decode": (C.c_int, [_vp, _i32, C.POINTER(C.c_char_p), _pi64, _vp, _pi64, _vp]),
     "rc_jpeg_decode_resized": (C.c_int, [_vp, _i32, C.POINTER(C.c_char_p), _pi64, _i32, _i32, _vp, _vp]),
+}
+
+# diagnostic builds only (tools/build_diag.sh, loaded with RC_LIB_PATH): bound when present,
+# never required of the product library
+DIAG_SIGNATURES = {
+    "rc_diag_set_gemm_variant": (C.c_int, [_vp, _i32]),
+    "rc_diag_set_stamps": (C.c_int, [_vp]),
 }
 
 _lock = threading.Lock()
@@ -174,6 +181,11 @@ def load() -> C.CDLL:
                 raise ImportError(f"{LIB_PATH} does not export {_n}: rebuild the library")
 
             setattr(lib, name, _missing)
+        for name, (res, args) in DIAG_SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is not None:
+                fn.restype = res
+                fn.argtypes = args
         lib.rc_missing_symbols = tuple(missing)
         if lib.rc_abi_version() != 1:
             raise ImportError("libretrieval_core ABI version mismatch")

@@ -83,10 +83,10 @@ __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
 // Values: x = (acc + bias) + residual (or + position), the skinny kernel's order.  HL: the
 // residual stream is the bf16 pair (a.ln_x, a.res_lo); otherwise f32 a.out_f32, plus the
 // bf16 copy in a.ln_x and the partials when a.ln_x is set.  All lanes run the swaps; rows
-// >= M load a clamped row and store nothing.
+// >= mlim (M, or the end of an image-aligned tile's image) load a clamped row and store nothing.
 template <int EPI, int NR>
 __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4 (&A)[NR][2][2], const int (&rows)[NR],
-                                                  int colw, int g, const float4 (&bq)[2][2]) {
+                                                  int colw, int g, const float4 (&bq)[2][2], int mlim) {
     constexpr bool HL = epi_hl(EPI);
     const bool stats = HL ? a.ln_stats != nullptr : a.ln_x != nullptr;
     const int cl = ln_slice_col(g, 0);
@@ -96,7 +96,7 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
     float4 sf[NR][2][2];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        const int rr = rows[r] < a.M ? rows[r] : a.M - 1;
+        const int rr = rows[r] < mlim ? rows[r] : mlim - 1;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int col = colw + 32 * c + cl;
@@ -126,7 +126,7 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
             const int img = row / np, p = row - img * np;
             orow = (int64_t)img * a.tokens + 1 + p;
         }
-        const bool ok = row < a.M;
+        const bool ok = row < mlim;
         float xs[16];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -180,14 +180,17 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
     }
 }
 
-// Epilogue of the 256x256 tile the 8 waves of gemm_pp_kernel / gemm_ring_kernel hold as
-// acc[mq][nq][mi][ni] (wave = grp * 4 + wc: rows grp*128 + mq*64 + mi*16 + li, columns
-// wc*64 + nq*32 + ni*16 + 4g + j).  smem: the ring (>= 128 KB, every read and DMA of the
-// K loop retired by its final barrier); ln_off: the LayerNorm-fold row scales (EPI_*_LN);
-// biasr: the bf16 epilogues' bias, loaded before the K loop.
-template <int EPI, int ABL, int NR = 4>
+// Epilogue of the BM x 256 tile the 8 waves of gemm_pp_kernel hold as acc[mq][nq][mi][ni]
+// (wave = grp * 4 + wc: rows grp*BM/2 + mq*64 + mi*16 + li, columns wc*64 + nq*32 + ni*16 +
+// 4g + j; BM = 224 leaves acc[1][*][3][*] unused).  smem: the ring (>= 128 KB, every read and
+// DMA of the K loop retired by its final barrier); ln_off: the LayerNorm-fold row scales
+// (EPI_*_LN); biasr: the bf16 epilogues' bias, loaded before the K loop; mlim: rows >= mlim
+// are not stored (M, or the end of an image-aligned tile's image).
+template <int EPI, int ABL, int BM = 256, int NR = 4>
 __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2][4][2], uint8_t *smem, int ln_off,
-                                            int m0, int n0, const float4 (&biasr)[2][2], int tid) {
+                                            int m0, int n0, const float4 (&biasr)[2][2], int tid, int mlim) {
+    static_assert(BM == 256 || (BM == 224 && epi_resid(EPI)), "224-row tiles: residual epilogues only");
+    constexpr int HALF = BM / 2, MI1 = (HALF - 64) / 16;  // row blocks of quadrant mq = 1
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wave >> 2, wc = wave & 3;
@@ -253,7 +256,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
                     const int col = n0 + wc * 64 + nq * 32 + (g & 1) * 16 + (g >> 1) * 8;
                     if constexpr ((ABL & 8) != 0) {  // diagnostic: no C stores
                         asm volatile("" ::"v"(u[0][0]), "v"(u[0][1]), "v"(u[1][0]), "v"(u[1][1]));
-                    } else if (row < a.M) {
+                    } else if (row < mlim) {
                         uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)row * (a.ldc ? a.ldc : a.N) + col);
                         const uint4 val = make_uint4(u[0][0], u[0][1], u[1][0], u[1][1]);
                         if constexpr ((ABL & 32) != 0) nt_store16(dst, val);
@@ -322,7 +325,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
             const uint4 v = *reinterpret_cast<const uint4 *>(smem + rl * 512 + ((ch ^ (rl & 31)) << 4));
             if constexpr ((ABL & 8) != 0) {
                 asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-            } else if (m0 + rl < a.M) {
+            } else if (m0 + rl < mlim) {
                 uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8);
                 if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
                 else *dst = v;
@@ -348,25 +351,30 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 const int mi = m4 + r;
-                rows[r] = m0 + grp * 128 + mq * 64 + mi * 16 + li;
+                // a row block past the tile (BM = 224: mq = 1, mi = 3) is masked like a row past M
+                rows[r] = (mq == 1 && mi >= MI1) ? mlim : m0 + grp * HALF + mq * 64 + mi * 16 + li;
 #pragma unroll
                 for (int c = 0; c < 2; ++c)
 #pragma unroll
                     for (int h = 0; h < 2; ++h) A[r][c][h] = acc[mq][c][mi][h];
             }
-            f32_rows_epilogue<EPI, NR>(a, A, rows, n0 + wc * 64, g, bq);
+            f32_rows_epilogue<EPI, NR>(a, A, rows, n0 + wc * 64, g, bq, mlim);
         }
 }
 
 // ----------------------------------------------------------- ping-pong GEMM --
-// 256x256x64 tile, 8 waves in two groups: G0 = waves 0-3 (output rows 0-127),
-// G1 = waves 4-7 (rows 128-255); wave w and w+4 share a SIMD.  Each wave owns
-// 128x64 outputs as 4 quadrants of 64x32 (16 MFMAs per quadrant per K-tile).
+// BM x 256 x 64 tile (BM = 256, or 224 for image-aligned tiles), 8 waves in two groups:
+// G0 = waves 0-3 (output rows 0 .. BM/2), G1 = waves 4-7 (rows BM/2 .. BM); wave w and w+4
+// share a SIMD.  Each wave owns (BM/2) x 64 outputs as 4 quadrants of 64x32 (16 MFMAs per
+// quadrant per K-tile; 12 in the mq = 1 quadrants of a 224-row tile).
 // A K-tile is 4 phases; a phase is an M segment (ds_read this quadrant's
 // fragments, issue this wave's LDS-DMA share of K-tile t+1, lgkmcnt(0)) and a
 // C segment (16 MFMAs), each closed by a block barrier.  G1 runs one segment
 // behind G0 (one extra barrier up front), so on every SIMD one wave's MFMAs
-// overlap its partner's LDS reads / DMA issue / waits.
+// overlap its partner's LDS reads / DMA issue / waits.  A wave's W fragments of a K-tile
+// are read once (phases 0-1) and kept for both row quadrants (24 LDS reads per wave per
+// K-tile instead of 32; round 4 in-model A/B: QKV 178.0 -> 175.3, fc1 274.5 -> 269.9, fc2
+// 297.7 -> 294.4 us per launch).
 // Hazards: DMA for t+1 goes to buffer (t+1)&1 only in phases 0-1 of K-tile t,
 // after the barrier that closes both groups' last reads of K-tile t-1 (every M
 // segment retires its ds_reads before its barrier); every wave waits vmcnt(0)
@@ -379,6 +387,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
 // 48: fc2), 0 = from a.K.  It also names the launch: O-proj (EPI 6, NKT 12) and fc2
 // (EPI 6, NKT 48) share an epilogue but are separate rows in a kernel trace.
 constexpr int PP_BM = 256, PP_BK = 64, PP_STAGE = 2 * PP_BM * PP_BK * 2;  // A tile then W tile, 32 KB each
+constexpr int PP_IMG_BM = 224;  // image-aligned tiles: 197 rows of one image in 14 row blocks of 16
 
 // Diagnostic builds (tools/build_diag.sh) only: s_memrealtime stamps of a workgroup's phases
 // into g_rc_stamps (set by rc_diag_set_stamps; tools/gemm_timeline.py reads them).  The
@@ -404,12 +413,11 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 // tile id -> (row tile, column tile): row-major, or groups of group_m row tiles walked
 // column-major inside a group
-__device__ __forceinline__ void pp_tile_coords(const GemmArgs &a, int tile, int &tm, int &tn) {
+__device__ __forceinline__ void pp_tile_coords(const GemmArgs &a, int ntm, int tile, int &tm, int &tn) {
     const int ntn = a.N / PP_BM;
     tm = tile / ntn;
     tn = tile % ntn;
     if (a.group_m > 0) {
-        const int ntm = (a.M + PP_BM - 1) / PP_BM;
         const int gt = a.group_m * ntn, gi = tile / gt, in = tile - gi * gt;
         const int gm = min(a.group_m, ntm - gi * a.group_m);
         tm = gi * a.group_m + in % gm;
@@ -417,21 +425,17 @@ __device__ __forceinline__ void pp_tile_coords(const GemmArgs &a, int tile, int 
     }
 }
 
-// Prologue + K loop of one 256x256 tile over the K-steps [kb, ke) (64 deep each), adding
-// into acc (which the caller zeroes, or loads with a partial sum of the K-steps before kb:
-// the MFMA chain then continues exactly as if it had run from 0).  The ping-pong schedule
-// described above gemm_pp_kernel.  smem: the 2-stage ring (2 * PP_STAGE) then, for the
-// LayerNorm-fold consumers, the tile rows' (rstd, -rstd*mu) at 2 * PP_STAGE.  On return
-// every wave has passed the loop's last barrier (the ring is free for the epilogue).
-// KL (K-loop form, bit-identical results): bit 0 = the wave's W fragments of a K-step are read
-// once and kept for both of its halves (24 LDS reads per wave per K-step instead of 32); bit 1 =
-// the LDS-DMA as buffer loads (one lane offset for all 8 pieces, the piece's rows in the scalar
-// offset, the K-step in the descriptor: no per-piece 64-bit address arithmetic).
-template <int EPI, int ABL, int KL = 0>
+// Prologue + K loop of one BM x 256 tile over the K-steps [kb, ke) (64 deep each), adding
+// into acc (which the caller zeroes).  The ping-pong schedule described above.  smem: the
+// 2-stage ring (2 * PP_STAGE) then, for the LayerNorm-fold consumers, the tile rows'
+// (rstd, -rstd*mu) at 2 * PP_STAGE.  On return every wave has passed the loop's last barrier
+// (the ring is free for the epilogue).
+template <int EPI, int ABL, int BM>
 __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m0, int n0, int kb, int ke,
                                          f32x4 (&acc)[2][2][4][2], int tid, int64_t sb = -1) {
-    constexpr bool WKEEP = (KL & 1) != 0, BUF = (KL & 2) != 0;
-    constexpr int BM = PP_BM, BK = PP_BK, A_BYTES = BM * BK * 2, STAGE = PP_STAGE;
+    constexpr int BK = PP_BK, A_BYTES = PP_BM * BK * 2, STAGE = PP_STAGE;
+    constexpr int HALF = BM / 2, MI1 = (HALF - 64) / 16;  // row blocks of quadrant mq = 1
+    constexpr int A_PIECES = BM / 8;                      // 1-KB pieces (8 rows x 128 B) of the A tile
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wave >> 2, wc = wave & 3;
@@ -441,28 +445,19 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
     const uint16_t *Wg = a.W + (int64_t)n0 * K;
 
     // 64 pieces of 1 KB per K-tile (A: 0-31, W: 32-63); wave w owns pieces w + 8 i.  Piece rows
-    // r = 8 w + 64 (i % 4) + lane / 8: the chunk swizzle (r >> 1) & 7 does not depend on i.
-    const int lr = wave * 8 + (lane >> 3);
-    const uint32_t voff = (uint32_t)(lr * K + (((lane & 7) ^ ((lr >> 1) & 7)) << 3)) * 2u;
+    // r = 8 w + 64 (i % 4) + lane / 8: the chunk swizzle (r >> 1) & 7 does not depend on i.  A
+    // 224-row tile skips the A pieces past its rows (28-31: waves 4-7 at i = 3; wave-uniform).
     auto stage4 = [&](int buf, int k0, int i0) {
         uint8_t *base = smem + buf * STAGE;
-        if constexpr (BUF) {
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc((void *)((i0 < 4 ? Ag : Wg) + k0), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-            for (int i = i0; i < i0 + 4; ++i)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(base + (wave + 8 * i) * 1024), 16, voff,
-                                                         (i & 3) * 64 * K * 2, 0, 0);
-        } else {
-#pragma unroll
-            for (int i = i0; i < i0 + 4; ++i) {
-                const int piece = wave + 8 * i;
-                const bool is_a = i < 4;
-                const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
-                const int c = (lane & 7) ^ ((r >> 1) & 7);
-                const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
-                __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
-            }
+        for (int i = i0; i < i0 + 4; ++i) {
+            const int piece = wave + 8 * i;
+            const bool is_a = i < 4;
+            if (is_a && piece >= A_PIECES) continue;
+            const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
+            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
         }
     };
     auto bar = [] {
@@ -483,7 +478,7 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
     if (sb >= 0) RC_STAMP(sb, RC_NOW());
     if (grp == 1) bar();  // stagger: G1 one segment behind
 
-    bf16x8 af[4][2], wf[WKEEP ? 2 : 1][2][2];  // [mi][s], [nq (W kept) or 0][ni][s]
+    bf16x8 af[4][2], wf[2][2][2];  // [mi][s], [nq][ni][s]
 #pragma nounroll
     for (int kt = kb; kt < ke; ++kt) {
         const int cur = (kt - kb) & 1;
@@ -494,25 +489,27 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
         for (int p = 0; p < 4; ++p) {
             const int mq = p >> 1;                 // quadrant rows
             const int nq = (p == 1 || p == 2);     // snake: (0,0) (0,1) (1,1) (1,0)
+            const int nmi = mq == 0 ? 4 : MI1;     // row blocks of this quadrant (compile-time)
             // ---- M segment
             if (p == 0 || p == 2) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const int r = grp * 128 + mq * 64 + mi * 16 + li;
+                        if (mi >= nmi) continue;
+                        const int r = grp * HALF + mq * 64 + mi * 16 + li;
                         const int c = s * 4 + g;
                         af[mi][s] = *reinterpret_cast<const bf16x8 *>(As + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                     }
             }
-            if (!WKEEP || p < 2) {
+            if (p < 2) {
 #pragma unroll
                 for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int r = wc * 64 + nq * 32 + ni * 16 + li;
                         const int c = s * 4 + g;
-                        wf[WKEEP ? nq : 0][ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                        wf[nq][ni][s] = *reinterpret_cast<const bf16x8 *>(Ws + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
                     }
             }
             if (!(ABL & 1) && more && p < 2) stage4(cur ^ 1, kofs(kt + 1), p * 4);
@@ -526,12 +523,14 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                    for (int ni = 0; ni < 2; ++ni)
+                    for (int ni = 0; ni < 2; ++ni) {
+                        if (mi >= nmi) continue;
                         if constexpr (!(ABL & 2))
-                            acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[WKEEP ? nq : 0][ni][s], af[mi][s],
+                            acc[mq][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nq][ni][s], af[mi][s],
                                                                                          acc[mq][nq][mi][ni], 0, 0, 0);
                         else
-                            asm volatile("" ::"v"(wf[WKEEP ? nq : 0][ni][s]), "v"(af[mi][s]));
+                            asm volatile("" ::"v"(wf[nq][ni][s]), "v"(af[mi][s]));
+                    }
             __builtin_amdgcn_s_setprio(0);
             bar();
         }
@@ -555,15 +554,23 @@ __device__ __forceinline__ void pp_bias_regs(const GemmArgs &a, int n0, float4 (
     }
 }
 
-template <int EPI, int ABL = 0, int NKT = 0, int KL = 0>
+// BM = 256: row tile tm covers rows [256 tm, 256 tm + 256).  BM = 224 (image-aligned, a.row_step
+// = tokens): row tile tm covers the rows of image tm, [tm·row_step, tm·row_step + row_step), so
+// a batch of n images is n × N/256 tiles — for the N = 768 residual producers (O-proj, fc2)
+// exactly 3 rounds of 256 CUs at n = 256, where 256-row tiles (197 × 3 = 591 tiles) left the
+// third round 31 % full.  The extra rows a tile computes (224 − 197) are never stored.
+template <int EPI, int ABL = 0, int NKT = 0, int BM = PP_BM>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     // LayerNorm-fold consumers keep the tile rows' (rstd, -rstd*mu) behind the ring (one
     // __shared__ array: a second one would make hipcc drain the LDS-DMA queue every K-step)
     constexpr int LN_LDS = epi_ln(EPI) ? PP_BM * 8 : 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * PP_STAGE + LN_LDS];
+    const int step = BM == PP_BM ? PP_BM : a.row_step;
+    const int ntm = (a.M + step - 1) / step;
     int tm, tn;
-    pp_tile_coords(a, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
-    const int m0 = tm * PP_BM, n0 = tn * PP_BM;
+    pp_tile_coords(a, ntm, xcd_remap(blockIdx.x, gridDim.x), tm, tn);
+    const int m0 = tm * step, n0 = tn * PP_BM;
+    const int mlim = min(m0 + step, a.M);
 
     f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -577,10 +584,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     const int64_t sb = (int64_t)blockIdx.x * 64;
     RC_STAMP(sb, RC_NOW());
     RC_STAMP(sb + 4, (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) | ((uint64_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32));
-    RC_STAMP(sb + 5, (uint64_t)(m0 / PP_BM) | ((uint64_t)(n0 / PP_BM) << 32));
+    RC_STAMP(sb + 5, (uint64_t)tm | ((uint64_t)tn << 32));
     float4 biasr[2][2];
     pp_bias_regs<EPI>(a, n0, biasr, threadIdx.x);
-    pp_kloop<EPI, ABL, KL>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, threadIdx.x, sb + 1);
+    pp_kloop<EPI, ABL, BM>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, threadIdx.x, sb + 1);
     if constexpr ((ABL & 4) != 0) {
 #pragma unroll
         for (int a0 = 0; a0 < 2; ++a0)
@@ -592,184 +599,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                     for (int a3 = 0; a3 < 2; ++a3) asm volatile("" ::"v"(acc[a0][a1][a2][a3]));
         return;
     }
-    pp_epilogue<EPI, ABL>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, threadIdx.x);
+    pp_epilogue<EPI, ABL, BM>(a, acc, smem, 2 * PP_STAGE, m0, n0, biasr, threadIdx.x, mlim);
     RC_STAMP(sb + 3, RC_NOW());
-}
-
-// --------------------------------------------------------------- ring GEMM --
-// The ping-pong tile (256x256, 8 waves in two staggered groups, the same wave ->
-// output map and epilogue) with a deeper DMA pipeline.  gemm_pp_kernel keeps one
-// 64-deep K-tile in flight and drains it (vmcnt(0)) every K-tile: the L2 -> LDS fill
-// is latency-bound (its no-MFMA ablation moves fc1's 1.86 GB in 137 us, 53 GB/s per
-// CU, against the ~70 GB/s per CU an LDS-DMA gather from L2 reaches with ~72 KB in
-// flight).  Here the ring has NS slots of one 32-deep K-step (A 256 x 32 + W 256 x 32,
-// 32 KB, 64-B rows with the 16-B chunk XOR ((row >> 3) & 1) << 1 of gemm_w2_kernel:
-// conflict-free ds_read_b128 fragments) and NS - 2 K-steps stay in flight across
-// every barrier: counted vmcnt, never 0 inside the loop.
-// A K-step is 2 phases (rows mq*64.. of the wave's 128); a phase is an M segment
-// (the phase's 4 A fragments, at phase 0 also the step's 4 W fragments, kept for both
-// phases; this wave's 2 DMA pieces of step t + NS - 1) and a C segment (16 MFMAs),
-// each closed by a barrier; G1 runs one segment behind G0.
-// Hazards: step t + NS - 1 goes to slot (t - 1) % NS, issued in step t's M segments
-// — after the barrier that closed both groups' last reads of step t - 1 (their phase-1
-// M segments).  Step t + 1 is read first by G0 in its (t + 1, 0) M segment; every
-// wave waits for its own pieces of step t + 1 (vmcnt(4 (NS - 3)) after issuing step
-// t + NS - 1's last pieces) in its (t, 1) M segment, and the barrier closing G1's (t, 1)
-// M segment precedes G0's (t + 1, 0) M segment.
-// NS = 5 (round 4): the ring takes all 160 KB and keeps 3 K-steps (96 KB) in flight; the LayerNorm
-// row scales then wait in a register (tid < 256: its row) through the K loop and go to LDS at
-// 128 KB once the loop is over (the epilogue stages at most 128 KB from offset 0).
-template <int EPI, int NS, int NKS = 0>
-__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
-    constexpr int BM = 256, BN = 256, BK = 32;
-    constexpr int A_BYTES = BM * BK * 2, SLOT = 2 * A_BYTES;  // 16 KB + 16 KB
-    constexpr int LN_LDS = epi_ln(EPI) ? BM * 8 : 0;
-    constexpr bool LN_REG = NS * SLOT > 128 * 1024;  // no room past the ring: scales in registers
-    // the epilogue stages up to 128 KB from offset 0: the LayerNorm row scales live past both
-    constexpr int LN_OFF = LN_REG ? 128 * 1024 : (NS * SLOT > 128 * 1024 ? NS * SLOT : 128 * 1024);
-    constexpr int SMEM = LN_REG ? NS * SLOT : LN_OFF + LN_LDS;
-    static_assert(NS >= 3 && NS <= 5 && SMEM <= 160 * 1024 && (!LN_REG || LN_OFF + LN_LDS <= SMEM), "ring of 3..5 slots");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    const int g = lane >> 4, li = lane & 15;
-
-    const int ntn = a.N / BN;
-    const int nwg = gridDim.x, orig = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-    int tm = tile / ntn, tn = tile % ntn;
-    if (a.group_m > 0) {
-        const int ntm = (a.M + BM - 1) / BM;
-        const int gt = a.group_m * ntn, gi = tile / gt, in = tile - gi * gt;
-        const int gm = min(a.group_m, ntm - gi * a.group_m);
-        tm = gi * a.group_m + in % gm;
-        tn = in / gm;
-    }
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int K = a.K;
-    const uint16_t *Ag = a.A + (int64_t)m0 * K;
-    const uint16_t *Wg = a.W + (int64_t)n0 * K;
-
-    // 32 pieces of 1 KB (16 rows x 64 B) per slot: A rows 0-255 = pieces 0-15, W = 16-31;
-    // wave w issues pieces w + 8 i, i = 0..3 (two per phase).  Lane l writes LDS bytes
-    // [16 l, 16 l + 16): row l >> 2 of the piece, stored chunk l & 3 = source chunk
-    // (l & 3) ^ (((l >> 5) & 1) << 1) (the row's bit 3 is bit 5 of the lane).
-    const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
-    auto stage2 = [&](int slot, int k0, int i0) {
-        uint8_t *base = smem + slot * SLOT;
-#pragma unroll
-        for (int i = i0; i < i0 + 2; ++i) {
-            const int piece = wave + 8 * i;
-            const bool is_a = piece < 16;
-            const uint16_t *src = (is_a ? Ag + (int64_t)(piece * 16 + prow) * K : Wg + (int64_t)((piece - 16) * 16 + prow) * K);
-            __builtin_amdgcn_global_load_lds((const void *)(src + k0 + pchunk * 8), (lds_void_t *)(base + piece * 1024), 16,
-                                             0, 0);
-        }
-    };
-    auto bar = [] {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    // fragment of rows r0 + li (r0 % 16 == 0), k chunk g: 16 B at row * 64 + (g ^ ((li >> 3) & 1) << 1) * 16
-    const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
-
-    f32x4 acc[2][2][4][2];
-#pragma unroll
-    for (int a0 = 0; a0 < 2; ++a0)
-#pragma unroll
-        for (int a1 = 0; a1 < 2; ++a1)
-#pragma unroll
-            for (int a2 = 0; a2 < 4; ++a2)
-#pragma unroll
-                for (int a3 = 0; a3 < 2; ++a3) acc[a0][a1][a2][a3] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 biasr[2][2];
-    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-                biasr[nq][ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wc * 64 + nq * 32 + ni * 16 + 4 * g);
-    }
-
-    const int nk = NKS > 0 ? NKS : K / BK;
-    // prologue: steps 0 .. NS - 2 in flight, wait for step 0
-#pragma unroll
-    for (int t = 0; t < NS - 1; ++t) {
-        if (t < nk) {
-            stage2(t, t * BK, 0);
-            stage2(t, t * BK, 2);
-        }
-    }
-    float2 ln_scale = make_float2(0.f, 0.f);
-    if constexpr (epi_ln(EPI)) {
-        if (tid < BM) {
-            ln_scale = ln_row_scale(a.ln_stats + (int64_t)(m0 + tid) * LN_STRIDE, a.ln_eps);
-            if constexpr (!LN_REG) *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) = ln_scale;
-        }
-    }
-    if (nk >= NS - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NS - 2)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (grp == 1) bar();  // stagger: G1 one segment behind
-
-    bf16x8 af[4], wf[2][2];  // [mi], [nq][ni]
-#pragma nounroll
-    for (int t = 0; t < nk; ++t) {
-        const int cur = t % NS;
-        const uint8_t *As = smem + cur * SLOT;
-        const uint8_t *Ws = As + A_BYTES;
-        const int tn_ = t + NS - 1;  // the step whose DMA this step issues
-        const int nslot = (t + NS - 1) % NS;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            // ---- M segment
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int r = grp * 128 + p * 64 + mi * 16 + li;
-                af[mi] = *reinterpret_cast<const bf16x8 *>(As + r * 64 + fchunk);
-            }
-            if (p == 0) {
-#pragma unroll
-                for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                    for (int ni = 0; ni < 2; ++ni) {
-                        const int r = wc * 64 + nq * 32 + ni * 16 + li;
-                        wf[nq][ni] = *reinterpret_cast<const bf16x8 *>(Ws + r * 64 + fchunk);
-                    }
-            }
-            if (tn_ < nk) stage2(nslot, tn_ * BK, 2 * p);
-            if (p == 1) {  // this wave's pieces of step t + 1 have landed (the younger steps may fly)
-                const int younger = min(NS - 2, max(0, nk - t - 2));  // steps issued after t + 1
-                if (younger >= 3 && NS >= 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * 3) : "memory");
-                else if (younger == 2 && NS >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * 2) : "memory");
-                else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * 1) : "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            bar();
-            // ---- C segment: rows p*64 .. +64 of the wave's 128, all 64 columns
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-                    for (int ni = 0; ni < 2; ++ni)
-                        acc[p][nq][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nq][ni], af[mi], acc[p][nq][mi][ni], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            bar();
-        }
-    }
-    if (grp == 0) bar();  // balance the stagger barrier
-    if constexpr (LN_REG && epi_ln(EPI)) {  // the ring is free (every DMA waited for, every read retired)
-        if (tid < BM) *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) = ln_scale;
-        __syncthreads();
-    }
-    pp_epilogue<EPI, 0>(a, acc, smem, LN_OFF, m0, n0, biasr, threadIdx.x);
 }
 
 // Epilogue of a 128 x 256 tile held as acc[mi][ni] by 4 waves (wave w: columns
@@ -838,7 +669,7 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
 #pragma unroll
                 for (int h = 0; h < 2; ++h) A[r][c][h] = acc[h4 * 4 + r][2 * c + h];
         }
-        f32_rows_epilogue<EPI, 4>(a, A, rows, n0 + wave * 64, g, bq);
+        f32_rows_epilogue<EPI, 4>(a, A, rows, n0 + wave * 64, g, bq, a.M);
     }
 }
 
@@ -1268,53 +1099,26 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
     if (ok && g == 0) *reinterpret_cast<float2 *>(ln_stats + (int64_t)row * LN_STRIDE + 2 * blk) = st;
 }
 
-// Kernel choice: 4 = ping-pong 256x256, 8 = two-workgroup 128x256, 9 = skinny
-// (M <= 256), 0 = auto.  Auto follows interleaved A/B timings on the batch-256 shapes
-// (tools/gemm_calib.py): ping-pong everywhere except the short square projections.
-// (Rounds 1-2 also measured a 128x128 4-wave kernel, a 256x256 / 128x256 single-
-// barrier kernel, a persistent kernel, Stream-K and a deferred-store persistent
-// kernel: each lost on every shape and was removed.)
-enum GemmVariant {
-    GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_RING4 = 5, GEMM_RING3 = 6, GEMM_W2 = 8, GEMM_SKINNY = 9,
-    // ping-pong with an explicit K-loop form KL = variant - 10 (A/B; GEMM_PINGPONG = the default form)
-    GEMM_PP_KL0 = 10, GEMM_PP_KL1 = 11, GEMM_PP_KL2 = 12, GEMM_PP_KL3 = 13,
-    GEMM_RING5 = 7  // the ring kernel with 5 slots (3 K-steps, 96 KB, in flight)
-};
-// the ping-pong K-loop form the product runs: W kept (r04b in-model A/B, tools/gemm_ab.py, median of
-// 3 interleaved rounds: QKV 178.0 -> 175.3, fc1 274.5 -> 269.9, fc2 297.7 -> 294.4 us per launch,
-// step 10.08 -> 10.02 ms; the buffer-load DMA (KL 2) lost on fc2, 297.7 -> 313.1)
-constexpr int GEMM_PP_KL_DEFAULT = 1;
+// Kernel choice: 4 = ping-pong 256x256, 10 = ping-pong on image-aligned 224-row tiles,
+// 8 = two-workgroup 128x256, 9 = skinny (M <= 256), 0 = auto.  Auto follows interleaved
+// A/B timings on the batch-256 shapes.  (Rounds 1-4 also measured a 128x128 4-wave kernel, a
+// 256x256 / 128x256 single-barrier kernel, persistent and Stream-K kernels, a deferred-store
+// persistent kernel, an LDS ring of 3-5 slots and buffer-load DMA: each lost or tied and was
+// removed; the forms live on in tools/gemm_lab.)
+enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9, GEMM_PP_IMG = 10 };
 
-inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue = false) {
+inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
-    // Short square projections (O-proj, patch embed: N = K = 768) finish in
-    // ~2.3 rounds of 256x256 tiles and carry a heavy f32 epilogue (residual /
-    // position read + write): the two-workgroup kernel overlaps that epilogue
-    // with the co-resident workgroup's MFMAs (O-proj 96 -> 89 us at batch 256,
-    // tools/gemm_calib.py).  Everything else streams K at 128 flop/B: ping-pong.
-    // Round 3: with every f32 epilogue storing straight from the accumulators (no LDS staging,
-    // no barrier) the two-workgroup kernel also wins O-proj on the bf16-pair stream: 141 ->
-    // 125 us per launch, -0.6 % step time at parts = 2 (profiles/r03/r03d_part_lag_w2_ab.log;
-    // fc2, K = 3072, stays on the ping-pong kernel: 305 -> 326 us there).
-    (void)pair_epilogue;
+    // The residual producers (O-proj, fc2: N = 768, every row tile one image) on image-aligned
+    // tiles: a batch is n x 3 tiles, whole rounds of the 256 CUs (197-row images make 256-row
+    // tiles 2.31 rounds at any batch).
+    if (a.row_step > 0 && a.N % 256 == 0 && !patch_epilogue) return GEMM_PP_IMG;
+    // Short square projections without image alignment (N = K = 768) finish in ~2.3 rounds of
+    // 256x256 tiles and carry a heavy epilogue: the two-workgroup kernel overlaps it with the
+    // co-resident workgroup's MFMAs.  Everything else streams K at 128 flop/B: ping-pong.
     if (a.N <= 768 && a.K <= 768) return GEMM_W2;
     return GEMM_PINGPONG;
-}
-
-// The model's A/B knob (rc_model_set_gemm_variant): 4 / 5 / 6 force that kernel on every full-batch
-// projection; the ring of 5 slots (7) and the ping-pong K-loop forms (10-13) replace the ping-pong
-// kernel only where auto picks it (O-proj keeps its two-workgroup kernel, small batches the skinny)
-inline int gemm_model_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool pair_epilogue) {
-    bool pp_only = variant == GEMM_RING5 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3);
-#if defined(RC_GEMM_ABLATION)
-    pp_only = pp_only || variant >= 100;  // ping-pong ablations (diagnostic builds) on ping-pong shapes only
-#endif
-    if (pp_only) {
-        const int p = gemm_pick(a, GEMM_AUTO, patch_epilogue, pair_epilogue);
-        return p == GEMM_PINGPONG ? variant : p;
-    }
-    return variant;
 }
 
 // Ping-pong tile order: groups of 8 row tiles (column-major inside a group) when
@@ -1340,48 +1144,33 @@ inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
 // rows the A buffer must provide beyond M (the kernels read whole tiles)
 inline int gemm_row_pad() { return 256; }
 
+template <int EPI, int ABL, int BM>
+void launch_pp(const GemmArgs &a, int ntm, hipStream_t s) {
+    const dim3 gr(ntm * (a.N / 256)), bl(512);
+    if (a.K == 768) hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, 12, BM>), gr, bl, 0, s, a);
+    else if (a.K == 3072) hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, 48, BM>), gr, bl, 0, s, a);
+    else hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, 0, BM>), gr, bl, 0, s, a);
+}
+
 template <int EPI>
 void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
-    const int pick = gemm_pick(a, variant, epi_patch(EPI), epi_hl(EPI));
+    const int pick = gemm_pick(a, variant, epi_patch(EPI));
     RC_REQUIRE(a.ldc == 0 || (a.ldc >= a.N && epi_bf16_out(EPI)), RC_ERR_UNSUPPORTED,
                "an output row stride (ldc) needs a bf16 epilogue");
     if constexpr (epi_hl(EPI)) {
         RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
     }
     if constexpr (epi_ln(EPI)) {
-        bool ln_ok = pick == GEMM_PINGPONG || (pick >= GEMM_PP_KL0 && pick <= GEMM_PP_KL3) || pick == GEMM_RING5 ||
-                     pick == GEMM_RING4 || pick == GEMM_RING3 || pick == GEMM_SKINNY;
+        bool ln_ok = pick == GEMM_PINGPONG || pick == GEMM_SKINNY;
 #if defined(RC_GEMM_ABLATION)
         ln_ok = ln_ok || (pick >= 100 && pick < 200);  // gemm_pp_kernel<EPI, ABL>
 #endif
-        RC_REQUIRE(ln_ok && a.ln_c &&
-                       a.ln_stats, RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers run on the ping-pong, ring or skinny kernel");
+        RC_REQUIRE(ln_ok && a.ln_c && a.ln_stats, RC_ERR_UNSUPPORTED,
+                   "LayerNorm-fold consumers run on the ping-pong or skinny kernel");
     }
     switch (pick) {
-        case GEMM_RING5:
-        case GEMM_RING4:
-        case GEMM_RING3: {
-            RC_REQUIRE(a.N % 256 == 0 && a.K % 32 == 0, RC_ERR_UNSUPPORTED, "ring GEMM: N % 256 == 0, K % 32 == 0");
-            a.group_m = gemm_group_m(a);
-            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
-            const dim3 gr(ntm * ntn), bl(512);
-            if (pick == GEMM_RING5) {
-                if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 5, 24>), gr, bl, 0, s, a);
-                else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 5, 96>), gr, bl, 0, s, a);
-                else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 5>), gr, bl, 0, s, a);
-            } else if (pick == GEMM_RING4) {
-                if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 24>), gr, bl, 0, s, a);
-                else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 96>), gr, bl, 0, s, a);
-                else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4>), gr, bl, 0, s, a);
-            } else {
-                if (a.K == 768) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 24>), gr, bl, 0, s, a);
-                else if (a.K == 3072) hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 96>), gr, bl, 0, s, a);
-                else hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3>), gr, bl, 0, s, a);
-            }
-            break;
-        }
         case GEMM_W2: {
             if constexpr (!epi_ln(EPI)) {
                 RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
@@ -1404,27 +1193,22 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
-        case GEMM_PINGPONG:
-        case GEMM_PP_KL0:
-        case GEMM_PP_KL1:
-        case GEMM_PP_KL2:
-        case GEMM_PP_KL3: {
+        case GEMM_PINGPONG: {
             RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
             a.group_m = gemm_group_m(a);
-            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
-            const dim3 gr(ntm * ntn), bl(512);
-            const int kl = pick == GEMM_PINGPONG ? GEMM_PP_KL_DEFAULT : pick - GEMM_PP_KL0;
-            auto go = [&](auto klc) {
-                constexpr int KLV = decltype(klc)::value;
-                if (a.K == 768) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 12, KLV>), gr, bl, 0, s, a);
-                else if (a.K == 3072) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 48, KLV>), gr, bl, 0, s, a);
-                else hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0, 0, KLV>), gr, bl, 0, s, a);
-            };
-            switch (kl) {
-                case 1: go(std::integral_constant<int, 1>{}); break;
-                case 2: go(std::integral_constant<int, 2>{}); break;
-                case 3: go(std::integral_constant<int, 3>{}); break;
-                default: go(std::integral_constant<int, 0>{}); break;
+            launch_pp<EPI, 0, PP_BM>(a, (a.M + PP_BM - 1) / PP_BM, s);
+            break;
+        }
+        case GEMM_PP_IMG: {
+            if constexpr (epi_resid(EPI)) {
+                // a tile computes 224 rows from its image's first row: the A buffer must hold
+                // row_step·ntm + (224 − row_step) rows (the model's workspace pads 256)
+                RC_REQUIRE(a.N % 256 == 0 && a.row_step > 0 && a.row_step <= PP_IMG_BM && a.row_step > PP_IMG_BM - 64,
+                           RC_ERR_UNSUPPORTED, "image-aligned GEMM: N % 256 == 0, 160 < row_step <= 224");
+                a.group_m = 0;
+                launch_pp<EPI, 0, PP_IMG_BM>(a, (a.M + a.row_step - 1) / a.row_step, s);
+            } else {
+                throw Error(RC_ERR_UNSUPPORTED, "image-aligned GEMM tiles: residual epilogues only");
             }
             break;
         }
@@ -1443,22 +1227,21 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         case 100 + 0: case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
         case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: {
             a.group_m = gemm_group_m(a);  // the product tile order
-            const int ntm = (a.M + 255) / 256, ntn = a.N / 256;
-            const dim3 gr(ntm * ntn), bl(512);
+            const int ntm = (a.M + 255) / 256;
             switch (variant - 100) {
-                case 0: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 0>), gr, bl, 0, s, a); break;
-                case 1: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1>), gr, bl, 0, s, a); break;
-                case 2: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 2>), gr, bl, 0, s, a); break;
-                case 3: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 3>), gr, bl, 0, s, a); break;
-                case 4: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 4>), gr, bl, 0, s, a); break;
-                case 5: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 5>), gr, bl, 0, s, a); break;
-                case 6: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 6>), gr, bl, 0, s, a); break;
-                case 8: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 8>), gr, bl, 0, s, a); break;
-                case 16: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 16>), gr, bl, 0, s, a); break;
-                case 24: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 24>), gr, bl, 0, s, a); break;
-                case 32: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 32>), gr, bl, 0, s, a); break;
-                case 64: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 64>), gr, bl, 0, s, a); break;
-                case 96: hipLaunchKernelGGL((gemm_pp_kernel<EPI, 96>), gr, bl, 0, s, a); break;
+                case 0: launch_pp<EPI, 0, PP_BM>(a, ntm, s); break;
+                case 1: launch_pp<EPI, 1, PP_BM>(a, ntm, s); break;
+                case 2: launch_pp<EPI, 2, PP_BM>(a, ntm, s); break;
+                case 3: launch_pp<EPI, 3, PP_BM>(a, ntm, s); break;
+                case 4: launch_pp<EPI, 4, PP_BM>(a, ntm, s); break;
+                case 5: launch_pp<EPI, 5, PP_BM>(a, ntm, s); break;
+                case 6: launch_pp<EPI, 6, PP_BM>(a, ntm, s); break;
+                case 8: launch_pp<EPI, 8, PP_BM>(a, ntm, s); break;
+                case 16: launch_pp<EPI, 16, PP_BM>(a, ntm, s); break;
+                case 24: launch_pp<EPI, 24, PP_BM>(a, ntm, s); break;
+                case 32: launch_pp<EPI, 32, PP_BM>(a, ntm, s); break;
+                case 64: launch_pp<EPI, 64, PP_BM>(a, ntm, s); break;
+                case 96: launch_pp<EPI, 96, PP_BM>(a, ntm, s); break;
             }
             break;
         }

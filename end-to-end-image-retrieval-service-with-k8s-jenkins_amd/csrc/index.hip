@@ -252,7 +252,6 @@ struct rc_index {
     int ws_nq = 0, ws_k = 0, ws_nblk = 0;
     float *qn = nullptr;
     uint64_t *partial = nullptr;
-    unsigned *q1_ticket = nullptr;  // query1_kernel's last-block ticket (0 between launches)
     unsigned *q1_done = nullptr;    // host-coherent completion word of the polled query1 path
     unsigned q1_seq = 0;
     BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
@@ -456,10 +455,6 @@ bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int wi
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceScope ds(h->device);
     ensure_workspace(h, 1, k);
-    if (h->q1_ticket == nullptr) {
-        h->q1_ticket = (unsigned *)dmalloc(sizeof(unsigned));
-        RC_HIP(hipMemsetAsync(h->q1_ticket, 0, sizeof(unsigned), s));
-    }
     Query1Args a{};
     a.rows = h->rows;
     a.norms = h->norms;
@@ -474,15 +469,9 @@ bool index_query1(rc_index *h, const float *query, int64_t n_rows, int k, int wi
     a.nblk = (int)((n_rows + rpb - 1) / rpb);
     a.k = k;
     a.with_values = with_values;
-    // scan and finish as two launches: the kernel boundary orders the partial lists for less than
-    // the one-launch ticket's device-scope fences cost (35.3 vs 40.9 us per 10k-row call,
-    // profiles/r04/r04_query1_ab.json); RC_QUERY1_LAUNCHES=1 keeps the ticket form (A/B)
-    const char *ql = std::getenv("RC_QUERY1_LAUNCHES");
-    a.launches = (ql && ql[0] == '1') ? 1 : 2;
     a.row_base = h->row_base;
     a.row_stride = h->row_stride;
     a.partial = h->partial;
-    a.ticket = h->q1_ticket;
     a.out_scores = out_scores;
     a.out_rows = out_rows;
     a.out_values = out_values;
@@ -569,7 +558,6 @@ int rc_index_destroy(rc_index *h) {
         dfree(h->norms);
         dfree(h->qn);
         dfree(h->partial);
-        dfree(h->q1_ticket);
         if (h->q1_done != nullptr) (void)hipHostFree(h->q1_done);
         delete h;
     });

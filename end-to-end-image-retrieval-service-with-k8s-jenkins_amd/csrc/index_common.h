@@ -112,10 +112,8 @@ struct Query1Args {
     int nblk;
     int k;
     int with_values;
-    int launches;           // 1: one launch (last-block ticket); 2: scan launch + finishing launch
     int64_t row_base, row_stride;
     uint64_t *partial;      // [nblk][k]
-    unsigned *ticket;       // 0 before the launch; the last block resets it
     float *out_scores;      // [k]
     int64_t *out_rows;      // [k]
     float *out_values;      // [k][dim] (with_values)
@@ -395,14 +393,13 @@ void launch_scan_dtype(const ScanArgs &a) {
     }
 }
 
-// rc_sharded_query_host's single-query launch (see Query1Args).  Every wave normalises the
+// rc_sharded_query_host's single-query launch pair (see Query1Args).  Every wave normalises the
 // query exactly as normalize_queries_kernel does (same lane partition of the sum of squares,
 // same wave_sum, same products), so scores are bit-identical to the multi-kernel path; the
-// top-k of a total order does not depend on how rows are split over blocks.
-// PHASE 0: one launch — each block publishes its partial list (release fence, then one
-// atomic ticket); the block that takes the last ticket acquires and finishes (every block
-// reaches the exit).  PHASE 1 / 2: the same work as two launches (scan blocks; one finishing
-// block), the kernel boundary ordering the lists instead of the fences.
+// top-k of a total order does not depend on how rows are split over blocks.  PHASE 1: the scan
+// blocks, each writing its partial list; PHASE 2: one block merges them (the kernel boundary
+// orders the lists: a one-launch form with a last-block ticket behind device-scope fences
+// measured 5.6 us slower per 10k-row call, round 4) and gathers the values.
 template <typename T, int NCH, int CAP>
 __device__ __forceinline__ void query1_scan(const Query1Args &a) {
     constexpr int EPC = ScanShape<T, NCH>::EPC;
@@ -467,9 +464,17 @@ __device__ __forceinline__ void query1_finish(const Query1Args &a) {
         }
     }
     if (a.done != nullptr) {  // completion word for a host that polls instead of synchronising
-        __syncthreads();      // every wave's result stores issued and retired
+        // Every wave releases its OWN result stores to system scope (a workgroup barrier does not
+        // wait for another wave's outstanding stores), then the barrier, then one lane publishes.
+        // The explicit vmcnt waits stay in inline asm: hipcc may drop a fence's own wait when it
+        // believes the store counter is already empty (MI355X_MICROARCH.md, compiler hazard).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (threadIdx.x == 0) {
             __threadfence_system();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
@@ -477,34 +482,15 @@ __device__ __forceinline__ void query1_finish(const Query1Args &a) {
 
 template <typename T, int NCH, int CAP, int PHASE>
 __global__ __launch_bounds__(256) void query1_kernel(const Query1Args a) {
-    if constexpr (PHASE == 2) {
-        query1_finish<T, CAP>(a);
-        return;
-    } else {
-        query1_scan<T, NCH, CAP>(a);
-        if constexpr (PHASE == 0) {
-            __shared__ int last;
-            __threadfence();  // this block's partial list, visible device-wide before its ticket
-            __syncthreads();
-            if (threadIdx.x == 0) last = atomicAdd(a.ticket, 1u) == (unsigned)(a.nblk - 1);
-            __syncthreads();
-            if (!last) return;
-            __threadfence();  // acquire: every other block's list
-            query1_finish<T, CAP>(a);
-            if (threadIdx.x == 0) *a.ticket = 0u;  // ready for the next launch (stream-ordered)
-        }
-    }
+    if constexpr (PHASE == 2) query1_finish<T, CAP>(a);
+    else query1_scan<T, NCH, CAP>(a);
 }
 
 template <typename T, int NCH, int CAP>
 void launch_query1_phases(const Query1Args &a, hipStream_t s) {
-    if (a.launches == 1) {
-        hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 0>), dim3(a.nblk), dim3(256), 0, s, a);
-    } else {
-        hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 1>), dim3(a.nblk), dim3(256), 0, s, a);
-        RC_LAUNCH_CHECK();
-        hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 2>), dim3(1), dim3(256), 0, s, a);
-    }
+    hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 1>), dim3(a.nblk), dim3(256), 0, s, a);
+    RC_LAUNCH_CHECK();
+    hipLaunchKernelGGL((query1_kernel<T, NCH, CAP, 2>), dim3(1), dim3(256), 0, s, a);
     RC_LAUNCH_CHECK();
 }
 

@@ -928,11 +928,6 @@ void launch_rescore(const BatchPlan &p, const BatchWs &ws, int final_pass, hipSt
     }
 }
 
-#if defined(RC_GEMM_ABLATION)
-// diagnostic builds only (tools/build_diag.sh): filter ablation variant from RC_FILTER_ABL
-static const int filter_abl = std::getenv("RC_FILTER_ABL") ? std::atoi(std::getenv("RC_FILTER_ABL")) : 0;
-#endif
-
 int batch_stage_ratio(int k, int cap, int inflation) {
     const int g = cap / (5 * k / 2 * inflation + 1);
     return std::max(2, std::min(64, g));
@@ -989,14 +984,6 @@ void run_batched(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *ti
         if (nkt == 2 || nkt == 4 || nkt == 8) {
             fa.tiles_per_chunk = ((c1 - c0 + QS_RT - 1) / QS_RT + nchunk - 1) / nchunk;
             const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * 16 / QS_QT);
-#if defined(RC_GEMM_ABLATION)
-            if (filter_abl != 0 && nkt == 8) {  // diagnostic builds: RC_FILTER_ABL
-#define RC_ABL(A) \
-    if (filter_abl == A) hipLaunchKernelGGL((filter_qs_kernel<T, 8, A>), gr, bl, 0, s, fa);
-                RC_ABL(8) RC_ABL(9) RC_ABL(12) RC_ABL(13)
-#undef RC_ABL
-            } else
-#endif
             if (nkt == 8) hipLaunchKernelGGL((filter_qs_kernel<T, 8>), gr, bl, 0, s, fa);
             else if (nkt == 4) hipLaunchKernelGGL((filter_qs_kernel<T, 4>), gr, bl, 0, s, fa);
             else hipLaunchKernelGGL((filter_qs_kernel<T, 2>), gr, bl, 0, s, fa);

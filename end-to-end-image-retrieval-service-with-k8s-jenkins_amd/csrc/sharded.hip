@@ -73,8 +73,8 @@ struct rc_sharded {
     int64_t cap = 0;  // rows per shard
     std::vector<int> dev;
     // shard s is driven through the cross-device path (peer copies to / from the leader):
-    // dev[s] != dev[0], or every shard s > 0 when RC_SHARDED_FORCE_REMOTE=1 at create (a test
-    // hook: the 8-GPU code path — gather, peer copies, leader merge — exercised on one GPU)
+    // dev[s] != dev[0], or every shard s > 0 after rc_sharded_force_remote (a test hook: the
+    // 8-GPU code path — gather, peer copies, leader merge — exercised on one GPU)
     std::vector<char> remote;
     std::vector<rc_index *> shard;
     std::vector<hipStream_t> st;
@@ -273,10 +273,8 @@ int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int6
         h->dtype = dtype;
         h->cap = capacity_per_shard;
         h->dev.assign(devices, devices + n_shards);
-        const char *fr = std::getenv("RC_SHARDED_FORCE_REMOTE");
-        const bool force_remote = fr && fr[0] == '1';
         h->remote.assign(n_shards, 0);
-        for (int s = 1; s < n_shards; ++s) h->remote[s] = (devices[s] != devices[0] || force_remote) ? 1 : 0;
+        for (int s = 1; s < n_shards; ++s) h->remote[s] = devices[s] != devices[0] ? 1 : 0;
         h->shard.assign(n_shards, nullptr);
         h->st.assign(n_shards, nullptr);
         h->ev_done.assign(n_shards, nullptr);
@@ -320,6 +318,20 @@ int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int6
 int rc_sharded_destroy(rc_sharded *h) {
     return guard([&] {
         if (h) destroy(h);
+    });
+}
+
+int rc_sharded_force_remote(rc_sharded *h) {
+    return guard([&] {
+        RC_REQUIRE(h, RC_ERR_INVALID, "null index");
+        std::lock_guard<std::mutex> lk(h->mu);
+        {
+            DeviceScope dl(h->dev[0]);
+            RC_HIP(hipDeviceSynchronize());  // nothing of the old routing is in flight
+        }
+        free_search(h);  // both are sized by the remote flags; regrown on the next call
+        free_staging(h);
+        for (int s = 1; s < h->n; ++s) h->remote[s] = 1;
     });
 }
 
@@ -559,25 +571,17 @@ int rc_sharded_query_host(rc_sharded *h, const float *queries, int nq, int64_t n
         const QueryLayout L = query_layout(h, nq, k, dev_values);
         ensure_query(h, L.total);
         DeviceScope dl(h->dev[0]);
-        const char *q1 = std::getenv("RC_QUERY1");  // "0": the multi-kernel path (A/B)
-        if (h->n == 1 && nq == 1 && !(q1 && q1[0] == '0')) {
-            // the request path: ONE launch (query in its arguments, results written straight
-            // into the pinned block), one synchronisation, no copies
+        if (h->n == 1 && nq == 1) {
+            // the request path: one launch pair (query in the kernel arguments, results written
+            // straight into the pinned block), no copies; the host polls the completion word
             float *hs = (float *)(h->qh + L.sc);
             int64_t *hr = (int64_t *)(h->qh + L.rw);
             float *hv = (float *)(h->qh + L.val);
-            const char *sp = std::getenv("RC_QUERY1_SPIN");  // "0": synchronise the stream (A/B)
-            const bool spin = !(sp && sp[0] == '0');
             volatile unsigned *word = nullptr;
             unsigned want = 0;
-            if (index_query1(h->shard[0], queries, n_rows, k, with_values, hs, hr, hv, h->qs, spin ? &word : nullptr,
-                             &want)) {
-                if (spin) {
-                    spin_until(word, want, h->qs);
-                    std::atomic_thread_fence(std::memory_order_acquire);  // the result reads stay below
-                } else {
-                    RC_HIP(hipStreamSynchronize(h->qs));
-                }
+            if (index_query1(h->shard[0], queries, n_rows, k, with_values, hs, hr, hv, h->qs, &word, &want)) {
+                spin_until(word, want, h->qs);
+                std::atomic_thread_fence(std::memory_order_acquire);  // the result reads stay below
                 std::memcpy(scores, hs, (size_t)k * sizeof(float));
                 std::memcpy(out_rows, hr, (size_t)k * sizeof(int64_t));
                 if (with_values) std::memcpy(values, hv, (size_t)k * h->dim * sizeof(float));

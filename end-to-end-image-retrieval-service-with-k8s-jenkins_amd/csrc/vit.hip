@@ -88,7 +88,7 @@ struct rc_model {
     uint8_t *resized = nullptr, *resize_tmp = nullptr;
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
-    int gemm_variant = GEMM_AUTO;  // diagnostic builds: RC_GEMM_VARIANT (ablation variants)
+    int gemm_variant = GEMM_AUTO;  // diagnostic builds only: rc_diag_set_gemm_variant
     int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -341,13 +341,30 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
     return m->resized;
 }
 
+#if defined(RC_GEMM_ABLATION)
+// Diagnostic builds: the A/B kernel for a full-batch projection.  The residual producers
+// (O-proj, fc2; auto = image-aligned tiles) take GEMM_PINGPONG / GEMM_W2 / GEMM_PP_IMG;
+// ping-pong ablations (100 + ABL) apply where auto picks the 256-row ping-pong kernel.
+int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue) {
+    if (variant == GEMM_AUTO) return variant;
+    const int pick = gemm_pick(a, GEMM_AUTO, patch_epilogue);
+    if (pick == GEMM_PP_IMG && (variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG)) return variant;
+    if (pick == GEMM_PINGPONG && variant >= 100 && variant < 200) return variant;
+    return GEMM_AUTO;
+}
+#endif
+
 // role: T_QKV / T_OPROJ / T_FC1 / T_FC2 (its own timer besides T_GEMM), or -1
 template <int EPI>
 void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
     const double flops = 2.0 * a.M * a.N * a.K;
     const int t0 = m->timers[T_GEMM].begin(s);
     const int t1 = role >= 0 ? m->timers[role].begin(s) : -1;
-    launch_gemm<EPI>(a, gemm_model_variant(a, m->gemm_variant, epi_patch(EPI), epi_hl(EPI)), s);
+    int variant = GEMM_AUTO;
+#if defined(RC_GEMM_ABLATION)
+    variant = diag_variant(a, m->gemm_variant, epi_patch(EPI));
+#endif
+    launch_gemm<EPI>(a, variant, s);
     if (role >= 0) m->timers[role].end(t1, s, flops);
     m->timers[T_GEMM].end(t0, s, flops);
 }
@@ -502,7 +519,11 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
                                scale * 1.4426950408889634f);
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
-        resid_gemm(m, produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true), s, T_OPROJ);
+        {
+            GemmArgs o = produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true);
+            o.row_step = T;  // image-aligned tiles (gemm_pp_kernel<.., 224>)
+            resid_gemm(m, o, s, T_OPROJ);
+        }
         if (fold) {
             GemmArgs a{ln, L.w_fc1_f, L.b_fc1_f, M, c.mlp, H, mlp, nullptr, nullptr, T};
             a.ln_c = L.c_fc1;
@@ -514,8 +535,11 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             gemm<EPI_GELU_BF16>(m, GemmArgs{ln, L.w_fc1, L.b_fc1, M, c.mlp, H, mlp, nullptr, nullptr, T}, s, T_FC1);
         }
         // the last layer's fc2 feeds only the final LN of the CLS rows (cls_final_kernel)
-        resid_gemm(m, produce(GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T},
-                              l + 1 < c.layers), s, T_FC2);
+        {
+            GemmArgs f2 = produce(GemmArgs{mlp, L.w_fc2, L.b_fc2, M, H, c.mlp, nullptr, hidden, nullptr, T}, l + 1 < c.layers);
+            f2.row_step = T;
+            resid_gemm(m, f2, s, T_FC2);
+        }
     }
     // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
     const float *fin = m->cls_only_last ? m->cls_hidden + (int64_t)i0 * H : hidden;
@@ -609,9 +633,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));
             build_lut(m);
-#if defined(RC_GEMM_ABLATION)
-            if (const char *gv = std::getenv("RC_GEMM_VARIANT")) m->gemm_variant = std::atoi(gv);
-#endif
             RC_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
             for (int p = 1; p < kMaxParts; ++p) {
                 RC_HIP(hipStreamCreateWithFlags(&m->sp[p], hipStreamNonBlocking));
@@ -809,22 +830,6 @@ int rc_model_set_parts(rc_model *m, int parts) {
     });
 }
 
-int rc_model_set_gemm_variant(rc_model *m, int variant) {
-    return guard([&] {
-        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
-        bool diag = false;
-#if defined(RC_GEMM_ABLATION)
-        diag = variant >= 100 && variant < 200;  // ping-pong ablations (tools/build_diag.sh builds only)
-#endif
-        RC_REQUIRE(diag || variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_RING5 || variant == GEMM_RING4 ||
-                       variant == GEMM_RING3 || (variant >= GEMM_PP_KL0 && variant <= GEMM_PP_KL3),
-                   RC_ERR_INVALID, "GEMM variant must be 0 (auto), 4 (ping-pong), 5 / 6 / 7 (ring of 4 / 3 / 5 slots), "
-                   "10-13 (ping-pong K-loop forms)");
-        std::lock_guard<std::mutex> lk(m->mu);
-        m->gemm_variant = variant;
-    });
-}
-
 int rc_model_set_ln_fold(rc_model *m, int on) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
@@ -857,6 +862,19 @@ int rc_model_timing_reset(rc_model *m) {
 // GEMM kernels' phase stamps, or null to stop stamping
 extern "C" int rc_diag_set_stamps(void *dev) {
     return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rc_stamps), &dev, sizeof(dev))); });
+}
+
+// diagnostic builds: the A/B kernel of the full-batch projections (diag_variant); not in the
+// product ABI — the product picks one kernel per shape
+extern "C" int rc_diag_set_gemm_variant(rc_model *m, int variant) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG ||
+                       (variant >= 100 && variant < 200),
+                   RC_ERR_INVALID, "GEMM variant: 0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 100 + ABL");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->gemm_variant = variant;
+    });
 }
 #endif
 

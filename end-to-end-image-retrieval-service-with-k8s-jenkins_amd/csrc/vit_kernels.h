@@ -47,6 +47,10 @@ struct GemmArgs {
     const float *pos;   // EPI_PATCH_F32: position embeddings [tokens][N]
     int tokens;         // EPI_PATCH_F32: tokens per image (patches + 1)
     int group_m = 0;                 // ping-pong tile order: 0 = row-major, G = groups of G row tiles
+    // image-aligned row tiles (the residual producers O-proj / fc2, N = 768): row tile tm covers
+    // the rows [tm·row_step, tm·row_step + row_step) of one image (row_step = tokens = 197), computed
+    // as a 224-row tile, so a batch of n images is exactly n × (N / 256) tiles (0: BM-row tiles)
+    int row_step = 0;
     int ldc = 0;                     // bf16 outputs: row stride in elements (0 = N)
     // LayerNorm folded across a GEMM pair (see "LayerNorm fold" below):
     //   producer (f32 epilogues): ln_x != null → also write bf16(x) rows and per-(row, 64-column

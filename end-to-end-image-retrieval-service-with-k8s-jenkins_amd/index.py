@@ -223,6 +223,88 @@ def topk_merge(scores: torch.Tensor, rows: torch.Tensor, k: int, stream=None):
     return out_s, out_r
 
 
+class Record(dict):
+    """A query match or fetched vector in Pinecone's shape (``{"id", "score" | "values",
+    "metadata"}``) whose ``"values"`` entry stays a float32 row until something reads it.
+
+    The reference's ``search`` asks for ``include_values=True`` and keeps only the ids
+    (``retriever/utils.py:62-65``), so building 5 x 768 Python floats per request is work no
+    caller of that path sees.  Every read path of the dict — ``[]``, ``get``, ``items``,
+    ``values``, iteration with ``dict(...)`` / ``{**m}``, ``==``, ``copy``, ``repr``, pickling,
+    ``json.dumps`` (which calls ``items()`` on a dict subclass) — first turns the row into the
+    list of Python floats a plain dict would hold, once."""
+
+    __slots__ = ("_row",)
+
+    def __init__(self, row: np.ndarray | None = None, **fields):
+        super().__init__(fields)
+        self._row = row
+        if row is not None:
+            dict.__setitem__(self, "values", None)
+
+    def _load(self) -> None:
+        row = self._row
+        if row is not None:
+            self._row = None
+            dict.__setitem__(self, "values", row.astype(np.float64).tolist())
+
+    def __getitem__(self, key):
+        if key == "values":
+            self._load()
+        return dict.__getitem__(self, key)
+
+    def get(self, key, default=None):
+        if key == "values":
+            self._load()
+        return dict.get(self, key, default)
+
+    def __iter__(self):  # a Python-level __iter__ sends dict(m) / {**m} through keys() + __getitem__
+        return dict.__iter__(self)
+
+    def items(self):
+        self._load()
+        return dict.items(self)
+
+    def values(self):
+        self._load()
+        return dict.values(self)
+
+    def copy(self):
+        self._load()
+        return dict(dict.items(self))
+
+    def pop(self, key, *default):
+        self._load()
+        return dict.pop(self, key, *default)
+
+    def popitem(self):
+        self._load()
+        return dict.popitem(self)
+
+    def setdefault(self, key, default=None):
+        self._load()
+        return dict.setdefault(self, key, default)
+
+    def __eq__(self, other):
+        self._load()
+        if isinstance(other, Record):
+            other._load()
+        return dict.__eq__(self, other)
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    __hash__ = None
+
+    def __repr__(self):
+        self._load()
+        return dict.__repr__(self)
+
+    def __reduce__(self):
+        self._load()
+        return (dict, (dict(dict.items(self)),))
+
+
 def _as_vector(values: Any, dim: int) -> list[float]:
     if isinstance(values, torch.Tensor):
         values = values.detach().cpu().reshape(-1).tolist()
@@ -239,13 +321,17 @@ def _as_vector_np(values: Any, dim: int) -> np.ndarray:
     Python loop)."""
     if isinstance(values, torch.Tensor):
         a = values.detach().to(device="cpu", dtype=torch.float32).reshape(-1).numpy()
-    elif isinstance(values, (list, tuple)):
-        try:  # a JSON list of floats: array('f') converts it ~4x faster than np.asarray (same f32 rounding)
-            a = np.frombuffer(array.array("f", values), dtype=np.float32)
-        except TypeError:
-            a = np.asarray(values, dtype=np.float32).reshape(-1)
     else:
-        a = np.asarray(values, dtype=np.float32).reshape(-1)
+        a = None
+        if isinstance(values, (list, tuple)):
+            try:  # a JSON list of floats: array('f') converts it ~4x faster than np.asarray (same f32 rounding)
+                a = np.frombuffer(array.array("f", values), dtype=np.float32)
+            except TypeError:
+                pass
+        if a is None:
+            a = np.asarray(values, dtype=np.float32)
+            if a.ndim != 1:  # as _as_vector: float() of a nested element raises, nothing is flattened
+                raise TypeError(f"a query vector must be a flat sequence of numbers (got shape {a.shape})")
     if a.shape[0] != dim:
         raise ValueError(f"Vector dimension {a.shape[0]} does not match the dimension of the index {dim}")
     if not a.any():
@@ -322,6 +408,11 @@ class ShardSet:
         ld = _lib.C.c_int64()
         check(self.lib.rc_sharded_info(self.handle, None, None, _lib.C.byref(ld)))
         return ld.value
+
+    def force_remote(self) -> None:
+        """Test hook (rc_sharded_force_remote): every shard but the leader through the
+        cross-device path, as on a multi-GPU node, even when the shards share one GPU."""
+        check(self.lib.rc_sharded_force_remote(self.handle))
 
     def shard(self, s: int) -> DeviceIndex:
         return self._shards[s]
@@ -496,7 +587,7 @@ class Index:
         # reference's search (retriever/utils.py:62-64) asks for values and its caller then
         # fetches the same ids (retriever/main.py:142) — each row leaves the GPU once
         self._gen = 0
-        self._recent: tuple[int, dict[str, list[float]]] = (-1, {})
+        self._recent: tuple[int, dict[str, np.ndarray]] = (-1, {})
 
     @property
     def shard_set(self) -> ShardSet:
@@ -709,19 +800,18 @@ class Index:
         scores = scores.cpu().tolist()
         rows = rows.cpu().tolist()
         out = []
-        recent: dict[str, list[float]] = {}
+        recent: dict[str, np.ndarray] = {}
         for sq, rq in zip(scores, rows):
             sel = [(s, r) for s, r in zip(sq, rq) if r >= 0]
-            vals = self._set.fetch_rows([r for _, r in sel]).tolist() if include_values and sel else None
+            vals = self._set.fetch_rows([r for _, r in sel]).numpy() if include_values and sel else None
             if vals is not None:
                 recent.update((self._ids[r], v) for (_, r), v in zip(sel, vals))
             matches = []
             for j, (s, r) in enumerate(sel):
-                m = {"id": self._ids[r], "score": float(s)}
-                if include_values:
-                    m["values"] = vals[j]
+                vid = self._ids[r]
+                m = Record(vals[j], id=vid, score=float(s)) if include_values else {"id": vid, "score": float(s)}
                 if include_metadata:
-                    m["metadata"] = dict(self._meta.get(self._ids[r], {}))
+                    dict.__setitem__(m, "metadata", dict(self._meta.get(vid, {})))
                 matches.append(m)
             out.append(matches)
         if include_values:
@@ -736,23 +826,29 @@ class Index:
             return [[] for _ in range(q.shape[0])]
         sc, rw, val = self._set.query_host(q, k, n, include_values)
         out = []
-        recent: dict[str, list[float]] = {}
+        recent: dict[str, np.ndarray] = {}
         ids, meta = self._ids, self._meta
         for qi in range(q.shape[0]):
             rows = rw[qi].tolist()
             live = k - rows.count(-1)  # the lists are sorted: empty slots (-1) come last
-            # one conversion per query, through f64 (exact for f32; numpy's f64 tolist is the faster one)
-            vals = val[qi, :live].astype(np.float64).tolist() if include_values else None
-            matches = []
-            for j, (s, r) in enumerate(zip(sc[qi, :live].tolist(), rows[:live])):
-                vid = ids[r]
-                m = {"id": vid, "score": s}
-                if include_values:
-                    m["values"] = v = vals[j]
-                    recent[vid] = v
+            scores = sc[qi, :live].tolist()
+            if include_values:
+                # the reused host buffer is copied once (one memcpy); each match keeps its row as f32
+                # and builds the Python list only if read (Record)
+                vals = val[qi, :live].copy()
+                matches = []
+                for j in range(live):
+                    vid = ids[rows[j]]
+                    m = Record(vals[j], id=vid, score=scores[j])
+                    recent[vid] = vals[j]
+                    if include_metadata:
+                        dict.__setitem__(m, "metadata", dict(meta.get(vid, {})))
+                    matches.append(m)
+            else:
+                matches = [{"id": ids[r], "score": s} for s, r in zip(scores, rows[:live])]
                 if include_metadata:
-                    m["metadata"] = dict(meta.get(vid, {}))
-                matches.append(m)
+                    for m in matches:
+                        m["metadata"] = dict(meta.get(m["id"], {}))
             out.append(matches)
         if include_values:
             self._recent = (self._gen, recent)
@@ -764,12 +860,14 @@ class Index:
             vectors = {}
             gen, recent = self._recent
             if found and gen == self._gen and all(i in recent for i, _ in found):
-                vals = [list(recent[i]) for i, _ in found]  # fetched by the query just before: no second device read
+                vals = [recent[i] for i, _ in found]  # fetched by the query just before: no second device read
             elif found:
-                vals = self._set.fetch_rows([r for _, r in found]).tolist()
+                vals = self._set.fetch_rows([r for _, r in found]).numpy()
             if found:
                 for (vid, _), v in zip(found, vals):
-                    vectors[vid] = {"id": vid, "values": v, "metadata": dict(self._meta.get(vid, {}))}
+                    rec = Record(v, id=vid)  # "values" becomes a list when read (retriever/main.py reads metadata)
+                    dict.__setitem__(rec, "metadata", dict(self._meta.get(vid, {})))
+                    vectors[vid] = rec
         return {"vectors": vectors, "namespace": namespace}
 
     # ---------------------------------------------------------- persistence --

@@ -34,6 +34,14 @@ def index():
     return get_index(Config.INDEX_NAME)
 
 
+def _feature_fn(request: Request):
+    """The app serving this request may embed its own way (service.py's one-process app sets
+    ``app.state.feature_vector``); otherwise this module's ``get_feature_vector`` (the name the
+    reference's tests monkeypatch)."""
+    fn = getattr(request.app.state, "feature_vector", None)
+    return fn if fn is not None else get_feature_vector
+
+
 def _missing_file(field: str):
     return RequestValidationError([{"type": "missing", "loc": ("body", field), "msg": "Field required", "input": None}])
 
@@ -55,7 +63,7 @@ async def push_image(request: Request):
     if f is None:
         raise _missing_file("file")
     return core.push_one(f.filename, f.data, index, content_type=f.content_type, storage=storage,
-                         feature_fn=lambda b: get_feature_vector(b))
+                         feature_fn=_feature_fn(request))
 
 
 @app.post("/push_images")

@@ -37,6 +37,14 @@ def index():
     return get_index(Config.INDEX_NAME)
 
 
+def _feature_fn(request: Request):
+    """The app serving this request may embed its own way (service.py's one-process app sets
+    ``app.state.feature_vector``); otherwise this module's ``get_feature_vector`` (the name the
+    reference's tests monkeypatch)."""
+    fn = getattr(request.app.state, "feature_vector", None)
+    return fn if fn is not None else get_feature_vector
+
+
 @app.get("/")
 def read_root():
     return {"message": "Welcome to the Image Retriever API. Visit /docs to test."}
@@ -58,7 +66,7 @@ async def search_image(request: Request):
         Image.open(BytesIO(f.data)).convert("RGB")
     except UnidentifiedImageError:
         raise HTTPException(status_code=400, detail="Uploaded file is not a valid image.")
-    feature = get_feature_vector(f.data)
+    feature = _feature_fn(request)(f.data)
     ix = index()
     match_ids = search(ix, feature, top_k=Config.TOP_K)
     if not match_ids:

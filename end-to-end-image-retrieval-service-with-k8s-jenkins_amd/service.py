@@ -13,7 +13,9 @@ pods into this one app: every route of the three services, one embedder, and one
 reads.  The per-service apps stay importable for their own contract tests.
 
   GET  /              → {"message": "Welcome to the Image Retrieval API. Visit /docs to test."}
-  GET  /healthz       → {"status": "healthy"}
+  GET  /healthz       → {"status": "healthy"}  (the embedding and ingest pods' body)
+  GET  /healthz/retriever → {"status": "OK!"}  (the retriever pod's body, retriever/main.py:99-101,
+                          for a probe or client of the old retriever URL that checks the body)
   POST /embed, /embed_batch                  (embedding/main.py:88-124)
   POST /push_image, /push_images             (ingesting/main.py:101-168)
   POST /search_image                         (retriever/main.py:104-169)
@@ -48,9 +50,10 @@ for _sub in SERVICE_APPS:
     _mount(_sub)
 
 # /embed is served by this very process: the ingest and retrieve routes embed in process
-# (an HTTP hop to ourselves would only add latency).
-ingesting_main.get_feature_vector = embed_locally
-retriever_main.get_feature_vector = embed_locally
+# (an HTTP hop to ourselves would only add latency).  Scoped to this app: the mounted route
+# handlers read request.app.state.feature_vector, so the per-service apps (and the
+# module-level get_feature_vector the reference's tests monkeypatch) are left as they are.
+app.state.feature_vector = embed_locally
 
 
 def index():
@@ -66,3 +69,8 @@ def read_root():
 @app.get("/healthz")
 def health_check():
     return {"status": "healthy"}
+
+
+@app.get("/healthz/retriever")
+def health_check_retriever():
+    return retriever_main.health_check()

@@ -361,8 +361,13 @@ class VitMsnEmbedder:
         check(self.lib.rc_model_set_last_layer(self._h, int(bool(cls_only))))
 
     def set_gemm_variant(self, variant: int) -> None:
-        """Full-batch projection GEMM kernel: 0 auto, 4 ping-pong, 5 / 6 ring (A/B; same bits)."""
-        check(self.lib.rc_model_set_gemm_variant(self._h, int(variant)))
+        """Diagnostic builds only (tools/build_diag.sh, RC_LIB_PATH): the A/B kernel of the
+        full-batch projections (0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 100 + ABL).
+        The product library picks one kernel per shape and has no such knob."""
+        fn = getattr(self.lib, "rc_diag_set_gemm_variant", None)
+        if fn is None:
+            raise RuntimeError("GEMM variants are a diagnostic-build knob (tools/build_diag.sh)")
+        check(fn(self._h, int(variant)))
 
     def timing_reset(self) -> None:
         check(self.lib.rc_model_timing_reset(self._h))

@@ -187,6 +187,10 @@ int rc_topk_merge(const float *scores, const int64_t *rows, int nlists, int nq, 
 int rc_sharded_create(int n_shards, const int *devices, int dim, int dtype, int64_t capacity_per_shard,
                       rc_sharded **out);
 int rc_sharded_destroy(rc_sharded *h);
+/* Test hook: drive every shard but the leader through the cross-device path (subset
+ * gather on the leader, peer copies of queries / subsets / result lists, leader merge)
+ * even where shards share the leader's GPU — the code an 8-GPU node runs, on one GPU. */
+int rc_sharded_force_remote(rc_sharded *h);
 int rc_sharded_info(const rc_sharded *h, int *n_shards, int64_t *capacity_per_shard, int64_t *ld);
 /* Borrowed handle of shard s (persistence, parity tests); owned by h. */
 int rc_sharded_shard(rc_sharded *h, int s, rc_index **out);
@@ -283,12 +287,6 @@ int rc_model_set_last_layer(rc_model *m, int cls_only);
  * parity tests). */
 int rc_model_set_ln_fold(rc_model *m, int on);
 
-/* Projection-GEMM kernel for the full-batch GEMMs (A/B measurements; results are
- * bit-identical across variants: every kernel accumulates K in the same order):
- * 0 auto, 4 ping-pong (one 64-deep K-tile in flight), 5 ring (4 slots of 32-deep
- * K-steps, 2 in flight), 6 ring (3 slots, 1 in flight). */
-int rc_model_set_gemm_variant(rc_model *m, int variant);
-
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM, 2 = attention, 3 = layernorm,
  * 4 = preprocess, 5 = QKV GEMM, 6 = O-proj GEMM, 7 = fc2 GEMM (5-7 and 1: the
@@ -302,8 +300,9 @@ int rc_model_timing_reset(rc_model *m);
  * out = epilogue(A[M][K] · W[N][K]ᵀ + bias): epi 0 → bf16 out, 1 → bf16 GELU(out),
  * 2 → f32 out += (residual, in place), 3 → f32 patch scatter (+pos, tokens/image).
  * A must have round_up(M, 256) readable rows; N % 256 == 0 (M > 256), K % 64 == 0.
- * variant: 0 auto, 4 256x256 ping-pong, 5 / 6 256x256 ring (4 / 3 slots), 8 128x256
- * two-workgroup, 9 skinny (M <= 256). */
+ * variant: 0 auto, 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256)
+ * (the image-aligned 224-row tiles the model's O-proj / fc2 run need rc_embed's
+ * residual stream and are reached through it). */
 int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N, int K,
                  void *out, const float *pos, int tokens, void *stream);
 

@@ -297,21 +297,26 @@ def test_from_pretrained_v5_layout_matches_golden(vitmod, cuda, tmp_path):
     direct.close()
 
 
-@pytest.mark.parametrize("base,variant", [(4, 5), (4, 6), (0, 7), (0, 10), (0, 11), (0, 12), (0, 13)])
-def test_ring_gemm_variant_bit_identical(vitmod, weights12, cuda, base, variant):
-    """The ring GEMM kernels (deeper LDS-DMA pipeline, 3 / 4 / 5 slots) and the ping-pong K-loop
-    forms (W kept, buffer-load DMA) accumulate K in the ping-pong kernel's order: the 12-layer
-    embedding of a batch is the same bits under each (all four projection epilogues: LN-fold
-    consumers, GELU, bf16-pair residual producers)."""
+def test_image_aligned_tiles_batch_invariant(vitmod, weights12, cuda):
+    """O-proj and fc2 run on image-aligned 224-row tiles (tile t = the rows of image t), the other
+    projections on 256-row tiles and a lone image on the skinny kernels: every kernel accumulates
+    K in the same order, so an image's 12-layer embedding is the same bits whatever batch, slice
+    or tile it lands in — a batch of 300 in one or two slices, three batches of 100, single images."""
     import torch
 
     rng = np.random.default_rng(21)
     imgs = torch.from_numpy(rng.integers(0, 256, (300, 224, 224, 3), dtype=np.uint8))
     m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=300)
-    m.set_gemm_variant(base)
+    m.set_parts(1)
     a, an = m.embed(imgs)
-    m.set_gemm_variant(variant)
+    m.set_parts(2)
     b, bn = m.embed(imgs)
+    parts = [m.embed(imgs[i:i + 100]) for i in range(0, 300, 100)]
+    c = torch.cat([p[0] for p in parts])
+    ones = [m.embed(imgs[i:i + 1])[0] for i in (0, 1, 150, 299)]
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(an, bn)
+    assert torch.equal(a, c)
+    for j, i in enumerate((0, 1, 150, 299)):
+        assert torch.equal(a[i:i + 1], ones[j]), i
     m.close()

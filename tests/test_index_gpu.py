@@ -176,3 +176,30 @@ def test_config3_full_size_planted(idxmod, cuda):
     Xr = dev.stored_rows(r.reshape(-1)).reshape(3, 10, dim).double()
     qn = Q.double() / Q.double().norm(dim=1, keepdim=True)
     assert torch.allclose(torch.einsum("qkd,qd->qk", Xr, qn).cpu(), s.double().cpu(), atol=1e-5)
+
+
+def test_query_host_values_follow_each_query(idxmod, cuda):
+    """The one-shard request path (rc_sharded_query_host -> query1 launch pair writing scores, rows
+    and the matches' values into reused pinned memory; the host polls a completion word the
+    finishing block stores after them): alternating distinct queries with include_values=True,
+    every match carries exactly its own row's upserted vector (no value left over from the
+    previous query), and ids / scores equal the multi-kernel device search (rc_sharded_search)."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((10000, 768)).astype(np.float32)
+    ix = idxmod.Index("q1-values", dimension=768, dtype="float32", capacity=len(X), device=cuda)
+    ix.upsert_tensor([f"r{i}" for i in range(len(X))], torch.from_numpy(X).to(cuda))
+    qs = [X[i] + 0.01 * rng.standard_normal(768).astype(np.float32) for i in (5, 777, 5, 9999, 1234, 777)]
+    for q in qs * 3:
+        res = ix.query(vector=q.tolist(), top_k=5, include_values=True)["matches"]
+        s_dev, r_dev = ix.shard_set.search(torch.from_numpy(q[None]), 5, len(ix))
+        assert [m["id"] for m in res] == [f"r{r}" for r in r_dev[0].tolist()]
+        assert [m["score"] for m in res] == s_dev[0].tolist()
+        for m in res:
+            assert np.array_equal(np.asarray(m["values"], np.float32), X[int(m["id"][1:])]), m["id"]
+        ids = [m["id"] for m in res]
+        got = ix.fetch(ids)["vectors"]  # served from the values this query just fetched
+        for i in ids:
+            assert np.array_equal(np.asarray(got[i]["values"], np.float32), X[int(i[1:])])
+    ix.close()

@@ -1,0 +1,71 @@
+"""``index.Record``: query matches / fetched vectors whose ``"values"`` list is built on first read.
+
+The reference's ``search`` requests ``include_values=True`` and keeps only the ids
+(``retriever/utils.py:62-65``); every way a caller can read the dict must still see the
+list of floats a plain Pinecone-shaped dict holds (GPU-free: the rows are numpy arrays)."""
+import copy
+import json
+import pickle
+
+import numpy as np
+import pytest
+
+from conftest import import_pkg
+
+
+def _rec():
+    Record = import_pkg("index").Record
+    row = np.array([0.5, -1.25, 3.0], np.float32)
+    r = Record(row, id="a", score=0.75)
+    dict.__setitem__(r, "metadata", {"gcs_path": "images/a.jpg"})
+    return r, {"id": "a", "score": 0.75, "values": [0.5, -1.25, 3.0], "metadata": {"gcs_path": "images/a.jpg"}}
+
+
+@pytest.mark.parametrize("read", [
+    lambda r: r["values"],
+    lambda r: r.get("values"),
+    lambda r: dict(r)["values"],
+    lambda r: {**r}["values"],
+    lambda r: dict(r.items())["values"],
+    lambda r: list(r.values())[2],
+    lambda r: r.copy()["values"],
+    lambda r: copy.deepcopy(r)["values"],
+    lambda r: pickle.loads(pickle.dumps(r))["values"],
+    lambda r: json.loads(json.dumps(r))["values"],
+])
+def test_every_read_path_sees_the_list(read):
+    r, _ = _rec()
+    v = read(r)
+    assert v == [0.5, -1.25, 3.0] and all(type(x) is float for x in v)
+
+
+def test_record_is_the_plain_dict():
+    r, plain = _rec()
+    assert list(r.keys()) == ["id", "score", "values", "metadata"] and len(r) == 4 and "values" in r
+    assert r["id"] == "a" and r["score"] == 0.75  # other keys read without building the list
+    assert r._row is not None
+    assert r == plain and plain == r and not (r != plain)
+    assert r._row is None and dict.__getitem__(r, "values") == plain["values"]
+    r2, _ = _rec()
+    assert repr(r2) == repr(plain)
+    r3, _ = _rec()
+    assert r3.pop("values") == plain["values"] and "values" not in r3
+
+
+def test_record_without_values_is_a_plain_match():
+    Record = import_pkg("index").Record
+    r = Record(None, id="b", score=0.5)
+    assert r == {"id": "b", "score": 0.5} and "values" not in r
+
+
+def test_query_vector_rejects_nested_lists():
+    """A nested query ([[v0..]]) is refused, as the per-element float() of the old parser did
+    (no silent flattening); flat lists, tuples and arrays are accepted."""
+    ix = import_pkg("index")
+    v = [0.25] * 8
+    assert ix._as_vector_np(v, 8).shape == (1, 8)
+    assert ix._as_vector_np(tuple(v), 8).shape == (1, 8)
+    assert ix._as_vector_np(np.asarray(v), 8).shape == (1, 8)
+    for bad in ([v], np.asarray([v])):
+        with pytest.raises(TypeError):
+            ix._as_vector_np(bad, 8)

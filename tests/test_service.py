@@ -34,6 +34,8 @@ def test_service_serves_every_route(svc):
     for p in ("/", "/healthz", "/embed", "/embed_batch", "/push_image", "/push_images", "/search_image"):
         assert p in paths, p
     assert svc.get("/healthz").json() == {"status": "healthy"}
+    # the retriever pod answered {"status": "OK!"} (retriever/main.py:99-101): served on its own path
+    assert svc.get("/healthz/retriever").json() == {"status": "OK!"}
     assert svc.get("/").json() == {"message": "Welcome to the Image Retrieval API. Visit /docs to test."}
 
 
@@ -54,11 +56,32 @@ def test_service_validation_contract(svc):
 
 
 def test_service_embeds_in_process():
+    """The one-process app embeds in process through its own app state; importing it rebinds
+    nothing in the per-service modules (the name the reference's tests monkeypatch stays theirs)."""
     s = import_pkg("service")
     utils = import_pkg("ingesting.utils")
-    assert import_pkg("ingesting.main").get_feature_vector is utils.embed_locally
-    assert import_pkg("retriever.main").get_feature_vector is utils.embed_locally
+    assert s.app.state.feature_vector is utils.embed_locally
+    for mod in ("ingesting.main", "retriever.main"):
+        m = import_pkg(mod)
+        assert getattr(m.app.state, "feature_vector", None) is None
+        cfg = import_pkg("config").Config
+        want = utils.embed_locally if cfg.EMBED_IN_PROCESS else utils.get_feature_vector
+        assert m.get_feature_vector is want
     assert s.index is not None
+
+
+def test_service_feature_vector_scoped_to_its_app(monkeypatch):
+    """A monkeypatched retriever.main.get_feature_vector (reference tests/test_retriever.py:11-16)
+    is what the retriever app uses; the one-process app keeps its own in-process embedder."""
+    from starlette.requests import Request
+
+    s = import_pkg("service")
+    rm = import_pkg("retriever.main")
+    fake = lambda _: [0.1] * 768  # noqa: E731
+    monkeypatch.setattr(rm, "get_feature_vector", fake)
+    req = lambda app: Request({"type": "http", "app": app, "headers": []})  # noqa: E731
+    assert rm._feature_fn(req(rm.app)) is fake
+    assert rm._feature_fn(req(s.app)) is import_pkg("ingesting.utils").embed_locally
 
 
 def _jpeg(seed, w=224, h=224):

@@ -37,16 +37,15 @@ def _items(rng, n, dim, prefix="v", start=0):
                                                  ("float16", 3, True), ("float32", 4, True)])
 def test_sharded_index_equals_single_shard(idxmod, cuda, dtype, shards, remote, monkeypatch):
     """A multi-shard index answers exactly like one shard.  remote: every shard but the leader
-    is driven through the cross-device path (RC_SHARDED_FORCE_REMOTE: subset gather on the
+    is driven through the cross-device path (rc_sharded_force_remote: subset gather on the
     leader, peer copies of queries / subsets / result lists, leader merge) — the code the
     8-GPU node runs, exercised on one GPU."""
     rng = np.random.default_rng(7)
     dim = 768
     one = idxmod.Index("one", dimension=dim, dtype=dtype, capacity=512, device=cuda)
-    if remote:
-        monkeypatch.setenv("RC_SHARDED_FORCE_REMOTE", "1")
     many = idxmod.Index("many", dimension=dim, dtype=dtype, capacity=512, device=cuda, shards=shards)
-    monkeypatch.delenv("RC_SHARDED_FORCE_REMOTE", raising=False)
+    if remote:
+        many.shard_set.force_remote()
     X, items = _items(rng, 3000, dim)
     X[1001] = X[17]  # exact ties on different shards (17 % n != 1001 % n for n = 2, 3, 4)
     items[1001] = ("v1001", X[17].tolist(), items[1001][2])

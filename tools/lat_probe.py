@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PKG = "end-to-end-image-retrieval-service-with-k8s-jenkins_amd"
 ing = importlib.import_module(f"{PKG}.ingesting.utils")
 ret = importlib.import_module(f"{PKG}.retriever.utils")
+idxmod = importlib.import_module(f"{PKG}.index")
 
 
 def lat(fn, reps=400):
@@ -36,23 +37,18 @@ ix.upsert_tensor([f"r{i}" for i in range(len(X))], torch.from_numpy(X).cuda(), N
 q = np.ascontiguousarray(np.asarray(vec, np.float32)[None])
 ss = ix._set
 out = {}
-for mode, env in (("multi_kernel", {"RC_QUERY1": "0"}), ("one_launch", {"RC_QUERY1_LAUNCHES": "1"}),
-                  ("stream_sync", {"RC_QUERY1_SPIN": "0"})):
-    os.environ.update(env)
-    out[f"lib_novalues_{mode}"] = lat(lambda: ss.query_host(q, 5, len(X), False))
-    for key in env:
-        del os.environ[key]
 out.update({
     "lib_values": lat(lambda: ss.query_host(q, 5, len(X), True)),
     "lib_novalues": lat(lambda: ss.query_host(q, 5, len(X), False)),
     "index_query_values": lat(lambda: ix.query(vector=vec, top_k=5, include_values=True)),
+    "index_query_values_read": lat(lambda: [m["values"] for m in ix.query(vector=vec, top_k=5, include_values=True)["matches"]]),
+    "as_vector_np": lat(lambda: idxmod._as_vector_np(vec, 768)),
     "index_query_novalues": lat(lambda: ix.query(vector=vec, top_k=5)),
     "search": lat(lambda: ret.search(ix, vec, top_k=5)),
     "lib_values_again": lat(lambda: ss.query_host(q, 5, len(X), True)),
     "asarray": lat(lambda: np.asarray(vec, np.float32)),
     "tolist_5x768": lat(lambda: np.zeros((5, 768), np.float32).tolist()),
 })
-idxmod = importlib.import_module(f"{PKG}.index")
 for n in (1, 1000, 100000):
     s2 = idxmod.ShardSet(768, dtype="float32", capacity_per_shard=n, devices=[0])
     s2.upsert_rows(torch.randn(n, 768), torch.arange(n))
