@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ 
 // removed; the forms live on in tools/gemm_lab.)
 enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 9, GEMM_PP_IMG = 10 };
 
-inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
+inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
     // The residual producers (O-proj, fc2: N = 768, every row tile one image) on image-aligned
@@ -1117,7 +1117,9 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue) {
     // Short square projections without image alignment (N = K = 768) finish in ~2.3 rounds of
     // 256x256 tiles and carry a heavy epilogue: the two-workgroup kernel overlaps it with the
     // co-resident workgroup's MFMAs.  Everything else streams K at 128 flop/B: ping-pong.
-    if (a.N <= 768 && a.K <= 768) return GEMM_W2;
+    // (LayerNorm-fold consumers, e.g. the CLS rows' Q of a batch above 256 images, stay on the
+    // ping-pong kernel, whose prologue computes the row scales.)
+    if (a.N <= 768 && a.K <= 768 && !ln_epilogue) return GEMM_W2;
     return GEMM_PINGPONG;
 }
 
@@ -1156,7 +1158,7 @@ template <int EPI>
 void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     GemmArgs a = a_in;
     RC_REQUIRE(a.K % 64 == 0 && a.K >= 64, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 64");
-    const int pick = gemm_pick(a, variant, epi_patch(EPI));
+    const int pick = gemm_pick(a, variant, epi_patch(EPI), epi_ln(EPI));
     RC_REQUIRE(a.ldc == 0 || (a.ldc >= a.N && epi_bf16_out(EPI)), RC_ERR_UNSUPPORTED,
                "an output row stride (ldc) needs a bf16 epilogue");
     if constexpr (epi_hl(EPI)) {

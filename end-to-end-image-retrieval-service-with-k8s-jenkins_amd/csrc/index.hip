@@ -171,6 +171,28 @@ __global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__r
     }
 }
 
+// First level of the two-level merge of many partial lists: block (g, qi) merges lists
+// [g·MERGE_L1, g·MERGE_L1 + MERGE_L1) of query qi into out[g][qi][0..k) (local keys; the second
+// level, merge_partials_kernel over those, applies the row map).  One block over ~2000 lists is
+// latency-bound (config 3, 1M rows / 1954 scan blocks: 30.5 us per call); G blocks of 32 lists
+// each, then one block over G lists, run the same per-wave top-k machinery in parallel.
+constexpr int MERGE_L1 = 32;
+template <int CAP>
+__global__ __launch_bounds__(256) void merge_stage1_kernel(const uint64_t *__restrict__ partial, int nlist, int nq_total,
+                                                          int k, const int *__restrict__ flags, uint64_t *__restrict__ out) {
+    __shared__ uint64_t lds[4][CAP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = blockIdx.x, qi = blockIdx.y;
+    if (flags != nullptr && flags[qi] == 0) return;  // block-uniform
+    const int l0 = g * MERGE_L1, nl = min(MERGE_L1, nlist - l0);
+    WaveTopK<CAP> tk;
+    merge_partial_lists<CAP>(partial + (int64_t)l0 * nq_total * k, nl, nq_total, qi, k, lds, tk);
+    if (wave == 0) {
+        uint64_t *dst = out + ((int64_t)g * nq_total + qi) * k;
+        for (int j = lane; j < k; j += 64) dst[j] = tk.buf[j];
+    }
+}
+
 // Cross-shard merge: nlists lists of (score, global row) per query.  The key's
 // low word is the global row itself (< 2^32), so equal scores order by row
 // whatever the row → shard routing (contiguous ranges or round-robin).  Rows
@@ -252,6 +274,7 @@ struct rc_index {
     int ws_nq = 0, ws_k = 0, ws_nblk = 0;
     float *qn = nullptr;
     uint64_t *partial = nullptr;
+    uint64_t *partial2 = nullptr;   // first-level merge output [kMaxBlocks / MERGE_L1][nq][k]
     unsigned *q1_done = nullptr;    // host-coherent completion word of the polled query1 path
     unsigned q1_seq = 0;
     BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
@@ -284,10 +307,13 @@ void ensure_workspace(rc_index *h, int nq, int k) {
     const int nq2 = std::max(nq, h->ws_nq), k2 = std::max(k, h->ws_k);
     dfree(h->qn);
     dfree(h->partial);
+    dfree(h->partial2);
     h->qn = nullptr;
     h->partial = nullptr;
+    h->partial2 = nullptr;
     h->qn = (float *)dmalloc((size_t)nq2 * h->ld * sizeof(float));
     h->partial = (uint64_t *)dmalloc((size_t)kMaxBlocks * nq2 * k2 * sizeof(uint64_t));
+    h->partial2 = (uint64_t *)dmalloc((size_t)(kMaxBlocks / MERGE_L1) * nq2 * k2 * sizeof(uint64_t));
     h->ws_nq = nq2;
     h->ws_k = k2;
 }
@@ -349,9 +375,22 @@ void launch_scan(rc_index *h, const ScanArgs &a) {
     }
 }
 
+// Top-k over nlist partial lists per query: one block per query, or — past 2·MERGE_L1 lists,
+// when the first-level buffer covers them (the scan's own h->partial) — two levels
+// (merge_stage1_kernel, then one block over its ceil(nlist / MERGE_L1) lists).  Same keys, same
+// total order: the result is identical either way.
 template <int CAP>
 void launch_merge_partials_t(rc_index *h, const uint64_t *partial, const int *flags, int nlist, int nq, int nq_stride, int k,
                              float *scores, int64_t *rows, hipStream_t s) {
+    const bool two = nlist > 2 * MERGE_L1 && nlist <= kMaxBlocks && nq_stride <= h->ws_nq && k <= h->ws_k;
+    if (two) {
+        const int G = (nlist + MERGE_L1 - 1) / MERGE_L1;
+        hipLaunchKernelGGL(merge_stage1_kernel<CAP>, dim3(G, nq), dim3(256), 0, s, partial, nlist, nq_stride, k, flags,
+                           h->partial2);
+        RC_LAUNCH_CHECK();
+        partial = h->partial2;
+        nlist = G;
+    }
     hipLaunchKernelGGL(merge_partials_kernel<CAP>, dim3(nq), dim3(256), 0, s, partial, nlist, nq_stride, k, h->row_base,
                        h->row_stride, flags, scores, rows);
     RC_LAUNCH_CHECK();
@@ -539,6 +578,7 @@ int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t ro
             dfree(h->norms);
             dfree(h->qn);
             dfree(h->partial);
+            dfree(h->partial2);
             delete h;
             throw;
         }
@@ -558,6 +598,7 @@ int rc_index_destroy(rc_index *h) {
         dfree(h->norms);
         dfree(h->qn);
         dfree(h->partial);
+        dfree(h->partial2);
         if (h->q1_done != nullptr) (void)hipHostFree(h->q1_done);
         delete h;
     });

@@ -345,9 +345,9 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
 // Diagnostic builds: the A/B kernel for a full-batch projection.  The residual producers
 // (O-proj, fc2; auto = image-aligned tiles) take GEMM_PINGPONG / GEMM_W2 / GEMM_PP_IMG;
 // ping-pong ablations (100 + ABL) apply where auto picks the 256-row ping-pong kernel.
-int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue) {
+int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_epilogue) {
     if (variant == GEMM_AUTO) return variant;
-    const int pick = gemm_pick(a, GEMM_AUTO, patch_epilogue);
+    const int pick = gemm_pick(a, GEMM_AUTO, patch_epilogue, ln_epilogue);
     if (pick == GEMM_PP_IMG && (variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG)) return variant;
     if (pick == GEMM_PINGPONG && variant >= 100 && variant < 200) return variant;
     return GEMM_AUTO;
@@ -362,7 +362,7 @@ void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
     const int t1 = role >= 0 ? m->timers[role].begin(s) : -1;
     int variant = GEMM_AUTO;
 #if defined(RC_GEMM_ABLATION)
-    variant = diag_variant(a, m->gemm_variant, epi_patch(EPI));
+    variant = diag_variant(a, m->gemm_variant, epi_patch(EPI), epi_ln(EPI));
 #endif
     launch_gemm<EPI>(a, variant, s);
     if (role >= 0) m->timers[role].end(t1, s, flops);
