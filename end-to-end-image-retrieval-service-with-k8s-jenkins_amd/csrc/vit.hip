@@ -883,6 +883,10 @@ extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint1
     return guard([&] {
         RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
         GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
+        if (variant == GEMM_PP_IMG) {  // image-aligned tiles: `tokens` rows per image (residual epilogue)
+            RC_REQUIRE(epi == EPI_RESID_F32 && tokens > 0, RC_ERR_INVALID, "variant 10: epi 2 and tokens (rows per image)");
+            a.row_step = tokens;
+        }
         hipStream_t s = (hipStream_t)stream;
         switch (epi) {
             case EPI_BF16: launch_gemm<EPI_BF16>(a, variant, s); break;

@@ -300,9 +300,10 @@ int rc_model_timing_reset(rc_model *m);
  * out = epilogue(A[M][K] · W[N][K]ᵀ + bias): epi 0 → bf16 out, 1 → bf16 GELU(out),
  * 2 → f32 out += (residual, in place), 3 → f32 patch scatter (+pos, tokens/image).
  * A must have round_up(M, 256) readable rows; N % 256 == 0 (M > 256), K % 64 == 0.
- * variant: 0 auto, 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256)
- * (the image-aligned 224-row tiles the model's O-proj / fc2 run need rc_embed's
- * residual stream and are reached through it). */
+ * variant: 0 auto, 4 256x256 ping-pong, 8 128x256 two-workgroup, 9 skinny (M <= 256),
+ * 10 image-aligned 224-row tiles (the model's O-proj / fc2 kernel; epi 2 only, `tokens` =
+ * rows per image, tile t = rows [t·tokens, t·tokens + tokens); A must then hold
+ * ceil(M / tokens)·tokens + 224 − tokens readable rows). */
 int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint16_t *W, const float *bias, int M, int N, int K,
                  void *out, const float *pos, int tokens, void *stream);
 

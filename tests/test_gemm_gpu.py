@@ -24,7 +24,7 @@ def run(epi, variant, A, W, bias, M, out, pos=None, tokens=0):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [4, 8])
 @pytest.mark.parametrize("M,N,K", [(300, 768, 768), (1000, 2304, 768), (513, 3072, 768), (257, 768, 3072), (64, 256, 64)])
 @pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
 def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
@@ -60,7 +60,7 @@ def test_skinny_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
     test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 11])
+@pytest.mark.parametrize("variant", [4, 8])
 def test_patch_epilogue_scatter(cuda, variant):
     import torch
 
@@ -80,3 +80,32 @@ def test_patch_epilogue_scatter(cuda, variant):
     assert torch.allclose(got[:, 1:], ref, atol=1e-4, rtol=1e-4)
     assert bool((got[:, 0] == -3.0).all())  # CLS rows are not the GEMM's
 
+
+
+@pytest.mark.parametrize("M,K", [(5 * 197, 768), (5 * 197 + 50, 3072), (2 * 197, 768), (197 + 1, 3072)])
+def test_image_aligned_tiles_match_torch_fp32(cuda, M, K):
+    """Variant 10 (the model's O-proj / fc2 kernel): 224-row tiles, tile t = rows [197 t, 197 t + 197),
+    f32 residual epilogue; a ragged last image (M not a multiple of 197) and rows >= M untouched.
+    The A buffer holds 224 - 197 rows past the last tile's start (the model pads 256)."""
+    import torch
+
+    N, T = 768, 197
+    g = torch.Generator(device=cuda).manual_seed(M + K)
+    Mp = (M + 255) // 256 * 256 + 256
+    A = (torch.randn(Mp, K, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
+    A[M:] = 0
+    W = (torch.randn(N, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    ref = A[:M].float() @ W.float().T + bias
+    resid = torch.randn(Mp, N, device=cuda, generator=g)
+    out = resid.clone()
+    L = import_pkg("_lib")
+    L.check(L.load().rc_gemm_bf16(EPI_RESID, 10, A.data_ptr(), W.data_ptr(), bias.data_ptr(), M, N, K, out.data_ptr(),
+                                  None, T, torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.allclose(out[:M], resid[:M] + ref, atol=1e-4, rtol=1e-4)
+    assert torch.equal(out[M:], resid[M:])
+    # the same bits as the 256-row ping-pong tile (one K order for every kernel)
+    out4 = resid.clone()
+    run(EPI_RESID, 4, A, W, bias, M, out4)
+    assert torch.equal(out[:M], out4[:M])
