@@ -89,6 +89,8 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // diagnostic builds only: rc_diag_set_gemm_variant
+    int attn_form = 3;             // attention_v3_kernel (persistent, register-prefetched); diag builds: 2 = v2
+    int ncu = 256;                 // compute units (persistent grids)
     int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
     int split_min = 32;            // fewest images per part
@@ -511,12 +513,22 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             break;
         }
         const int ta = m->timers[T_ATTN].begin(s);
-        if (T == 197)
-            hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+        const int items = n * c.heads;
+        if (m->attn_form == 3) {  // persistent: two blocks per CU walk the (image, head) items
+            const int nb = std::min(items, 2 * m->ncu);
+            if (T == 197)
+                hipLaunchKernelGGL(attention_v3_kernel<197>, dim3(nb), dim3(256), 0, s, qkv, attn, T, c.heads, items,
+                                   scale * 1.4426950408889634f);
+            else
+                hipLaunchKernelGGL(attention_v3_kernel<0>, dim3(nb), dim3(256), 0, s, qkv, attn, T, c.heads, items,
+                                   scale * 1.4426950408889634f);
+        } else if (T == 197) {
+            hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(items), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
-        else
-            hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(n * c.heads), dim3(256), 0, s, qkv, attn, T, c.heads,
+        } else {
+            hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(items), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
+        }
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
         {
@@ -633,6 +645,7 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));
             build_lut(m);
+            RC_HIP(hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, device));
             RC_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
             for (int p = 1; p < kMaxParts; ++p) {
                 RC_HIP(hipStreamCreateWithFlags(&m->sp[p], hipStreamNonBlocking));
@@ -862,6 +875,16 @@ int rc_model_timing_reset(rc_model *m) {
 // GEMM kernels' phase stamps, or null to stop stamping
 extern "C" int rc_diag_set_stamps(void *dev) {
     return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rc_stamps), &dev, sizeof(dev))); });
+}
+
+// diagnostic builds: attention_v2_kernel (2) or attention_v3_kernel (3, the product's) for the
+// full-token layers (A/B; the same bits)
+extern "C" int rc_diag_set_attention(rc_model *m, int form) {
+    return guard([&] {
+        RC_REQUIRE(m && (form == 2 || form == 3), RC_ERR_INVALID, "attention form must be 2 or 3");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->attn_form = form;
+    });
 }
 
 // diagnostic builds: the A/B kernel of the full-batch projections (diag_variant); not in the

@@ -592,6 +592,101 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     }
 }
 
+// Self-attention v3: the per-(image, head) arithmetic of attention_v2_kernel (att_scores /
+// att_pv_store: the same bits), re-scheduled so that HBM never idles.  In v2 every block loads
+// its K and V, then computes, then stores — and with all blocks of a round doing the same
+// thing at the same time, the chip alternates between an HBM-bound load phase and a latency-
+// bound math phase (0.5 of HBM, mfma_busy 0.18).  Here the grid is persistent: two blocks per
+// CU, each walking items (image, head) = blockIdx.x, + gridDim.x, ...; while it computes item i
+// from LDS, the block's lanes already hold item i+1's Q, K and V in registers (20 16-B loads per
+// lane, issued before the math: register staging, issue early / write late), which are written
+// into LDS between two barriers once every wave is done with item i.  Q joins K and V in LDS
+// (3 x 208 rows x 128 B = 78 KB per block, XOR-swizzled as in v2: conflict-free ds_read_b128
+// fragments and ds_write_b128 rows).
+constexpr int ATT3_CHUNKS = 3 * ATT2_ROWS * 8;             // 16-B chunks of Q, K, V (208 rows each)
+constexpr int ATT3_PER_LANE = (ATT3_CHUNKS + 255) / 256;   // 20 (the last one on lanes 0-127 only)
+
+template <int TOK>
+__global__ __launch_bounds__(256, 2) void attention_v3_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
+                                                          int tokens_rt, int heads, int items, float scale_log2e) {
+    constexpr int W = 4, HD = 64, TB = ATT2_ROWS * 128;  // waves, head dim, bytes per staged tensor
+    const int tokens = TOK > 0 ? TOK : tokens_rt;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[3 * TB];  // Q | K | V
+    const uint8_t *Qs = lds, *Ks = lds + TB, *Vs = lds + 2 * TB;
+    const int H = heads * HD, H3 = 3 * H;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    const int nqt = (tokens + 15) / 16;
+
+    // chunk c = tid + 256 i: tensor c / (208·8) (0 Q, 1 K, 2 V; the tensors sit at column
+    // offsets 0, H, 2H of a qkv row), row (c / 8) % 208, 16-B column chunk c % 8 — eight lanes
+    // read one 128-B row segment; rows >= tokens re-read the last token (finite, masked later)
+    // (tensor ts, row r) of chunk i: 208·8 = 6.5·256, so ts and r follow from compares; the
+    // column chunk is tid & 7 for every i
+    const int ch = tid & 7;
+    auto chunk_rows = [&](int i, int &ts, int &r) {
+        const int c = tid + 256 * i;
+        ts = (c >= ATT2_ROWS * 8) + (c >= 2 * ATT2_ROWS * 8);
+        r = (c - ts * (ATT2_ROWS * 8)) >> 3;
+    };
+    uint4 pf[ATT3_PER_LANE];
+    auto load_item = [&](int item) {
+        const int img = item / heads, h = item - img * heads;
+        const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD + ch * 8;
+#pragma unroll
+        for (int i = 0; i < ATT3_PER_LANE; ++i) {
+            int ts, r;
+            chunk_rows(i, ts, r);
+            const int rr = r < tokens ? r : tokens - 1;
+            if (i < ATT3_PER_LANE - 1 || tid < ATT3_CHUNKS - 256 * (ATT3_PER_LANE - 1))
+                pf[i] = *reinterpret_cast<const uint4 *>(base + (int64_t)rr * H3 + ts * H);
+        }
+    };
+    // source chunk ch of row r goes to 16-B slot ch ^ s(r): s = (r >> 1) & 7 for Q and K (the
+    // att_scores fragment reads), ((r >> 1) & 3) << 1 for V (the transposed P·V reads)
+    auto store_item = [&] {
+#pragma unroll
+        for (int i = 0; i < ATT3_PER_LANE; ++i) {
+            int ts, r;
+            chunk_rows(i, ts, r);
+            const int slot = ts == 2 ? (ch ^ (((r >> 1) & 3) << 1)) : (ch ^ ((r >> 1) & 7));
+            if (i < ATT3_PER_LANE - 1 || tid < ATT3_CHUNKS - 256 * (ATT3_PER_LANE - 1))
+                *reinterpret_cast<uint4 *>(lds + ts * TB + r * 128 + slot * 16) = pf[i];
+        }
+    };
+
+    int item = blockIdx.x;
+    if (item >= items) return;  // (the host launches at most `items` blocks)
+    load_item(item);
+    store_item();
+    __syncthreads();
+    for (; item < items; item += gridDim.x) {
+        const int nxt = item + gridDim.x;  // block-uniform
+        if (nxt < items) load_item(nxt);   // lands under this item's math
+        const int img = item / heads, h = item - img * heads;
+        uint16_t *obase = out + (int64_t)img * tokens * H + h * HD;
+        for (int qt = wave; qt < nqt; qt += W) {
+            bf16x8 qf[2];
+            const int q = qt * 16 + li;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = s * 4 + g;
+                qf[s] = *reinterpret_cast<const bf16x8 *>(Qs + q * 128 + ((c ^ ((q >> 1) & 7)) << 4));
+            }
+            f32x4 st[ATT2_TILES];
+            float sum = 0.f;
+            att_scores<TOK>(Ks, qf, tokens, scale_log2e, st, sum);
+            att_pv_store(Vs, st, sum, qt, tokens, obase, H);
+        }
+        __syncthreads();  // every wave is done reading this item from LDS
+        if (nxt < items) {
+            store_item();
+            __syncthreads();
+        }
+    }
+}
+
 // ------------------------------------------------- last layer, CLS rows only
 // /embed returns last_hidden_state[:, 0, :] (embedding/main.py:113-114), and in
 // the last encoder layer (modeling_vit_msn.py:254-283) row 0 of an image depends
