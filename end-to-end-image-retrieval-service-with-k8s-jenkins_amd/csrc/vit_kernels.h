@@ -605,6 +605,7 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
 // fragments and ds_write_b128 rows).
 constexpr int ATT3_CHUNKS = 3 * ATT2_ROWS * 8;             // 16-B chunks of Q, K, V (208 rows each)
 constexpr int ATT3_PER_LANE = (ATT3_CHUNKS + 255) / 256;   // 20 (the last one on lanes 0-127 only)
+typedef unsigned int att_u32x4 __attribute__((ext_vector_type(4)));  // (a HIP uint4 array stayed in scratch)
 
 template <int TOK>
 __global__ __launch_bounds__(256, 2) void attention_v3_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
@@ -625,13 +626,16 @@ __global__ __launch_bounds__(256, 2) void attention_v3_kernel(const uint16_t *__
     // (tensor ts, row r) of chunk i: 208·8 = 6.5·256, so ts and r follow from compares; the
     // column chunk is tid & 7 for every i
     const int ch = tid & 7;
-    auto chunk_rows = [&](int i, int &ts, int &r) {
-        const int c = tid + 256 * i;
+    // (lanes past the last chunk, i = 19, tid >= 128, re-load the last chunk: every pf[i] is loaded
+    // on every lane — no conditional load, which made hipcc keep pf in scratch — and only stored
+    // where it is real)
+    auto chunk_rows = [&](int i, int &ts, int &r) __attribute__((always_inline)) {
+        const int c = min(tid + 256 * i, ATT3_CHUNKS - 8 + ch);
         ts = (c >= ATT2_ROWS * 8) + (c >= 2 * ATT2_ROWS * 8);
         r = (c - ts * (ATT2_ROWS * 8)) >> 3;
     };
-    uint4 pf[ATT3_PER_LANE];
-    auto load_item = [&](int item) {
+    att_u32x4 pf[ATT3_PER_LANE];
+    auto load_item = [&](int item) __attribute__((always_inline)) {
         const int img = item / heads, h = item - img * heads;
         const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD + ch * 8;
 #pragma unroll
@@ -639,20 +643,19 @@ __global__ __launch_bounds__(256, 2) void attention_v3_kernel(const uint16_t *__
             int ts, r;
             chunk_rows(i, ts, r);
             const int rr = r < tokens ? r : tokens - 1;
-            if (i < ATT3_PER_LANE - 1 || tid < ATT3_CHUNKS - 256 * (ATT3_PER_LANE - 1))
-                pf[i] = *reinterpret_cast<const uint4 *>(base + (int64_t)rr * H3 + ts * H);
+            pf[i] = *reinterpret_cast<const att_u32x4 *>(base + (int64_t)rr * H3 + ts * H);
         }
     };
     // source chunk ch of row r goes to 16-B slot ch ^ s(r): s = (r >> 1) & 7 for Q and K (the
     // att_scores fragment reads), ((r >> 1) & 3) << 1 for V (the transposed P·V reads)
-    auto store_item = [&] {
+    auto store_item = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < ATT3_PER_LANE; ++i) {
             int ts, r;
             chunk_rows(i, ts, r);
             const int slot = ts == 2 ? (ch ^ (((r >> 1) & 3) << 1)) : (ch ^ ((r >> 1) & 7));
             if (i < ATT3_PER_LANE - 1 || tid < ATT3_CHUNKS - 256 * (ATT3_PER_LANE - 1))
-                *reinterpret_cast<uint4 *>(lds + ts * TB + r * 128 + slot * 16) = pf[i];
+                *reinterpret_cast<att_u32x4 *>(lds + ts * TB + r * 128 + slot * 16) = pf[i];
         }
     };
 

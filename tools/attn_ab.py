@@ -1,0 +1,60 @@
+"""Interleaved A/B of attention_v2_kernel (2) vs attention_v3_kernel (3) inside the real embed
+(diagnostic build: RC_LIB_PATH=.../lib/diag/libretrieval_core.so).  Per round and form: `steps`
+timed batch-256 embeds at PARTS (step time) and the attention launches' HIP-event time on the
+unsplit batch; the embeddings must be the same bits under both forms.
+    RC_LIB_PATH=... python tools/attn_ab.py [ROUNDS=5] [STEPS=10] [PARTS=2]
+"""
+import importlib
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+vit = importlib.import_module("end-to-end-image-retrieval-service-with-k8s-jenkins_amd.vit")
+_lib = importlib.import_module("end-to-end-image-retrieval-service-with-k8s-jenkins_amd._lib")
+rounds = int(os.environ.get("ROUNDS", "5"))
+steps = int(os.environ.get("STEPS", "10"))
+parts = int(os.environ.get("PARTS", "2"))
+B = 256
+dev = torch.device("cuda", 0)
+m = vit.VitMsnEmbedder(vit.random_state_dict(seed=0), device=0, max_batch=B)
+lib = _lib.load()
+g = torch.Generator(device=dev).manual_seed(1)
+imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
+raw = torch.empty((B, 768), device=dev)
+nrm = torch.empty((B, 768), device=dev)
+forms = [2, 3]
+res = {f: {"step_ms": [], "attn_us": []} for f in forms}
+ref = None
+for r in range(rounds):
+    for f in forms:
+        _lib.check(lib.rc_diag_set_attention(m._h, f))
+        m.set_parts(parts)
+        for _ in range(2):
+            m.embed(imgs, out=(raw, nrm))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m.embed(imgs, out=(raw, nrm))
+        torch.cuda.synchronize()
+        res[f]["step_ms"].append((time.perf_counter() - t0) / steps * 1e3)
+        if ref is None:
+            ref = raw.clone()
+        assert torch.equal(raw, ref), f"attention form {f} changed the embedding bits"
+        m.set_parts(1)
+        m.timing(["attention"])
+        m.timing_reset()
+        for _ in range(3):
+            m.embed(imgs, out=(raw, nrm))
+        torch.cuda.synchronize()
+        ms, n, _ = m.timing_read("attention")
+        res[f]["attn_us"].append(ms / max(n, 1) * 1e3)
+        m.timing(False)
+    print(json.dumps({"round": r, **{str(f): {k: round(x[-1], 2) for k, x in res[f].items()} for f in forms}}), flush=True)
+summary = {str(f): {k: round(statistics.median(x), 2) for k, x in res[f].items()} for f in forms}
+print(json.dumps({"summary_median": summary, "bit_identical": True,
+                  "units": "step_ms: ms per batch-256 embed at PARTS; attn_us: per full-token attention launch (parts 1)"}))
