@@ -513,30 +513,51 @@ __device__ __forceinline__ int sample_at(const uint8_t *__restrict__ planes, con
     return planes[blk * 64 + (y & 7) * 8 + (x & 7)];
 }
 
-// Component c's sample at output pixel (x, y) through jdsample.c's upsampler.
-__device__ __forceinline__ int upsampled(const uint8_t *__restrict__ planes, const Desc &d, int c, int x, int y) {
+// Component c's sample at output pixel (x, y) through jdsample.c's upsampler; at(c, x, y) reads
+// one stored sample (from the planes in HBM, or from a band's copy of them in LDS).
+template <typename At>
+__device__ __forceinline__ int upsampled_t(const Desc &d, int c, int x, int y, At &&at) {
     const int rx = d.rx[c], ry = d.ry[c];
-    if (rx == 1 && ry == 1) return sample_at(planes, d, c, x, y);
+    if (rx == 1 && ry == 1) return at(c, x, y);
     const int dw = d.dw[c], dh = d.dh[c];
     if (ry == 1) {  // h2v1
         const int i = x >> 1;
-        const int s = sample_at(planes, d, c, i, y);
+        const int s = at(c, i, y);
         if (dw <= 2) return s;
-        if ((x & 1) == 0) return i == 0 ? s : (3 * s + sample_at(planes, d, c, i - 1, y) + 1) >> 2;
-        return i == dw - 1 ? s : (3 * s + sample_at(planes, d, c, i + 1, y) + 2) >> 2;
+        if ((x & 1) == 0) return i == 0 ? s : (3 * s + at(c, i - 1, y) + 1) >> 2;
+        return i == dw - 1 ? s : (3 * s + at(c, i + 1, y) + 2) >> 2;
     }
     const int j = y >> 1, vv = y & 1;
     const int far = vv == 0 ? max(j - 1, 0) : min(j + 1, dh - 1);
     if (rx == 1) {  // h1v2 (always fancy)
-        return (3 * sample_at(planes, d, c, x, j) + sample_at(planes, d, c, x, far) + (vv == 0 ? 1 : 2)) >> 2;
+        return (3 * at(c, x, j) + at(c, x, far) + (vv == 0 ? 1 : 2)) >> 2;
     }
     // h2v2
     const int i = x >> 1;
-    if (dw <= 2) return sample_at(planes, d, c, i, j);
-    auto colsum = [&](int ii) { return 3 * sample_at(planes, d, c, ii, j) + sample_at(planes, d, c, ii, far); };
+    if (dw <= 2) return at(c, i, j);
+    auto colsum = [&](int ii) { return 3 * at(c, ii, j) + at(c, ii, far); };
     const int cs = colsum(i);
     if ((x & 1) == 0) return i == 0 ? (cs * 4 + 8) >> 4 : (3 * cs + colsum(i - 1) + 8) >> 4;
     return i == dw - 1 ? (cs * 4 + 7) >> 4 : (3 * cs + colsum(i + 1) + 7) >> 4;
+}
+
+__device__ __forceinline__ int upsampled(const uint8_t *__restrict__ planes, const Desc &d, int c, int x, int y) {
+    return upsampled_t(d, c, x, y, [&](int cc, int xx, int yy) { return sample_at(planes, d, cc, xx, yy); });
+}
+
+// The 8-row block rows of component c that the upsampler reads for the image rows [y_lo, y_hi):
+// [*br0, *br0 + *nbr).  A v2 component also reads the chroma row beyond each end (jdsample.c's
+// "far" row, clamped to the plane).  Host and device compute it alike (the band kernel's LDS plan).
+__host__ __device__ inline void plane_block_rows(const Desc &d, int c, int y_lo, int y_hi, int *br0, int *nbr) {
+    int r_lo = y_lo, r_hi = y_hi - 1;
+    if (d.ry[c] == 2) {
+        r_lo = (y_lo >> 1) - 1;
+        r_lo = r_lo < 0 ? 0 : r_lo;
+        r_hi = ((y_hi - 1) >> 1) + 1;
+        r_hi = r_hi > d.dh[c] - 1 ? d.dh[c] - 1 : r_hi;
+    }
+    *br0 = r_lo >> 3;
+    *nbr = (r_hi >> 3) - *br0 + 1;
 }
 
 // grid (ceil(max_pixels / 256), n): one lane per output pixel of image blockIdx.y.
@@ -701,25 +722,39 @@ __global__ __launch_bounds__(256) void jpeg_resize_v_kernel(const RDesc *__restr
 // dynamic LDS = the largest per-image need (band_lds_bytes, host).
 // LDS layout of one band: src [rows][W][3] (need_h only), tmp [rows][S][3], the band's output
 // [nout][S][3] (need_v only: over src when it fits there, else after tmp); returns the bytes.
+// (pl: the band's copy of the planes' block rows, first; every other offset is past it)
 struct BandLayout {
     int tmp, band, total;
 };
-__host__ __device__ inline BandLayout band_layout(int rows, int nout, int W, int S, int need_h, int need_v) {
+__host__ __device__ inline BandLayout band_layout(int rows, int nout, int W, int S, int need_h, int need_v, int pl) {
     auto al = [](int b) { return (b + 15) & ~15; };
     BandLayout L;
     const int src = need_h ? al(rows * W * 3) : 0;
-    L.tmp = src;
-    L.total = src + al(rows * S * 3);
+    L.tmp = pl + src;
+    L.total = L.tmp + al(rows * S * 3);
     L.band = L.tmp;  // no vertical pass: tmp is the band
     if (need_v) {
         if (nout * S * 3 <= src) {
-            L.band = 0;
+            L.band = pl;
         } else {
             L.band = L.total;
             L.total += al(nout * S * 3);
         }
     }
     return L;
+}
+
+// LDS bytes of the planes' block rows a band of image rows [y_lo, y_hi) reads (16-B aligned per
+// component; offsets written to off[c])
+__host__ __device__ inline int band_planes_bytes(const Desc &d, int y_lo, int y_hi, int *off) {
+    int total = 0;
+    for (int c = 0; c < d.ncomp; ++c) {
+        int br0, nbr;
+        plane_block_rows(d, c, y_lo, y_hi, &br0, &nbr);
+        if (off) off[c] = total;
+        total += nbr * d.bw[c] * 64;  // (a multiple of 64)
+    }
+    return total;
 }
 
 __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
@@ -735,17 +770,40 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
     const int lo = r.need_v ? r.vb[2 * yo0] : yo0;
     const int hi = r.need_v ? r.vb[2 * (yo1 - 1)] + r.vb[2 * (yo1 - 1) + 1] : yo1;
     const int rows = hi - lo, W = d.W;
-    const BandLayout L = band_layout(rows, nout, W, S, r.need_h, r.need_v);
-    uint8_t *src = lds, *tmp = lds + L.tmp, *band = lds + L.band;
+    // 0. the planes' 8-row block rows the band's colour conversion reads, copied contiguous
+    //    (block layout kept) into LDS with 16-B loads: the upsampler's 1-9 byte reads per pixel
+    //    then hit LDS instead of scattered byte loads from HBM / L2
+    int poff[3] = {0, 0, 0}, pbr0[3] = {0, 0, 0};
+    const int pl = band_planes_bytes(d, r.y0 + lo, r.y0 + hi, poff);
+    for (int c = 0; c < d.ncomp; ++c) {
+        int nbr;
+        plane_block_rows(d, c, r.y0 + lo, r.y0 + hi, &pbr0[c], &nbr);
+        const uint4 *g = reinterpret_cast<const uint4 *>(planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64);
+        uint4 *l = reinterpret_cast<uint4 *>(lds + poff[c]);
+        const int n16 = nbr * d.bw[c] * 4;
+        for (int i = threadIdx.x; i < n16; i += 256) l[i] = g[i];
+    }
+    const BandLayout L = band_layout(rows, nout, W, S, r.need_h, r.need_v, pl);
+    uint8_t *src = lds + pl, *tmp = lds + L.tmp, *band = lds + L.band;
+    __syncthreads();
+    auto at = [&](int c, int x, int y) {
+        return (int)lds[poff[c] + (((y >> 3) - pbr0[c]) * d.bw[c] + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7)];
+    };
     // 1. colour: the band's source rows (straight into tmp when the width already is S)
     {
         uint8_t *dst = r.need_h ? src : tmp;
         const int n = rows * W;
 #pragma unroll 4
-        for (int idx = threadIdx.x; idx < n; idx += 256) {  // (unrolled: several pixels' plane loads in flight)
-            const int rr = idx / W, x = idx - rr * W;
-            int R, G, B;
-            ycc_rgb(planes, d, x, r.y0 + lo + rr, R, G, B);
+        for (int idx = threadIdx.x; idx < n; idx += 256) {
+            const int rr = idx / W, x = idx - rr * W, y = r.y0 + lo + rr;
+            const int Y = upsampled_t(d, 0, x, y, at);
+            int R = Y, G = Y, B = Y;
+            if (d.ncomp != 1) {  // jdcolor.c ycc_rgb_convert, as ycc_rgb
+                const int cb = upsampled_t(d, 1, x, y, at) - 128, cr = upsampled_t(d, 2, x, y, at) - 128;
+                R = min(max(Y + ((91881 * cr + 32768) >> 16), 0), 255);
+                G = min(max(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16), 0), 255);
+                B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
+            }
             uint8_t *o = dst + 3 * idx;
             o[0] = (uint8_t)R;
             o[1] = (uint8_t)G;
@@ -1111,17 +1169,23 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
             }
             r.out_off = (int64_t)i * S * S * 3;
             maxrows = std::max(maxrows, r.Hs);
-            // band height: the tallest band (32 .. 1 output rows) whose LDS fits 32 KB, else 64 KB
+            // band height: the tallest band (32 .. 1 output rows) whose LDS (planes' block rows +
+            // colour rows + horizontal pass + band) fits 32 KB, else 64 KB — and no taller than
+            // gives the batch >= 128 blocks (a lone /embed image: 224 / 4 = 56 bands, not 7-14)
             r.bh = 0;
             int need = 0;
+            int bh_max = 32;
+            while (bh_max > 4 && (int64_t)n * ((S + bh_max - 1) / bh_max) < 128) bh_max /= 2;
+            const jpeg::Desc &dd = h->h_desc[i];
             for (const int cap : {32 * 1024, 64 * 1024}) {
-                for (int bh = 32; bh >= 1 && r.bh == 0; bh /= 2) {
+                for (int bh = bh_max; bh >= 1 && r.bh == 0; bh /= 2) {
                     int worst = 0;
                     for (int yo0 = 0; yo0 < S; yo0 += bh) {
                         const int yo1 = std::min(S, yo0 + bh);
                         const int lo = vb ? (*vb)[2 * yo0] : yo0;
                         const int hi = vb ? (*vb)[2 * (yo1 - 1)] + (*vb)[2 * (yo1 - 1) + 1] : yo1;
-                        worst = std::max(worst, jpeg::band_layout(hi - lo, yo1 - yo0, W, S, r.need_h, r.need_v).total);
+                        const int pl = jpeg::band_planes_bytes(dd, r.y0 + lo, r.y0 + hi, nullptr);
+                        worst = std::max(worst, jpeg::band_layout(hi - lo, yo1 - yo0, W, S, r.need_h, r.need_v, pl).total);
                     }
                     if (worst <= cap) {
                         r.bh = bh;

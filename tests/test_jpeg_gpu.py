@@ -187,3 +187,16 @@ def test_decode_resized_band_and_two_pass_paths(J, cuda):
                 assert np.array_equal(got[-1].cpu().numpy(), _pil_resized(wide if n == 1 else small))
     assert sum(rises[:8]) <= 6 and not any(rises[8:]), rises
     d.close()
+
+
+@pytest.mark.parametrize("resample", [3, 2])
+def test_decode_resized_single_images_fine_bands(dec, resample):
+    """One image per call (the /embed request): the band kernel splits the 224 output rows into
+    bands of <= 4 rows (>= 56 blocks for the image) — every decode case alone, bit-exact with PIL
+    decode + Image.resize; and a batch of two picks the same bands."""
+    cs = cases()
+    for name, data in cs:
+        got = dec.decode_resized([data], 224, resample)
+        assert np.array_equal(got[0].cpu().numpy(), _pil_resized(data, 224, resample)), name
+    pair = dec.decode_resized([cs[0][1], cs[-1][1]], 224, resample)
+    assert np.array_equal(pair[1].cpu().numpy(), _pil_resized(cs[-1][1], 224, resample))
