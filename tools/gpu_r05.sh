@@ -2,7 +2,7 @@
 # Round-5 GPU call: -m gpu suite, bench line, in-model A/Bs on the diagnostic build: the
 # residual-producer GEMM tiles (10 image-aligned 224-row, 8 two-workgroup 128x256, 4 ping-pong
 # 256x256) and the attention form (2 = v2, 3 = v3).
-# usage: tools/gpu_r05.sh TAG [tests|notests] [bench|nobench] [ab|noab]
+# usage: tools/gpu_r05.sh TAG [tests|notests] [bench|nobench] [ab|noab] [jpeg|nojpeg]
 set -u
 TAG=$1
 export TMPDIR=/tmp
@@ -15,6 +15,10 @@ fi
 if [ "${3:-bench}" = "bench" ]; then
 timeout -k 10 600 python -u bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err
 rc=$?; head -c 3000 gpurun_out/$TAG/bench.json; echo; [ $rc -ne 0 ] && { tail -20 gpurun_out/$TAG/bench.err; exit $rc; }
+fi
+if [ "${5:-jpeg}" = "jpeg" ]; then
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/prof_jpeg -o run --output-format csv -- python -u tools/jpeg_probe.py > gpurun_out/$TAG/jpeg_probe.log 2>&1
+rc=$?; tail -1 gpurun_out/$TAG/jpeg_probe.log; find gpurun_out/$TAG/prof_jpeg -name '*kernel_trace.csv' -delete; [ $rc -ne 0 ] && exit $rc
 fi
 if [ "${4:-ab}" = "ab" ]; then
 RC_LIB_PATH=$DIAG ROUNDS=5 STEPS=10 PARTS=2 timeout -k 10 300 python -u tools/attn_ab.py > gpurun_out/$TAG/attn_ab_p2.log 2>&1
