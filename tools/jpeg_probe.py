@@ -17,7 +17,7 @@ J = importlib.import_module("end-to-end-image-retrieval-service-with-k8s-jenkins
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 fixture = open(os.path.join(REPO, "tests", "golden", "test_image.jpeg"), "rb").read()
 batch = synthetic_jpegs(256, 7100, size=(168, 300))
-dec = J.JpegDecoder(device=0, max_images=256)
+dec = J.JpegDecoder(device=0, max_images=256, max_pixels=256 * 168 * 304)
 out = {}
 for name, datas, reps in (("fixture_shape_256", batch, 20), ("fixture_1", [fixture], 200)):
     for _ in range(3):
