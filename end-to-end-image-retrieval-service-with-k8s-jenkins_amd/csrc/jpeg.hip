@@ -757,6 +757,13 @@ __host__ __device__ inline int band_planes_bytes(const Desc &d, int y_lo, int y_
     return total;
 }
 
+// MAXT > 0: every image's horizontal taps fit MAXT (the coefficient table's ksize <= MAXT:
+// Pillow bicubic down to a 1.5x downscale): a lane owns output columns and keeps their
+// bounds and coefficients in registers across the band's rows (taps past a column's count
+// have coefficient 0, and their pixel index is clamped into the row: exact).  MAXT = 0: the
+// general form (coefficients read per output).  The vertical pass's bounds and coefficients
+// depend on the output row only: wave-uniform (scalar loads) in both forms.
+template <int MAXT>
 __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
                                                               const Desc *__restrict__ descs,
                                                               const RDesc *__restrict__ rdescs, uint8_t *__restrict__ out) {
@@ -789,13 +796,15 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
     auto at = [&](int c, int x, int y) {
         return (int)lds[poff[c] + (((y >> 3) - pbr0[c]) * d.bw[c] + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7)];
     };
-    // 1. colour: the band's source rows (straight into tmp when the width already is S)
+    // 1. colour: the band's source rows (straight into tmp when the width already is S); pixel
+    //    idx = rr·W + x walked by (rr, x) increments (no division per pixel)
     {
         uint8_t *dst = r.need_h ? src : tmp;
         const int n = rows * W;
-#pragma unroll 4
+        int rr = threadIdx.x / W, x = threadIdx.x - rr * W;
+        const int drr = 256 / W, dx = 256 - drr * W;
         for (int idx = threadIdx.x; idx < n; idx += 256) {
-            const int rr = idx / W, x = idx - rr * W, y = r.y0 + lo + rr;
+            const int y = r.y0 + lo + rr;
             const int Y = upsampled_t(d, 0, x, y, at);
             int R = Y, G = Y, B = Y;
             if (d.ncomp != 1) {  // jdcolor.c ycc_rgb_convert, as ycc_rgb
@@ -808,51 +817,84 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
             o[0] = (uint8_t)R;
             o[1] = (uint8_t)G;
             o[2] = (uint8_t)B;
+            rr += drr;
+            x += dx;
+            if (x >= W) {
+                x -= W;
+                ++rr;
+            }
         }
     }
     __syncthreads();
     // 2. horizontal pass (Pillow's fixed point: 22 fractional bits, rounding 1 << 21, clip)
     if (r.need_h) {
-        const int n = rows * S;
-        for (int idx = threadIdx.x; idx < n; idx += 256) {
-            const int rr = idx / S, xo = idx - rr * S;
-            const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
-            const int *c = r.hc + xo * r.hk;
-            const uint8_t *p = src + (rr * W + xmin) * 3;
-            int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-            for (int k = 0; k < xn; ++k) {
-                const int ck = c[k];
-                a0 += p[3 * k] * ck;
-                a1 += p[3 * k + 1] * ck;
-                a2 += p[3 * k + 2] * ck;
+        if constexpr (MAXT > 0) {
+            for (int xo = threadIdx.x; xo < S; xo += 256) {
+                const int xmin = r.hb[2 * xo];
+                int cf[MAXT], px[MAXT];
+#pragma unroll
+                for (int k = 0; k < MAXT; ++k) {
+                    cf[k] = k < r.hk ? r.hc[xo * r.hk + k] : 0;
+                    px[k] = 3 * min(xmin + k, W - 1);
+                }
+                for (int rr = 0; rr < rows; ++rr) {
+                    const uint8_t *p = src + rr * W * 3;
+                    int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+#pragma unroll
+                    for (int k = 0; k < MAXT; ++k) {
+                        a0 += p[px[k]] * cf[k];
+                        a1 += p[px[k] + 1] * cf[k];
+                        a2 += p[px[k] + 2] * cf[k];
+                    }
+                    uint8_t *o = tmp + (rr * S + xo) * 3;
+                    o[0] = clip8_22(a0);
+                    o[1] = clip8_22(a1);
+                    o[2] = clip8_22(a2);
+                }
             }
-            uint8_t *o = tmp + 3 * idx;
-            o[0] = clip8_22(a0);
-            o[1] = clip8_22(a1);
-            o[2] = clip8_22(a2);
+        } else {
+            const int n = rows * S;
+            for (int idx = threadIdx.x; idx < n; idx += 256) {
+                const int rr = idx / S, xo = idx - rr * S;
+                const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
+                const int *c = r.hc + xo * r.hk;
+                const uint8_t *p = src + (rr * W + xmin) * 3;
+                int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+                for (int k = 0; k < xn; ++k) {
+                    const int ck = c[k];
+                    a0 += p[3 * k] * ck;
+                    a1 += p[3 * k + 1] * ck;
+                    a2 += p[3 * k + 2] * ck;
+                }
+                uint8_t *o = tmp + 3 * idx;
+                o[0] = clip8_22(a0);
+                o[1] = clip8_22(a1);
+                o[2] = clip8_22(a2);
+            }
         }
         __syncthreads();
     }
-    // 3. vertical pass into the band's LDS image (over src, free now, when it fits), then 16-B stores
+    // 3. vertical pass into the band's LDS image (over src, free now, when it fits), then 16-B
+    //    stores: a lane owns columns, the band's output rows (and their taps) are wave-uniform
     if (r.need_v) {
-        const int n = nout * S;
-        for (int idx = threadIdx.x; idx < n; idx += 256) {
-            const int j = idx / S, x = idx - j * S, yo = yo0 + j;
-            const int ymin = r.vb[2 * yo] - lo, yn = r.vb[2 * yo + 1];
-            const int *c = r.vc + yo * r.vk;
-            const uint8_t *q = tmp + (ymin * S + x) * 3;
-            int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-            for (int k = 0; k < yn; ++k) {
-                const int ck = c[k];
-                a0 += q[k * S * 3] * ck;
-                a1 += q[k * S * 3 + 1] * ck;
-                a2 += q[k * S * 3 + 2] * ck;
+        for (int x = threadIdx.x; x < S; x += 256)
+            for (int j = 0; j < nout; ++j) {
+                const int yo = yo0 + j;
+                const int ymin = r.vb[2 * yo] - lo, yn = r.vb[2 * yo + 1];
+                const int *c = r.vc + yo * r.vk;
+                const uint8_t *q = tmp + (ymin * S + x) * 3;
+                int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+                for (int k = 0; k < yn; ++k) {
+                    const int ck = c[k];
+                    a0 += q[k * S * 3] * ck;
+                    a1 += q[k * S * 3 + 1] * ck;
+                    a2 += q[k * S * 3 + 2] * ck;
+                }
+                uint8_t *o = band + (j * S + x) * 3;
+                o[0] = clip8_22(a0);
+                o[1] = clip8_22(a1);
+                o[2] = clip8_22(a2);
             }
-            uint8_t *o = band + 3 * idx;
-            o[0] = clip8_22(a0);
-            o[1] = clip8_22(a1);
-            o[2] = clip8_22(a2);
-        }
         __syncthreads();
     }
     uint8_t *g = out + r.out_off + (int64_t)yo0 * S * 3;
@@ -1135,7 +1177,7 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
         stage_idct(h, n, jpgs, lens, nullptr, s, hd, maxpix);
         const int S = out_size;
         int64_t tmp_need = 0;
-        int maxrows = 1, maxbands = 1, band_lds = 0;
+        int maxrows = 1, maxbands = 1, band_lds = 0, max_hk = 0;
         bool band_ok = true;  // every image's bands fit in LDS: the band kernel, else the two-pass path
         for (int i = 0; i < n; ++i) {
             const int W = hd[i].width, H = hd[i].height;
@@ -1150,6 +1192,7 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
                 r.hb = ch.bounds;
                 r.hc = ch.coef;
                 r.hk = ch.ksize;
+                max_hk = std::max(max_hk, r.hk);
             }
             const std::vector<int> *vb = nullptr;
             if (r.need_v) {
@@ -1203,8 +1246,13 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
         if (band_ok) {
             RC_HIP(hipMemcpyAsync(h->d_rdesc, h->h_rdesc, (size_t)n * sizeof(jpeg::RDesc), hipMemcpyHostToDevice, s));
             RC_HIP(hipEventRecord(h->staged, s));
-            hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel, dim3((unsigned)maxbands, (unsigned)n), dim3(256),
-                               (size_t)band_lds, s, h->d_planes, h->d_desc, h->d_rdesc, out);
+            const dim3 gr((unsigned)maxbands, (unsigned)n);
+            if (max_hk <= 8)  // every horizontal pass within 8 taps: coefficients in registers
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<8>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+                                   h->d_desc, h->d_rdesc, out);
+            else
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<0>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+                                   h->d_desc, h->d_rdesc, out);
             RC_LAUNCH_CHECK();
             return;
         }

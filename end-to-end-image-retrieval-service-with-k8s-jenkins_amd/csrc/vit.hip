@@ -89,7 +89,7 @@ struct rc_model {
     size_t resize_tmp_bytes = 0;
     KernelTimer timers[T_COUNT];
     int gemm_variant = GEMM_AUTO;  // diagnostic builds only: rc_diag_set_gemm_variant
-    int attn_form = 3;             // attention_v3_kernel (persistent, register-prefetched); diag builds: 2 = v2
+    int attn_form = 2;             // attention_v2_kernel; diag builds: 3 = attention_v3_kernel (A/B: v3 lost, 92 vs 75 us)
     int ncu = 256;                 // compute units (persistent grids)
     int split = 2;                 // batch parts encoded concurrently (rc_model_set_parts);
                                    // 2 beats 3 and 4 by 1-2 % at batch 256 (profiles/r01j_ab_parts.jsonl)
@@ -351,6 +351,8 @@ int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_ep
     if (variant == GEMM_AUTO) return variant;
     const int pick = gemm_pick(a, GEMM_AUTO, patch_epilogue, ln_epilogue);
     if (pick == GEMM_PP_IMG && (variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG)) return variant;
+    if (pick == GEMM_PP_IMG && variant == 11) return a.K <= 768 ? GEMM_W2 : GEMM_PP_IMG;  // O-proj two-workgroup, fc2 image-aligned
+    if (pick == GEMM_PP_IMG && variant == 12) return a.K <= 768 ? GEMM_W2 : GEMM_PINGPONG;  // the round-4 product
     if (pick == GEMM_PINGPONG && variant >= 100 && variant < 200) return variant;
     return GEMM_AUTO;
 }
@@ -514,15 +516,14 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
         }
         const int ta = m->timers[T_ATTN].begin(s);
         const int items = n * c.heads;
+#if defined(RC_GEMM_ABLATION)
         if (m->attn_form == 3) {  // persistent: two blocks per CU walk the (image, head) items
             const int nb = std::min(items, 2 * m->ncu);
-            if (T == 197)
-                hipLaunchKernelGGL(attention_v3_kernel<197>, dim3(nb), dim3(256), 0, s, qkv, attn, T, c.heads, items,
-                                   scale * 1.4426950408889634f);
-            else
-                hipLaunchKernelGGL(attention_v3_kernel<0>, dim3(nb), dim3(256), 0, s, qkv, attn, T, c.heads, items,
-                                   scale * 1.4426950408889634f);
-        } else if (T == 197) {
+            hipLaunchKernelGGL(attention_v3_kernel<197>, dim3(nb), dim3(256), 0, s, qkv, attn, T, c.heads, items,
+                               scale * 1.4426950408889634f);
+        } else
+#endif
+        if (T == 197) {
             hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(items), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f);
         } else {
@@ -893,7 +894,7 @@ extern "C" int rc_diag_set_gemm_variant(rc_model *m, int variant) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG ||
-                       (variant >= 100 && variant < 200),
+                       variant == 11 || variant == 12 || (variant >= 100 && variant < 200),
                    RC_ERR_INVALID, "GEMM variant: 0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 100 + ABL");
         std::lock_guard<std::mutex> lk(m->mu);
         m->gemm_variant = variant;

@@ -607,6 +607,9 @@ constexpr int ATT3_CHUNKS = 3 * ATT2_ROWS * 8;             // 16-B chunks of Q, 
 constexpr int ATT3_PER_LANE = (ATT3_CHUNKS + 255) / 256;   // 20 (the last one on lanes 0-127 only)
 typedef unsigned int att_u32x4 __attribute__((ext_vector_type(4)));  // (a HIP uint4 array stayed in scratch)
 
+// (Diagnostic builds only, rc_diag_set_attention: measured 92.4 vs 75.3 us per launch for v2 —
+// two blocks of 4 waves per CU leave the latency-bound math too few waves, and each item's
+// barrier waits for the wave with the 13th query tile; profiles/r05/.)
 template <int TOK>
 __global__ __launch_bounds__(256, 2) void attention_v3_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
                                                           int tokens_rt, int heads, int items, float scale_log2e) {

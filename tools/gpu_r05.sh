@@ -23,8 +23,8 @@ fi
 if [ "${4:-ab}" = "ab" ]; then
 RC_LIB_PATH=$DIAG ROUNDS=5 STEPS=10 PARTS=2 timeout -k 10 300 python -u tools/attn_ab.py > gpurun_out/$TAG/attn_ab_p2.log 2>&1
 rc=$?; tail -1 gpurun_out/$TAG/attn_ab_p2.log; [ $rc -ne 0 ] && exit $rc
-RC_LIB_PATH=$DIAG VARIANTS=10,8,4 ROUNDS=5 STEPS=10 PARTS=2 timeout -k 10 400 python -u tools/gemm_ab.py > gpurun_out/$TAG/gemm_ab_p2.log 2>&1
+RC_LIB_PATH=$DIAG VARIANTS=${GV:-12,11,10} ROUNDS=5 STEPS=10 PARTS=2 timeout -k 10 400 python -u tools/gemm_ab.py > gpurun_out/$TAG/gemm_ab_p2.log 2>&1
 rc=$?; tail -1 gpurun_out/$TAG/gemm_ab_p2.log; [ $rc -ne 0 ] && exit $rc
-RC_LIB_PATH=$DIAG VARIANTS=10,8,4 ROUNDS=5 STEPS=10 PARTS=1 timeout -k 10 400 python -u tools/gemm_ab.py > gpurun_out/$TAG/gemm_ab_p1.log 2>&1
+RC_LIB_PATH=$DIAG VARIANTS=${GV:-12,11,10} ROUNDS=5 STEPS=10 PARTS=1 timeout -k 10 400 python -u tools/gemm_ab.py > gpurun_out/$TAG/gemm_ab_p1.log 2>&1
 rc=$?; tail -1 gpurun_out/$TAG/gemm_ab_p1.log; exit $rc
 fi
