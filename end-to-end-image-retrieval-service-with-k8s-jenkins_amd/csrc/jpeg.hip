@@ -548,7 +548,7 @@ __device__ __forceinline__ int upsampled(const uint8_t *__restrict__ planes, con
 // The 8-row block rows of component c that the upsampler reads for the image rows [y_lo, y_hi):
 // [*br0, *br0 + *nbr).  A v2 component also reads the chroma row beyond each end (jdsample.c's
 // "far" row, clamped to the plane).  Host and device compute it alike (the band kernel's LDS plan).
-__host__ __device__ inline void plane_block_rows(const Desc &d, int c, int y_lo, int y_hi, int *br0, int *nbr) {
+__host__ __device__ __forceinline__ void plane_block_rows(const Desc &d, int c, int y_lo, int y_hi, int *br0, int *nbr) {
     int r_lo = y_lo, r_hi = y_hi - 1;
     if (d.ry[c] == 2) {
         r_lo = (y_lo >> 1) - 1;
@@ -780,15 +780,27 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
     // 0. the planes' 8-row block rows the band's colour conversion reads, copied contiguous
     //    (block layout kept) into LDS with 16-B loads: the upsampler's 1-9 byte reads per pixel
     //    then hit LDS instead of scattered byte loads from HBM / L2
-    int poff[3] = {0, 0, 0}, pbr0[3] = {0, 0, 0};
-    const int pl = band_planes_bytes(d, r.y0 + lo, r.y0 + hi, poff);
-    for (int c = 0; c < d.ncomp; ++c) {
-        int nbr;
-        plane_block_rows(d, c, r.y0 + lo, r.y0 + hi, &pbr0[c], &nbr);
-        const uint4 *g = reinterpret_cast<const uint4 *>(planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64);
-        uint4 *l = reinterpret_cast<uint4 *>(lds + poff[c]);
-        const int n16 = nbr * d.bw[c] * 4;
-        for (int i = threadIdx.x; i < n16; i += 256) l[i] = g[i];
+    //    (components unrolled with constant indices: a runtime-indexed Desc / offset array would
+    //    live in scratch memory, one scratch load per sample read)
+    int poff[3], pbr0[3], pnbr[3];
+    int pl = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        poff[c] = pl;
+        pbr0[c] = pnbr[c] = 0;
+        if (c < d.ncomp) {
+            plane_block_rows(d, c, r.y0 + lo, r.y0 + hi, &pbr0[c], &pnbr[c]);
+            pl += pnbr[c] * d.bw[c] * 64;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        if (c < d.ncomp) {
+            const uint4 *g = reinterpret_cast<const uint4 *>(planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64);
+            uint4 *l = reinterpret_cast<uint4 *>(lds + poff[c]);
+            const int n16 = pnbr[c] * d.bw[c] * 4;
+            for (int i = threadIdx.x; i < n16; i += 256) l[i] = g[i];
+        }
     }
     const BandLayout L = band_layout(rows, nout, W, S, r.need_h, r.need_v, pl);
     uint8_t *src = lds + pl, *tmp = lds + L.tmp, *band = lds + L.band;
