@@ -313,8 +313,13 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
     log("bench: latency search top-5")
     out["search_top5"] = dict(_lat(lambda: ret.search(ix, vec, top_k=5), reps * 5),
                               what="retriever.utils.search(index, emb, top_k=5) over 10,000 x 768 f32 rows "
-                                   "(index.query with include_values=True, as the reference calls it)",
+                                   "(index.query with include_values=True, as the reference calls it), emb as "
+                                   "embed_bytes returns it in process (retriever/main.py:122-128)",
                               planted_found=sorted(got) == sorted(f"r{r}" for r in planted))
+    plain = [float(x) for x in vec]  # the same vector as a plain JSON list (an HTTP client's body)
+    out["search_top5"]["plain_list"] = dict(
+        _lat(lambda: ret.search(ix, plain, top_k=5), reps * 5),
+        what="the same search with emb a plain list of 768 Python floats (parsed to f32 per call)")
     # where a request's time goes: the library call alone (one launch pair + sync, results as host
     # arrays) and the Python list building the Pinecone-shaped response needs on top
     qv = np.ascontiguousarray(np.asarray(vec, np.float32)[None])
@@ -324,9 +329,9 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
     vals = np.zeros((5, 768), np.float32)
     idxmod = importlib.import_module(f"{pkg}.index")
     out["search_top5"]["python_lists"] = dict(
-        _lat(lambda: (idxmod._as_vector_np(vec, 768), vals.astype(np.float64).tolist()), reps * 5),
-        what="the response's Python side alone (as Index.query does it): the 768-float query list to an "
-             "array, 5 x 768 values to lists")
+        _lat(lambda: (idxmod._as_vector_np(plain, 768), vals.astype(np.float64).tolist()), reps * 5),
+        what="what the request path no longer does: a 768-float query list parsed to an array, and 5 x 768 "
+             "values built as lists (Index.query's matches build them only when read)")
     from fastapi.testclient import TestClient
 
     log("bench: latency /search_image")

@@ -142,9 +142,14 @@ def embed_many_device(blobs: List[bytes], normalized: bool = False):
 
 
 def embed_many(blobs: List[bytes]) -> list[list[float]]:
-    """Image bytes → raw CLS vectors: GPU JPEG decode where it applies, PIL otherwise."""
+    """Image bytes → raw CLS vectors: GPU JPEG decode where it applies, PIL otherwise.  Each
+    vector is a list of Python floats (the /embed body) that also carries its float32 row
+    (``index.F32List``), for in-process callers that hand it straight to ``index.query``."""
+    from ..index import F32List
+
     raw, _ = embed_many_device(blobs)
-    return raw.cpu().tolist()
+    a = raw.cpu().numpy()
+    return [F32List(row.tolist(), row) for row in a]
 
 
 def embed_bytes(data: bytes) -> list[float]:

@@ -305,6 +305,54 @@ class Record(dict):
         return (dict, (dict(dict.items(self)),))
 
 
+class F32List(list):
+    """A list of floats (an embedding as ``/embed`` returns it) that also carries the float32
+    array it was made from, so an in-process ``search`` (retriever/main.py:122-128: the
+    feature goes straight back into ``index.query``) skips re-parsing 768 Python floats.  Any
+    mutation drops the array; the list is then parsed like any other."""
+
+    __slots__ = ("f32",)
+
+    def __init__(self, values=(), f32: np.ndarray | None = None):
+        super().__init__(values)
+        self.f32 = f32
+
+    def __setitem__(self, *a):
+        self.f32 = None
+        return list.__setitem__(self, *a)
+
+    def __delitem__(self, *a):
+        self.f32 = None
+        return list.__delitem__(self, *a)
+
+    def __iadd__(self, other):
+        self.f32 = None
+        return list.__iadd__(self, other)
+
+    def __imul__(self, n):
+        self.f32 = None
+        return list.__imul__(self, n)
+
+    def __reduce__(self):  # pickles / copies as the plain list
+        return (list, (list(self),))
+
+
+def _invalidating(name):
+    base = getattr(list, name)
+
+    def method(self, *a, **k):
+        self.f32 = None
+        return base(self, *a, **k)
+
+    method.__name__ = name
+    return method
+
+
+for _m in ("append", "extend", "insert", "pop", "remove", "reverse", "sort", "clear"):
+    setattr(F32List, _m, _invalidating(_m))
+del _m
+
+
 def _as_vector(values: Any, dim: int) -> list[float]:
     if isinstance(values, torch.Tensor):
         values = values.detach().cpu().reshape(-1).tolist()
@@ -319,7 +367,9 @@ def _as_vector(values: Any, dim: int) -> list[float]:
 def _as_vector_np(values: Any, dim: int) -> np.ndarray:
     """``_as_vector`` as a C-contiguous f32 [1, dim] host array (the request path: no per-element
     Python loop)."""
-    if isinstance(values, torch.Tensor):
+    if type(values) is F32List and values.f32 is not None:  # an in-process embedding: its own f32 row
+        a = values.f32
+    elif isinstance(values, torch.Tensor):
         a = values.detach().to(device="cpu", dtype=torch.float32).reshape(-1).numpy()
     else:
         a = None
@@ -368,6 +418,7 @@ class ShardSet:
         # this counts the extra xGMI traffic
         self.cross_device_rows = 0
         self._qbufs: dict = {}  # query_host's reused host buffers per (nq, k, values)
+        self._query_fn = self.lib.rc_sharded_query_host
         self._shards = []
         for sh in range(self.n):
             ih = _lib.C.c_void_p()
@@ -487,12 +538,15 @@ class ShardSet:
         if bufs is None:
             if len(self._qbufs) > 16:
                 self._qbufs.clear()
-            bufs = (np.empty((nq, k), np.float32), np.empty((nq, k), np.int64),
-                    np.empty((nq, k, self.dim), np.float32) if with_values else None)
+            sc = np.empty((nq, k), np.float32)
+            rw = np.empty((nq, k), np.int64)
+            val = np.empty((nq, k, self.dim), np.float32) if with_values else None
+            # the buffers' addresses once (ctypes attribute reads cost ~1 us each per call)
+            ptrs = (int(bool(with_values)), sc.ctypes.data, rw.ctypes.data, val.ctypes.data if val is not None else None)
+            bufs = (sc, rw, val, ptrs)
             self._qbufs[key] = bufs
-        sc, rw, val = bufs
-        check(self.lib.rc_sharded_query_host(self.handle, q.ctypes.data, nq, int(n_rows), int(k), int(bool(with_values)),
-                                             sc.ctypes.data, rw.ctypes.data, val.ctypes.data if val is not None else None))
+        sc, rw, val, ptrs = bufs
+        check(self._query_fn(self._h, q.ctypes.data, nq, n_rows, k, ptrs[0], ptrs[1], ptrs[2], ptrs[3]))
         return sc, rw, val
 
     def fetch_rows(self, rows, stored: bool = False) -> torch.Tensor:

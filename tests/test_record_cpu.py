@@ -69,3 +69,24 @@ def test_query_vector_rejects_nested_lists():
     for bad in ([v], np.asarray([v])):
         with pytest.raises(TypeError):
             ix._as_vector_np(bad, 8)
+
+
+def test_f32list_carries_its_row_until_mutated():
+    """An in-process embedding (index.F32List) is a plain list of floats for every reader, hands
+    its float32 row to the query parser, and any mutation makes the parser read the list again."""
+    ix = import_pkg("index")
+    row = np.array([0.5, -2.0, 3.25, 1.0], np.float32)
+    v = ix.F32List(row.tolist(), row)
+    assert v == [0.5, -2.0, 3.25, 1.0] and isinstance(v, list) and json.loads(json.dumps(v)) == v
+    assert ix._as_vector_np(v, 4)[0] is not None and np.array_equal(ix._as_vector_np(v, 4)[0], row)
+    assert pickle.loads(pickle.dumps(v)) == v and type(pickle.loads(pickle.dumps(v))) is list
+    for mutate in (lambda x: x.__setitem__(0, 9.0), lambda x: x.append(1.0), lambda x: x.pop(),
+                   lambda x: x.reverse(), lambda x: x.sort(), lambda x: x.extend([1.0]), lambda x: x.insert(0, 7.0)):
+        w = ix.F32List(row.tolist(), row)
+        mutate(w)
+        assert w.f32 is None
+        if len(w) == 4:
+            assert np.array_equal(ix._as_vector_np(w, 4)[0], np.asarray(w, np.float32))
+    w = ix.F32List(row.tolist(), row)
+    w += [1.0]
+    assert w.f32 is None
