@@ -264,6 +264,7 @@ struct rc_index {
     int64_t capacity = 0;
     int64_t row_base = 0;    // a search returns row_base + local row * row_stride (shard → global rows)
     int64_t row_stride = 1;
+    int ncu = 256;           // compute units of the device (scan grid rounds)
     void *rows = nullptr;
     float *norms = nullptr;
     // int8 filter copy (RC_FILTER_I8): [cap_pad][ld] x8, sx / ex [cap_pad] at i8_slot(row)
@@ -425,6 +426,11 @@ void scan_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int 
     hipLaunchKernelGGL(normalize_queries_kernel, dim3(nq_pad), dim3(64), 0, s, queries, nq, h->dim, h->ld, h->qn);
     RC_LAUNCH_CHECK();
     int nblk = (int)std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (n_rows + 511) / 512));
+    // past one round of resident blocks (4 per CU), whole rounds: 1M rows were 1954 blocks = 1.9
+    // rounds, a tail of CUs with one block fewer; 1024 blocks of ~1000 rows are one round (and a
+    // merge over half the lists)
+    const int round_blocks = 4 * h->ncu;
+    if (nblk > round_blocks) nblk = nblk / round_blocks * round_blocks;
     int64_t rpb = (n_rows + nblk - 1) / nblk;
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb == 0) rpb = 32;
@@ -566,6 +572,7 @@ int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t ro
         h->capacity = capacity;
         h->row_base = row_base;
         try {
+            RC_HIP(hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, device));
             // whole 256-row tiles: the batched search reads row tiles without a bounds check
             const int64_t cap_pad = (capacity + INDEX_ROW_PAD - 1) / INDEX_ROW_PAD * INDEX_ROW_PAD;
             h->rows = dmalloc((size_t)cap_pad * h->ld * dtype_size(dtype));

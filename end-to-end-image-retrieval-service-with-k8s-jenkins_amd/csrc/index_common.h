@@ -334,8 +334,13 @@ __device__ __forceinline__ void scan_rows(const T *__restrict__ rows, int64_t ld
     scan_rows_q<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, q, q0, nq_total, k, partial);
 }
 
+// f32 rows of 512 (config 3): 131 VGPRs by default = 3 waves per SIMD; capped at 128 (no spill)
+// the CU holds 4 blocks and a 1M-row scan runs as one round of 4 blocks per CU
 template <typename T, int NCH, int QB, int CAP>
-__global__ __launch_bounds__(256) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
+constexpr int scan_min_waves() { return (sizeof(T) == 4 && NCH == 4 && QB == 1 && CAP <= 256) ? 4 : 1; }
+
+template <typename T, int NCH, int QB, int CAP>
+__global__ __launch_bounds__(256, (scan_min_waves<T, NCH, QB, CAP>())) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
                                                        int64_t rows_per_block, const float *__restrict__ qn, int q0,
                                                        int nq_total, int k, uint64_t *__restrict__ partial,
                                                        const int *__restrict__ flags) {

@@ -757,8 +757,8 @@ __host__ __device__ inline int band_planes_bytes(const Desc &d, int y_lo, int y_
     return total;
 }
 
-// MAXT > 0: every image's horizontal taps fit MAXT (the coefficient table's ksize <= MAXT:
-// Pillow bicubic down to a 1.5x downscale): a lane owns output columns and keeps their
+// MAXT > 0: every image's horizontal taps fit MAXT (the coefficient table's ksize <= MAXT: 5
+// for any bicubic upscale, 7 down to a 1.5x downscale): a lane owns output columns and keeps their
 // bounds and coefficients in registers across the band's rows (taps past a column's count
 // have coefficient 0, and their pixel index is clamped into the row: exact).  MAXT = 0: the
 // general form (coefficients read per output).  The vertical pass's bounds and coefficients
@@ -1259,8 +1259,13 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
             RC_HIP(hipMemcpyAsync(h->d_rdesc, h->h_rdesc, (size_t)n * sizeof(jpeg::RDesc), hipMemcpyHostToDevice, s));
             RC_HIP(hipEventRecord(h->staged, s));
             const dim3 gr((unsigned)maxbands, (unsigned)n);
-            if (max_hk <= 8)  // every horizontal pass within 8 taps: coefficients in registers
-                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<8>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+            // horizontal taps in registers: 5 (any bicubic upscale, e.g. the fixture's 168 -> 224), 7
+            // (down to 1.5x), else the general form
+            if (max_hk <= 5)
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<5>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+                                   h->d_desc, h->d_rdesc, out);
+            else if (max_hk <= 7)
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<7>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
                                    h->d_desc, h->d_rdesc, out);
             else
                 hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<0>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
