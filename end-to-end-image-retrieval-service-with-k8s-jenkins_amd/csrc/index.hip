@@ -422,9 +422,7 @@ void scan_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int 
     int qb = 1;
     while (qb * 2 <= std::min(nq, scan_max_qb(h->nch, k))) qb *= 2;
     const int nq_pad = (nq + qb - 1) / qb * qb;  // every scan pass runs qb real-or-zero query slots
-    ensure_workspace(h, nq_pad, k);
-    hipLaunchKernelGGL(normalize_queries_kernel, dim3(nq_pad), dim3(64), 0, s, queries, nq, h->dim, h->ld, h->qn);
-    RC_LAUNCH_CHECK();
+    ensure_workspace(h, nq_pad, k);  // (the scan normalises the queries itself: no separate launch)
     int nblk = (int)std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (n_rows + 511) / 512));
     // past one round of resident blocks (4 per CU), whole rounds: 1M rows were 1954 blocks = 1.9
     // rounds, a tail of CUs with one block fewer; 1024 blocks of ~1000 rows are one round (and a
@@ -440,6 +438,9 @@ void scan_search(rc_index *h, const float *queries, int nq, int64_t n_rows, int 
     for (int q0 = 0; q0 < nq_pad; q0 += qb) {
         const int slot = h->timer.begin(s);
         ScanArgs a{h->rows, h->ld, h->nch, n_rows, rpb, nblk, h->qn, q0, qb, nq_pad, k, h->partial, s};
+        a.qraw = queries;
+        a.dim = h->dim;
+        a.nq_real = nq;
         launch_scan(h, a);
         h->timer.end(slot, s, bytes);
     }

@@ -82,6 +82,11 @@ struct ScanArgs {
     // (qb = 1; q0 unused); partial is then [nblk][nq_total][k].
     const int *flags = nullptr;
     int grid_y = 1;
+    // Single-query scans (scan_search): the raw queries [nq_real][dim]; every wave normalises its
+    // query itself, with normalize_queries_kernel's exact arithmetic (no separate launch), and
+    // qn is not read.  nullptr: qn holds the normalised queries.
+    const float *qraw = nullptr;
+    int dim = 0, nq_real = 0;
 };
 
 // largest queries-per-pass for a row width: query registers per lane = QB*nch*8 floats <= 64
@@ -320,17 +325,37 @@ __device__ __forceinline__ void scan_rows_q(const T *__restrict__ rows, int64_t 
 template <typename T, int NCH, int QB, int CAP>
 __device__ __forceinline__ void scan_rows(const T *__restrict__ rows, int64_t ld, int64_t n_rows, int64_t rows_per_block,
                                           const float *__restrict__ qn, int q0, int nq_total, int k,
-                                          uint64_t *__restrict__ partial) {
+                                          uint64_t *__restrict__ partial, const float *__restrict__ qraw = nullptr,
+                                          int dim = 0, int nq_real = 0) {
     constexpr int EPC = ScanShape<T, NCH>::EPC;
     constexpr int CPL = ScanShape<T, NCH>::CPL;
-    const int sub = threadIdx.x & 15;
+    const int lane = threadIdx.x & 63, sub = lane & 15;
     float q[QB][CPL][EPC];
+    if (qraw != nullptr) {  // block-uniform: normalise in the wave, as normalize_queries_kernel does
 #pragma unroll
-    for (int b = 0; b < QB; ++b)
+        for (int b = 0; b < QB; ++b) {
+            const bool valid = q0 + b < nq_real;
+            const float *src = qraw + (int64_t)(valid ? q0 + b : 0) * dim;
+            float ss = 0.f;
+            for (int c = lane; c < dim; c += 64) ss = valid ? fmaf(src[c], src[c], ss) : 0.f;
+            ss = wave_sum(ss);
+            const float inv = ss > 0.f ? 1.0f / sqrtf(ss) : 0.f;
 #pragma unroll
-        for (int i = 0; i < CPL; ++i)
+            for (int i = 0; i < CPL; ++i)
 #pragma unroll
-            for (int e = 0; e < EPC; ++e) q[b][i][e] = qn[(int64_t)(q0 + b) * ld + (sub + 16 * i) * EPC + e];
+                for (int e = 0; e < EPC; ++e) {
+                    const int c = (sub + 16 * i) * EPC + e;
+                    q[b][i][e] = (valid && c < dim) ? src[c] * inv : 0.f;
+                }
+        }
+    } else {
+#pragma unroll
+        for (int b = 0; b < QB; ++b)
+#pragma unroll
+            for (int i = 0; i < CPL; ++i)
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) q[b][i][e] = qn[(int64_t)(q0 + b) * ld + (sub + 16 * i) * EPC + e];
+    }
     scan_rows_q<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, q, q0, nq_total, k, partial);
 }
 
@@ -343,7 +368,8 @@ template <typename T, int NCH, int QB, int CAP>
 __global__ __launch_bounds__(256, (scan_min_waves<T, NCH, QB, CAP>())) void scan_topk_kernel(const T *__restrict__ rows, int64_t ld, int64_t n_rows,
                                                        int64_t rows_per_block, const float *__restrict__ qn, int q0,
                                                        int nq_total, int k, uint64_t *__restrict__ partial,
-                                                       const int *__restrict__ flags) {
+                                                       const int *__restrict__ flags, const float *__restrict__ qraw,
+                                                       int dim, int nq_real) {
     if (flags != nullptr) {  // exact fallback: the overflowed queries only (block-uniform branches)
         for (int qf = blockIdx.y; qf < nq_total; qf += gridDim.y)
             if (flags[qf]) {
@@ -352,13 +378,14 @@ __global__ __launch_bounds__(256, (scan_min_waves<T, NCH, QB, CAP>())) void scan
             }
         return;
     }
-    scan_rows<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, qn, q0, nq_total, k, partial);
+    scan_rows<T, NCH, QB, CAP>(rows, ld, n_rows, rows_per_block, qn, q0, nq_total, k, partial, qraw, dim, nq_real);
 }
 
 template <typename T, int NCH, int QB, int CAP>
 void launch_scan_t(const ScanArgs &a) {
     hipLaunchKernelGGL((scan_topk_kernel<T, NCH, QB, CAP>), dim3(a.nblk, a.grid_y), dim3(256), 0, a.stream, (const T *)a.rows,
-                       a.ld, a.n_rows, a.rows_per_block, a.qn, a.q0, a.nq_total, a.k, a.partial, a.flags);
+                       a.ld, a.n_rows, a.rows_per_block, a.qn, a.q0, a.nq_total, a.k, a.partial, a.flags, a.qraw, a.dim,
+                       a.nq_real);
     RC_LAUNCH_CHECK();
 }
 
