@@ -928,6 +928,53 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     w2_epilogue<EPI>(a, acc, smem, m0, n0);
 }
 
+// The skinny kernels' K chain: nk steps of 32, acc[ni] += W[ni]·A in k order (one dependent
+// 16x16x32 MFMA per step, the order of every tiled kernel: the same bits), with the operands of
+// the next D steps in flight in a register ring, so the chain waits for one step's loads while
+// D − 1 more are on their way (a lone image's GEMMs are latency-bound: 197 rows give 300-1250
+// waves for 1024 SIMDs).  NK > 0: the step count is a constant and the chain is straight-line
+// code — in a loop the wait-count pass falls back to vmcnt(0) at the loop head, one full memory
+// latency per trip.  NK = 0: any even nk, a 2-deep ring in a loop.
+template <int NI, int NK, int D>
+__device__ __forceinline__ void skinny_chain_t(const uint16_t *Ar, const uint16_t *Wr, int K, int nk, f32x4 (&acc)[NI]) {
+    bf16x8 ra[D], rw[D][NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        ra[d] = *reinterpret_cast<const bf16x8 *>(Ar + 32 * d);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) rw[d][ni] = *reinterpret_cast<const bf16x8 *>(Wr + (int64_t)ni * 16 * K + 32 * d);
+    }
+    auto step = [&](int st, bf16x8 &a_, bf16x8 (&w_)[NI], bool more) __attribute__((always_inline)) {
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_[ni], a_, acc[ni], 0, 0, 0);
+        if (more) {
+            const int kn = 32 * (st + D);
+            a_ = *reinterpret_cast<const bf16x8 *>(Ar + kn);
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) w_[ni] = *reinterpret_cast<const bf16x8 *>(Wr + (int64_t)ni * 16 * K + kn);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the ring: no load hoisted or sunk across steps
+    };
+    if constexpr (NK > 0) {
+        static_assert(NK % D == 0, "ring depth divides the step count");
+#pragma unroll
+        for (int st = 0; st < NK; ++st) step(st, ra[st % D], rw[st % D], st + D < NK);
+    } else {
+        for (int kb = 0; kb < nk; kb += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) step(kb + d, ra[d], rw[d], kb + d + D < nk);
+        }
+    }
+}
+// K (per chain) 768 / 3072: straight-line chains; otherwise the looped form (K % 64 == 0)
+template <int NI, int KT>
+__device__ __forceinline__ void skinny_chain(const uint16_t *Ar, const uint16_t *Wr, int K, int nk, f32x4 (&acc)[NI]) {
+    if constexpr (KT > 0) skinny_chain_t<NI, KT / 32, 12>(Ar, Wr, K, nk, acc);
+    else skinny_chain_t<NI, 0, 2>(Ar, Wr, K, nk, acc);
+}
+
 // Skinny GEMM for M <= 256 (the last layer's CLS rows: O-proj, fc1, fc2 with
 // M = images in the slice).  A 256-row tile kernel would put the whole launch on
 // N/256 CUs with the full K loop on each (fc2: 3 CUs x 3072-deep); here every
@@ -936,28 +983,28 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
 // launch spreads over ceil(M/16)·N/(16·NI) waves.  Swapped operands as in the
 // tiled kernels: the A-operand is 16 weight rows, so lane (g, li) ends with
 // activation row li, output columns 4g..4g+3 of each 16-column group.
-template <int EPI, int NI>
+// Block b runs on XCD b % 8; skinny_block(b) numbers the blocks so that each XCD gets one
+// contiguous range (bijective), and tiles are numbered column-major — so the waves of a block
+// (consecutive row tiles of one column tile) read the same weight rows at about the same time
+// (L1 hits), and a column tile's weights are fetched into one XCD's L2 only (W is re-read by
+// every row tile: 13x for a lone image's 197 rows).
+__device__ __forceinline__ int skinny_block(int b, int nwg) {
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+}
+
+template <int EPI, int NI, int KT>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
     const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int w = skinny_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     if (w >= nct * nrt) return;
-    const int ct = w % nct, rt = w / nct;
+    const int ct = w / nrt, rt = w % nrt;
     const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
-    const uint16_t *Ar = a.A + (int64_t)row * K + 8 * g;
+    const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
     const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
     f32x4 acc[NI];
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int k0 = 0; k0 < K; k0 += 32) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8 *>(Ar + k0);
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-            const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(Wr + (int64_t)ni * 16 * K + k0);
-            acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af, acc[ni], 0, 0, 0);
-        }
-    }
+    skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
     if (row >= a.M) return;
     float2 lrs;  // LayerNorm fold: this row's (rstd, -rstd*mu), as gemm_pp_kernel computes it
     if constexpr (epi_ln(EPI)) lrs = ln_row_scale(a.ln_stats + (int64_t)row * LN_STRIDE, a.ln_eps);
@@ -975,7 +1022,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
         } else {
             v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
         }
-        if constexpr (EPI == EPI_RESID_HL) {  // residual stream as bf16 pairs (ln_emit_kernel adds the statistics)
+        if constexpr (EPI == EPI_RESID_HL) {  // residual stream as bf16 pairs (LN producers: gemm_skinny_ln_kernel)
             const int64_t off = (int64_t)row * a.N + c;
             const float4 r = hl_value(hl_load(a.ln_x + off, a.res_lo + off));
             hl_store(hl_split(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w)), a.ln_x + off, a.res_lo + off);
@@ -997,6 +1044,70 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
     }
 }
 
+// The skinny GEMM as a LayerNorm-fold producer (residual epilogues with ln_x + ln_stats, N = 768:
+// O-proj / fc2 of a batch of one image, the CLS O-proj): the block-partial statistics are
+// computed in the epilogue (the canonical slices and reduction tree of every producer, bit for bit;
+// round 4 ran them as a second launch, 5 us each at batch 1).
+// A block of 4 waves owns 2 row tiles × one 64-column LayerNorm block (blocks numbered column-
+// block-major through skinny_block: a column block's weights stay in one XCD): wave w computes rows
+// 16·(2·rtp + (w >> 1)) + li, columns 64·blk + 32·(w & 1) + 16·ni + 4g + e (the skinny kernel's
+// tile and K chain), stores as gemm_skinny_kernel does and puts the value each element now stands
+// for (the stored f32, or hl_value of the stored pair) into LDS; then waves 0-1 read the 32 rows'
+// canonical slices (4 lanes per row) and reduce them with ln_block_reduce_quad.
+template <int EPI, int KT>
+__global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(GemmArgs a) {
+    static_assert(epi_resid(EPI), "LayerNorm producers are residual epilogues");
+    constexpr int NI = 2, LP = 68;  // LDS row pitch (floats)
+    __shared__ float xs_l[32 * LP];
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15, wave = threadIdx.x >> 6;
+    const int nrtp = (a.M + 31) / 32, lb = skinny_block(blockIdx.x, gridDim.x);
+    const int blk = lb / nrtp, rtp = lb % nrtp;  // column-block-major (skinny_block)
+    const int rl = (wave >> 1) * 16 + li;  // row within the block's 32
+    const int K = a.K, n0 = blk * 64 + (wave & 1) * 32, row = rtp * 32 + rl;
+    const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;
+    const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
+    f32x4 acc[NI];
+    skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
+    const bool valid = row < a.M;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+        const int c = n0 + ni * 16 + 4 * g;
+        const float4 b = *reinterpret_cast<const float4 *>(a.bias + c);
+        const float v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
+        const int64_t off = (int64_t)min(row, a.M - 1) * a.N + c;
+        float4 x;
+        if constexpr (EPI == EPI_RESID_HL) {
+            const float4 r = hl_value(hl_load(a.ln_x + off, a.res_lo + off));
+            const uint4 p = hl_split(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w));
+            if (valid) hl_store(p, a.ln_x + off, a.res_lo + off);
+            x = hl_value(p);
+        } else {
+            float4 *o = reinterpret_cast<float4 *>(a.out_f32 + off);
+            const float4 r = *o;
+            x = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
+            if (valid) {
+                *o = x;
+                *reinterpret_cast<uint2 *>(a.ln_x + off) = pack_bf16x4(x);
+            }
+        }
+        *reinterpret_cast<float4 *>(xs_l + rl * LP + (wave & 1) * 32 + ni * 16 + 4 * g) = x;
+    }
+    __syncthreads();
+    if (wave >= 2) return;
+    const int item = wave * 64 + lane, r = item >> 2, sg = item & 3;
+    float xs[16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float *q = xs_l + r * LP + ln_slice_col(sg, c);
+        const float4 u = *reinterpret_cast<const float4 *>(q), v = *reinterpret_cast<const float4 *>(q + 4);
+        xs[8 * c] = u.x, xs[8 * c + 1] = u.y, xs[8 * c + 2] = u.z, xs[8 * c + 3] = u.w;
+        xs[8 * c + 4] = v.x, xs[8 * c + 5] = v.y, xs[8 * c + 6] = v.z, xs[8 * c + 7] = v.w;
+    }
+    const float2 st = ln_block_reduce_quad(ln_slice_stats(xs), sg);
+    const int srow = rtp * 32 + r;
+    if (sg == 0 && srow < a.M) *reinterpret_cast<float2 *>(a.ln_stats + (int64_t)srow * LN_STRIDE + 2 * blk) = st;
+}
+
 // Split-K skinny GEMM with an f32 residual epilogue, for the last layer's fc2 on the
 // CLS rows (M = images, N = 768, K = 3072; every batch size, so the CLS rows of an image
 // get the same bits in any batch): the skinny kernel's one wave per 16
@@ -1005,7 +1116,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
 // skinny_reduce_kernel adds them in ks order + bias + the residual (deterministic).
 // Used only on the CLS rows, so batch invariance is unaffected (the full-layer GEMMs of
 // a small batch keep the skinny kernel, bit-identical to the tiled ones).
-template <int NI, int KS>
+template <int NI, int KS, int KT>
 __global__ __launch_bounds__(256) void gemm_skinny_splitk_kernel(GemmArgs a, float *__restrict__ part) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
     const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
@@ -1015,20 +1126,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_splitk_kernel(GemmArgs a, flo
     const int ct = tile % nct, rt = tile / nct;
     const int KL = a.K / KS, k0 = ks * KL;
     const int n0 = ct * 16 * NI, row = rt * 16 + li;
-    const uint16_t *Ar = a.A + (int64_t)row * a.K + k0 + 8 * g;
+    const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * a.K + k0 + 8 * g;
     const uint16_t *Wr = a.W + (int64_t)(n0 + li) * a.K + k0 + 8 * g;
     f32x4 acc[NI];
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int k = 0; k < KL; k += 32) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8 *>(Ar + k);
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-            const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(Wr + (int64_t)ni * 16 * a.K + k);
-            acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af, acc[ni], 0, 0, 0);
-        }
-    }
+    skinny_chain<NI, KT>(Ar, Wr, a.K, KL / 32, acc);
     if (row >= a.M) return;
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni)
@@ -1060,43 +1161,14 @@ inline void launch_skinny_splitk_resid(const GemmArgs &a, float *part, hipStream
     RC_REQUIRE(a.M >= 1 && a.N % 32 == 0 && a.K % (32 * SKINNY_KS) == 0 && a.out_f32 && !a.ln_x, RC_ERR_UNSUPPORTED,
                "split-K skinny GEMM: N % 32 == 0, K % 128 == 0, f32 residual");
     const int waves = ((a.M + 15) / 16) * (a.N / 32) * SKINNY_KS;
-    hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS>), dim3((waves + 3) / 4), dim3(256), 0, s, a, part);
+    if (a.K == 768 * SKINNY_KS)
+        hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS, 768>), dim3((waves + 3) / 4), dim3(256), 0, s, a, part);
+    else
+        hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS, 0>), dim3((waves + 3) / 4), dim3(256), 0, s, a, part);
     RC_LAUNCH_CHECK();
     const int64_t n4 = (int64_t)a.M * a.N / 4;
     hipLaunchKernelGGL(skinny_reduce_kernel<SKINNY_KS>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, a, part);
     RC_LAUNCH_CHECK();
-}
-
-// LayerNorm-fold producer pass for rows a skinny GEMM wrote (M <= 256): four lanes per
-// (row, 64-column block), one canonical slice each (vit_kernels.h, LN_PARTS) and the same
-// reduction tree as the tiled epilogues, so the partials are bit-identical for any M.
-// lo != null: the rows are the bf16 pairs (ln_x, lo), only the partials are written;
-// otherwise x is the f32 stream and ln_x receives its bf16 copy.
-__global__ __launch_bounds__(256) void ln_emit_kernel(const float *__restrict__ x, uint16_t *__restrict__ ln_x,
-                                                     const uint8_t *__restrict__ lo, float *__restrict__ ln_stats, int M) {
-    constexpr int H = 64 * LN_PARTS;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    const int item = t >> 2, g = t & 3;
-    const bool ok = item < M * LN_PARTS;  // every lane joins the shuffles; only valid items store
-    const int it = ok ? item : 0;
-    const int row = it / LN_PARTS, blk = it - row * LN_PARTS;
-    float xs[16];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int64_t off = (int64_t)row * H + blk * 64 + ln_slice_col(g, c);
-        float v[8];
-        if (lo != nullptr) {
-            hl8_value(*reinterpret_cast<const uint4 *>(ln_x + off), *reinterpret_cast<const uint2 *>(lo + off), v);
-        } else {
-            const float4 a = *reinterpret_cast<const float4 *>(x + off), b = *reinterpret_cast<const float4 *>(x + off + 4);
-            v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
-            if (ok) *reinterpret_cast<uint4 *>(ln_x + off) = bf16x8_pack(v);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) xs[8 * c + k] = v[k];
-    }
-    const float2 st = ln_block_reduce_quad(ln_slice_stats(xs), g);
-    if (ok && g == 0) *reinterpret_cast<float2 *>(ln_stats + (int64_t)row * LN_STRIDE + 2 * blk) = st;
 }
 
 // Kernel choice: 4 = ping-pong 256x256, 10 = ping-pong on image-aligned 224-row tiles,
@@ -1185,14 +1257,20 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
         case GEMM_SKINNY: {
             RC_REQUIRE(!epi_patch(EPI) && a.N % 32 == 0 && a.M >= 1, RC_ERR_UNSUPPORTED,
                        "skinny GEMM: bf16 / GELU / residual epilogues, N a multiple of 32");
-            const int waves = ((a.M + 15) / 16) * (a.N / 32);
-            hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
-            if (a.ln_x != nullptr && a.ln_stats != nullptr) {  // LayerNorm-fold producer: the partials in a second pass
-                RC_LAUNCH_CHECK();
-                RC_REQUIRE(a.N == 64 * LN_PARTS, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
-                hipLaunchKernelGGL(ln_emit_kernel, dim3((a.M * LN_PARTS + 63) / 64), dim3(256), 0, s, a.out_f32, a.ln_x,
-                                   a.res_lo, a.ln_stats, a.M);
+            if constexpr (epi_resid(EPI)) {
+                if (a.ln_x != nullptr && a.ln_stats != nullptr) {  // LayerNorm-fold producer: partials in the epilogue
+                    RC_REQUIRE(a.N == 64 * LN_PARTS, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
+                    const dim3 gr(((a.M + 31) / 32) * LN_PARTS);
+                    if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 768>), gr, dim3(256), 0, s, a);
+                    else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 3072>), gr, dim3(256), 0, s, a);
+                    else hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 0>), gr, dim3(256), 0, s, a);
+                    break;
+                }
             }
+            const dim3 gr((((a.M + 15) / 16) * (a.N / 32) + 3) / 4);
+            if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768>), gr, dim3(256), 0, s, a);
+            else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072>), gr, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 0>), gr, dim3(256), 0, s, a);
             break;
         }
         case GEMM_PINGPONG: {

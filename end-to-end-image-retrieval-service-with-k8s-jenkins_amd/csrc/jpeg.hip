@@ -710,37 +710,30 @@ __global__ __launch_bounds__(256) void jpeg_resize_v_kernel(const RDesc *__restr
 
 
 // Band-fused decode → resize (rc_jpeg_decode_resized when every image's band fits in LDS):
-// grid (max bands, n), 256 lanes; block (b, i) produces output rows [b·bh, b·bh + bh) of image
-// i whole.  It reads once the source rows their vertical taps span ([lo, hi), Pillow's
+// grid (max bands, n), 256 lanes = 4 waves; block (b, i) produces output rows [b·bh, b·bh + bh)
+// of image i whole.  It reads once the source rows their vertical taps span ([lo, hi), Pillow's
 // ImagingResampleInner order: the horizontal pass covers exactly the rows the vertical one
-// reads), colour-converts them into LDS (src, [rows][W][3]), runs the horizontal pass into
-// LDS (tmp, [rows][S][3], u8 as Pillow's intermediate image), then the vertical pass into an
-// LDS copy of the band, stored with 16-B writes.  No intermediate image in HBM and no
-// per-row blocks: each block streams its band's plane rows with every lane busy.  The
-// arithmetic is jpeg_color_resize_h_kernel's + jpeg_resize_v_kernel's, so the bytes equal
-// that path's (and PIL decode + Image.resize).
-// dynamic LDS = the largest per-image need (band_lds_bytes, host).
-// LDS layout of one band: src [rows][W][3] (need_h only), tmp [rows][S][3], the band's output
-// [nout][S][3] (need_v only: over src when it fits there, else after tmp); returns the bytes.
-// (pl: the band's copy of the planes' block rows, first; every other offset is past it)
+// reads).  The arithmetic is jpeg_color_resize_h_kernel's + jpeg_resize_v_kernel's, so the
+// bytes equal that path's (and PIL decode + Image.resize).
+//   0. the planes' 8-row block rows the band reads, copied into LDS with 16-B loads;
+//   1. per wave, one source row at a time (no block barrier): the row's colour pixels as RGBX
+//      words into the wave's row buffer, then Pillow's horizontal pass from it (one 4-byte LDS
+//      read per tap for all three channels) into tmp [rows][TP] (RGB bytes, TP = 3S rounded to 4);
+//   2. the vertical pass, which does not care about channels: a lane owns one 4-byte column of
+//      tmp, reads one word per tap, keeps 4 sums, and stores the 4 output bytes straight to HBM
+//      as one word (a wave writes 256 contiguous bytes of an output row; the band's rows and
+//      their taps are wave-uniform).
+// dynamic LDS = the largest per-image need (band_layout, host and device alike).
 struct BandLayout {
-    int tmp, band, total;
+    int rowbuf, tmp, total, tp;
 };
-__host__ __device__ inline BandLayout band_layout(int rows, int nout, int W, int S, int need_h, int need_v, int pl) {
+__host__ __device__ inline BandLayout band_layout(int rows, int W, int S, int need_h, int pl) {
     auto al = [](int b) { return (b + 15) & ~15; };
     BandLayout L;
-    const int src = need_h ? al(rows * W * 3) : 0;
-    L.tmp = pl + src;
-    L.total = L.tmp + al(rows * S * 3);
-    L.band = L.tmp;  // no vertical pass: tmp is the band
-    if (need_v) {
-        if (nout * S * 3 <= src) {
-            L.band = pl;
-        } else {
-            L.band = L.total;
-            L.total += al(nout * S * 3);
-        }
-    }
+    L.tp = (3 * S + 3) & ~3;
+    L.rowbuf = pl;
+    L.tmp = pl + (need_h ? al(4 * ((W + 1) & ~1) * 4) : 0);  // 4 waves × W RGBX words (even, 8-B rows)
+    L.total = L.tmp + al(rows * L.tp);
     return L;
 }
 
@@ -757,14 +750,21 @@ __host__ __device__ inline int band_planes_bytes(const Desc &d, int y_lo, int y_
     return total;
 }
 
-// MAXT > 0: every image's horizontal taps fit MAXT (the coefficient table's ksize <= MAXT: 5
-// for any bicubic upscale, 7 down to a 1.5x downscale): a lane owns output columns and keeps their
-// bounds and coefficients in registers across the band's rows (taps past a column's count
-// have coefficient 0, and their pixel index is clamped into the row: exact).  MAXT = 0: the
-// general form (coefficients read per output).  The vertical pass's bounds and coefficients
-// depend on the output row only: wave-uniform (scalar loads) in both forms.
+constexpr int BAND_NXO = 4;  // output columns per lane held in registers (S <= 256)
+
+#if defined(RC_GEMM_ABLATION)
+// diagnostic builds: phases of jpeg_band_resize_kernel to skip (1 colour, 2 horizontal, 4 vertical
+// math; the stores stay), for a per-phase time split (tools/jpeg_phase.py); wrong pixels
+__device__ int g_band_skip = 0;
+#endif
+
+// MAXT > 0 (S <= 64·BAND_NXO): every image's horizontal taps fit MAXT (the coefficient table's
+// ksize <= MAXT: 5 for any bicubic upscale, 7 down to a 1.5x downscale): a lane owns output
+// columns lane + 64t and keeps their tap offsets and coefficients in registers across the rows
+// its wave filters (taps past a column's count have coefficient 0, and their pixel index is
+// clamped into the row: exact).  MAXT = 0: the general form (coefficients read per output).
 template <int MAXT>
-__global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
+__global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
                                                               const Desc *__restrict__ descs,
                                                               const RDesc *__restrict__ rdescs, uint8_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -773,15 +773,14 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
     const int S = r.S, yo0 = (int)blockIdx.x * r.bh;
     if (yo0 >= S) return;  // block-uniform: this image has fewer bands
     const int yo1 = min(S, yo0 + r.bh), nout = yo1 - yo0;
+    // wave-uniform in an SGPR: the row-dependent upsampler offsets below then stay scalar
+    const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     // source rows of the band (relative to r.y0; Pillow's bounds are monotone in the output row)
     const int lo = r.need_v ? r.vb[2 * yo0] : yo0;
     const int hi = r.need_v ? r.vb[2 * (yo1 - 1)] + r.vb[2 * (yo1 - 1) + 1] : yo1;
     const int rows = hi - lo, W = d.W;
-    // 0. the planes' 8-row block rows the band's colour conversion reads, copied contiguous
-    //    (block layout kept) into LDS with 16-B loads: the upsampler's 1-9 byte reads per pixel
-    //    then hit LDS instead of scattered byte loads from HBM / L2
-    //    (components unrolled with constant indices: a runtime-indexed Desc / offset array would
-    //    live in scratch memory, one scratch load per sample read)
+    // 0. planes (components unrolled with constant indices: a runtime-indexed Desc / offset array
+    //    would live in scratch memory, one scratch load per sample read)
     int poff[3], pbr0[3], pnbr[3];
     int pl = 0;
 #pragma unroll
@@ -799,132 +798,245 @@ __global__ __launch_bounds__(256) void jpeg_band_resize_kernel(const uint8_t *__
             const uint4 *g = reinterpret_cast<const uint4 *>(planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64);
             uint4 *l = reinterpret_cast<uint4 *>(lds + poff[c]);
             const int n16 = pnbr[c] * d.bw[c] * 4;
+#pragma unroll 2
             for (int i = threadIdx.x; i < n16; i += 256) l[i] = g[i];
         }
     }
-    const BandLayout L = band_layout(rows, nout, W, S, r.need_h, r.need_v, pl);
-    uint8_t *src = lds + pl, *tmp = lds + L.tmp, *band = lds + L.band;
-    __syncthreads();
-    auto at = [&](int c, int x, int y) {
-        return (int)lds[poff[c] + (((y >> 3) - pbr0[c]) * d.bw[c] + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7)];
-    };
-    // 1. colour: the band's source rows (straight into tmp when the width already is S); pixel
-    //    idx = rr·W + x walked by (rr, x) increments (no division per pixel)
-    {
-        uint8_t *dst = r.need_h ? src : tmp;
-        const int n = rows * W;
-        int rr = threadIdx.x / W, x = threadIdx.x - rr * W;
-        const int drr = 256 / W, dx = 256 - drr * W;
-        for (int idx = threadIdx.x; idx < n; idx += 256) {
-            const int y = r.y0 + lo + rr;
-            const int Y = upsampled_t(d, 0, x, y, at);
-            int R = Y, G = Y, B = Y;
-            if (d.ncomp != 1) {  // jdcolor.c ycc_rgb_convert, as ycc_rgb
-                const int cb = upsampled_t(d, 1, x, y, at) - 128, cr = upsampled_t(d, 2, x, y, at) - 128;
-                R = min(max(Y + ((91881 * cr + 32768) >> 16), 0), 255);
-                G = min(max(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16), 0), 255);
-                B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
-            }
-            uint8_t *o = dst + 3 * idx;
-            o[0] = (uint8_t)R;
-            o[1] = (uint8_t)G;
-            o[2] = (uint8_t)B;
-            rr += drr;
-            x += dx;
-            if (x >= W) {
-                x -= W;
-                ++rr;
+    const BandLayout L = band_layout(rows, W, S, r.need_h, pl);
+    const int TP = L.tp;
+    uint32_t *rowbuf = reinterpret_cast<uint32_t *>(lds + L.rowbuf) + wave * ((W + 1) & ~1);
+    uint8_t *tmp = lds + L.tmp;
+    // horizontal taps of this lane's output columns (MAXT > 0), kept across its wave's rows
+    int cf[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1], px[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1];
+    if constexpr (MAXT > 0) {
+        if (r.need_h) {
+#pragma unroll
+            for (int t = 0; t < BAND_NXO; ++t) {
+                const int xo = min(lane + 64 * t, S - 1);
+                const int xmin = r.hb[2 * xo];
+#pragma unroll
+                for (int k = 0; k < MAXT; ++k) {
+                    cf[t][k] = k < r.hk ? r.hc[xo * r.hk + k] : 0;
+                    px[t][k] = min(xmin + k, W - 1);
+                }
             }
         }
     }
     __syncthreads();
-    // 2. horizontal pass (Pillow's fixed point: 22 fractional bits, rounding 1 << 21, clip)
-    if (r.need_h) {
-        if constexpr (MAXT > 0) {
-            for (int xo = threadIdx.x; xo < S; xo += 256) {
-                const int xmin = r.hb[2 * xo];
-                int cf[MAXT], px[MAXT];
+    // jdsample.c's upsampler for one source row y as wave-uniform row offsets into the LDS planes
+    // (near / far sample row) and a kind: 0 the sample itself (1x1, or box h2 when the plane is
+    // <= 2 samples wide), 1 h1v2, 2 h2v1, 3 h2v2 fancy.  The fancy forms read the neighbour
+    // column clamped into the plane, which gives upsampled_t's edge values exactly.
+    struct RowTap {
+        int bn, bf, kind, rnd, sx, dw1;
+    };
+    auto row_tap = [&](int c, int y) {
+        RowTap t;
+        const int rx = d.rx[c], ry = d.ry[c];
+        int j = y, far = y;
+        t.rnd = 0;
+        if (ry == 2) {
+            j = y >> 1;
+            const int vv = y & 1;
+            far = vv == 0 ? max(j - 1, 0) : min(j + 1, d.dh[c] - 1);
+            t.rnd = vv == 0 ? 1 : 2;
+        }
+        auto rowoff = [&](int jj) { return poff[c] + ((jj >> 3) - pbr0[c]) * d.bw[c] * 64 + (jj & 7) * 8; };
+        t.bn = rowoff(j);
+        t.bf = rowoff(far);
+        t.sx = rx == 2 ? 1 : 0;
+        t.dw1 = d.dw[c] - 1;
+        if (rx == 1) t.kind = ry == 2 ? 1 : 0;
+        else if (d.dw[c] <= 2) t.kind = 0;
+        else t.kind = ry == 2 ? 3 : 2;
+        return t;
+    };
+    auto col = [](int i) { return ((i >> 3) << 6) + (i & 7); };
+    // the component's samples at the pixel pair (2p, 2p + 1): a fancy h2 pair shares its centre
+    // column and reads one neighbour each side (3 column reads instead of 4, colsums once)
+    auto sample2 = [&](const RowTap &t, int p, int &v0, int &v1) {
+        if (t.kind == 0) {
+            if (t.sx) {
+                v0 = v1 = (int)lds[t.bn + col(p)];
+            } else {  // x = 2p is even: 2p and 2p + 1 are neighbours within one 8-sample block row
+                const int c0 = col(2 * p);
+                v0 = (int)lds[t.bn + c0];
+                v1 = (int)lds[t.bn + c0 + 1];
+            }
+            return;
+        }
+        if (t.kind == 1) {
+            const int c0 = col(2 * p);
+            v0 = (3 * (int)lds[t.bn + c0] + (int)lds[t.bf + c0] + t.rnd) >> 2;
+            v1 = (3 * (int)lds[t.bn + c0 + 1] + (int)lds[t.bf + c0 + 1] + t.rnd) >> 2;
+            return;
+        }
+        const int c0 = col(p), cl = col(max(p - 1, 0)), cr = col(min(p + 1, t.dw1));
+        if (t.kind == 2) {
+            const int s0 = 3 * (int)lds[t.bn + c0];
+            v0 = (s0 + (int)lds[t.bn + cl] + 1) >> 2;
+            v1 = (s0 + (int)lds[t.bn + cr] + 2) >> 2;
+            return;
+        }
+        const int cs0 = 3 * (3 * (int)lds[t.bn + c0] + (int)lds[t.bf + c0]);
+        const int csl = 3 * (int)lds[t.bn + cl] + (int)lds[t.bf + cl];
+        const int csr = 3 * (int)lds[t.bn + cr] + (int)lds[t.bf + cr];
+        v0 = (cs0 + csl + 8) >> 4;
+        v1 = (cs0 + csr + 7) >> 4;
+    };
+    // jdcolor.c ycc_rgb_convert, as ycc_rgb: RGB of one pixel as the word R | G << 8 | B << 16
+    auto rgbw = [&](int Y, int cb, int cr) {
+        if (d.ncomp == 1) return (uint32_t)Y * 0x010101u;
+        cb -= 128;
+        cr -= 128;
+        const int R = min(max(Y + ((91881 * cr + 32768) >> 16), 0), 255);
+        const int G = min(max(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16), 0), 255);
+        const int B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
+        return (uint32_t)R | ((uint32_t)G << 8) | ((uint32_t)B << 16);
+    };
+    auto pair_rgb = [&](const RowTap *tp, int p, uint32_t &w0, uint32_t &w1) {
+        int y0, y1, b0 = 0, b1 = 0, r0 = 0, r1 = 0;
+        sample2(tp[0], p, y0, y1);
+        if (d.ncomp != 1) {
+            sample2(tp[1], p, b0, b1);
+            sample2(tp[2], p, r0, r1);
+        }
+        w0 = rgbw(y0, b0, r0);
+        w1 = rgbw(y1, b1, r1);
+    };
+    // 1. colour + horizontal pass, one source row per wave at a time
+    for (int rr = wave; rr < rows; rr += 4) {
+        const int y = r.y0 + lo + rr;
+        RowTap tp[3];
 #pragma unroll
-                for (int k = 0; k < MAXT; ++k) {
-                    cf[k] = k < r.hk ? r.hc[xo * r.hk + k] : 0;
-                    px[k] = 3 * min(xmin + k, W - 1);
-                }
-                for (int rr = 0; rr < rows; ++rr) {
-                    const uint8_t *p = src + rr * W * 3;
+        for (int c = 0; c < 3; ++c)
+            if (c < d.ncomp) tp[c] = row_tap(c, y);
+        uint8_t *trow = tmp + rr * TP;
+        // pixel pairs (2p, 2p + 1); an odd width's last pair computes a pixel past the row (its
+        // samples clamped in the plane copy's padding) and does not store it
+        const int npair = (W + 1) >> 1;
+        if (!r.need_h) {  // the width already is S: the colour row is the pass's output
+            for (int p = lane; p < npair; p += 64) {
+                uint32_t w[2];
+                pair_rgb(tp, p, w[0], w[1]);
+                for (int e = 0; e < 2 && 2 * p + e < W; ++e)
+                    for (int b = 0; b < 3; ++b) trow[3 * (2 * p + e) + b] = (uint8_t)(w[e] >> (8 * b));
+            }
+            continue;
+        }
+#if defined(RC_GEMM_ABLATION)
+        const int skip = g_band_skip;
+#else
+        constexpr int skip = 0;
+#endif
+#pragma unroll 1
+        for (int p = lane; p < npair; p += 64) {
+            uint32_t w0 = p, w1 = p;
+            if (!(skip & 1)) pair_rgb(tp, p, w0, w1);
+            if (2 * p + 1 < W) *reinterpret_cast<uint2 *>(rowbuf + 2 * p) = make_uint2(w0, w1);
+            else rowbuf[2 * p] = w0;
+        }
+        // the row buffer is this wave's alone and LDS executes a wave's accesses in order: no
+        // barrier, only no compiler reordering across this point
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (skip & 2) {
+        } else if constexpr (MAXT > 0) {
+#pragma unroll
+            for (int t = 0; t < BAND_NXO; ++t) {
+                const int xo = lane + 64 * t;
+                if (xo < S) {
                     int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
 #pragma unroll
                     for (int k = 0; k < MAXT; ++k) {
-                        a0 += p[px[k]] * cf[k];
-                        a1 += p[px[k] + 1] * cf[k];
-                        a2 += p[px[k] + 2] * cf[k];
+                        const uint32_t w = rowbuf[px[t][k]];
+                        a0 += (int)(w & 255u) * cf[t][k];
+                        a1 += (int)((w >> 8) & 255u) * cf[t][k];
+                        a2 += (int)(w >> 16) * cf[t][k];
                     }
-                    uint8_t *o = tmp + (rr * S + xo) * 3;
-                    o[0] = clip8_22(a0);
-                    o[1] = clip8_22(a1);
-                    o[2] = clip8_22(a2);
+                    trow[3 * xo] = clip8_22(a0);
+                    trow[3 * xo + 1] = clip8_22(a1);
+                    trow[3 * xo + 2] = clip8_22(a2);
                 }
             }
         } else {
-            const int n = rows * S;
-            for (int idx = threadIdx.x; idx < n; idx += 256) {
-                const int rr = idx / S, xo = idx - rr * S;
+            for (int xo = lane; xo < S; xo += 64) {
                 const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
                 const int *c = r.hc + xo * r.hk;
-                const uint8_t *p = src + (rr * W + xmin) * 3;
                 int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
                 for (int k = 0; k < xn; ++k) {
+                    const uint32_t w = rowbuf[xmin + k];
                     const int ck = c[k];
-                    a0 += p[3 * k] * ck;
-                    a1 += p[3 * k + 1] * ck;
-                    a2 += p[3 * k + 2] * ck;
+                    a0 += (int)(w & 255u) * ck;
+                    a1 += (int)((w >> 8) & 255u) * ck;
+                    a2 += (int)(w >> 16) * ck;
                 }
-                uint8_t *o = tmp + 3 * idx;
-                o[0] = clip8_22(a0);
-                o[1] = clip8_22(a1);
-                o[2] = clip8_22(a2);
+                trow[3 * xo] = clip8_22(a0);
+                trow[3 * xo + 1] = clip8_22(a1);
+                trow[3 * xo + 2] = clip8_22(a2);
             }
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the next row rewrites the row buffer
     }
-    // 3. vertical pass into the band's LDS image (over src, free now, when it fits), then 16-B
-    //    stores: a lane owns columns, the band's output rows (and their taps) are wave-uniform
-    if (r.need_v) {
-        for (int x = threadIdx.x; x < S; x += 256)
-            for (int j = 0; j < nout; ++j) {
-                const int yo = yo0 + j;
-                const int ymin = r.vb[2 * yo] - lo, yn = r.vb[2 * yo + 1];
-                const int *c = r.vc + yo * r.vk;
-                const uint8_t *q = tmp + (ymin * S + x) * 3;
-                int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-                for (int k = 0; k < yn; ++k) {
-                    const int ck = c[k];
-                    a0 += q[k * S * 3] * ck;
-                    a1 += q[k * S * 3 + 1] * ck;
-                    a2 += q[k * S * 3 + 2] * ck;
-                }
-                uint8_t *o = band + (j * S + x) * 3;
-                o[0] = clip8_22(a0);
-                o[1] = clip8_22(a1);
-                o[2] = clip8_22(a2);
+    __syncthreads();
+    // 2. vertical pass (or, without one, the rows as they are), one output row per wave at a time
+    const int rowbytes = 3 * S, nw = TP >> 2;
+    const bool words = (rowbytes & 3) == 0;  // out_off = i·S·S·3 is then 4-aligned as well
+    uint8_t *gimg = out + r.out_off;
+    const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tmp);
+    for (int j = wave; j < nout; j += 4) {
+        const int yo = yo0 + j;
+        uint8_t *grow = gimg + (int64_t)yo * rowbytes;
+        if (!r.need_v) {
+            for (int cw = lane; cw < nw; cw += 64) {
+                const uint32_t v = t32[j * nw + cw];
+                if (words) *reinterpret_cast<uint32_t *>(grow + 4 * cw) = v;
+                else
+                    for (int b = 0; b < 4; ++b)
+                        if (4 * cw + b < rowbytes) grow[4 * cw + b] = (uint8_t)(v >> (8 * b));
             }
-        __syncthreads();
-    }
-    uint8_t *g = out + r.out_off + (int64_t)yo0 * S * 3;
-    const int nbytes = nout * S * 3;
-    if (((r.out_off + (int64_t)yo0 * S * 3) & 15) == 0 && (nbytes & 15) == 0) {
-        for (int i = threadIdx.x; i < nbytes / 16; i += 256)
-            reinterpret_cast<uint4 *>(g)[i] = reinterpret_cast<const uint4 *>(band)[i];
-    } else {
-        for (int i = threadIdx.x; i < nbytes; i += 256) g[i] = band[i];
+            continue;
+        }
+        const int ymin = r.vb[2 * yo] - lo;
+#if defined(RC_GEMM_ABLATION)
+        const int yn = (g_band_skip & 4) ? 0 : r.vb[2 * yo + 1];
+#else
+        const int yn = r.vb[2 * yo + 1];
+#endif
+        const int *c = r.vc + yo * r.vk;
+        for (int cw = lane; cw < nw; cw += 64) {
+            const uint32_t *q = t32 + ymin * nw + cw;
+            int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
+            for (int k = 0; k < yn; ++k) {
+                const uint32_t w = q[k * nw];
+                const int ck = c[k];
+                a0 += (int)(w & 255u) * ck;
+                a1 += (int)((w >> 8) & 255u) * ck;
+                a2 += (int)((w >> 16) & 255u) * ck;
+                a3 += (int)(w >> 24) * ck;
+            }
+            const uint32_t v = (uint32_t)clip8_22(a0) | ((uint32_t)clip8_22(a1) << 8) | ((uint32_t)clip8_22(a2) << 16) |
+                               ((uint32_t)clip8_22(a3) << 24);
+            if (words) *reinterpret_cast<uint32_t *>(grow + 4 * cw) = v;
+            else
+                for (int b = 0; b < 4; ++b)
+                    if (4 * cw + b < rowbytes) grow[4 * cw + b] = (uint8_t)(v >> (8 * b));
+        }
     }
 }
 }  // namespace jpeg
 
-// Batched decoder: pinned host staging + device buffers sized at create.
+// Batched decoder: one pinned host staging buffer and its device twin, sized at create.  A call
+// lays out [Desc × n | RDesc × n | quant tables × n | qsel × blocks | coefficients × blocks] in
+// both (stage_layout) and uploads it with ONE copy (a lone /embed image paid 5 copies, ~5 us each).
 struct JpegDecoder {
     int device = 0;
     int max_images = 0;
     int64_t max_blocks = 0;
+    uint8_t *h_stage = nullptr, *d_stage = nullptr;
+    size_t stage_cap = 0, stage_used = 0;
+    // views into the staging (set per call by stage_layout)
     int16_t *h_coef = nullptr;
     int32_t *h_qsel = nullptr;
     uint16_t *h_qtab = nullptr;
@@ -936,8 +1048,8 @@ struct JpegDecoder {
     uint8_t *d_planes = nullptr;
     hipEvent_t staged = nullptr;  // the last H2D copy out of the pinned staging
     std::mutex mu;
-    // fused decode → resize: per-image plans (pinned + device), the horizontal pass's output,
-    // Pillow coefficient tables per (size in, size out, filter, y0 shift) built on first use
+    // fused decode → resize: per-image plans (in the staging), the two-pass path's horizontal
+    // output, Pillow coefficient tables per (size in, size out, filter, y0 shift) built on first use
     jpeg::RDesc *h_rdesc = nullptr, *d_rdesc = nullptr;
     uint8_t *d_tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -975,6 +1087,31 @@ extern "C" int rc_jpeg_decode_coefficients(const uint8_t *jpg, int64_t len, int1
     });
 }
 
+// The staging layout of a call with n images and nb blocks (256-B aligned regions); with the
+// buffers allocated, points the h_* / d_* views at it.  Returns the bytes used.
+static size_t stage_layout(JpegDecoder *h, int n, int64_t nb) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_rdesc = al((size_t)n * sizeof(jpeg::Desc));
+    const size_t o_qtab = o_rdesc + al((size_t)n * sizeof(jpeg::RDesc));
+    const size_t o_qsel = o_qtab + al((size_t)n * 3 * 128);
+    const size_t o_coef = o_qsel + al((size_t)nb * 4);
+    const size_t total = o_coef + (size_t)nb * 128;
+    if (h->h_stage != nullptr) {
+        h->h_desc = reinterpret_cast<jpeg::Desc *>(h->h_stage);
+        h->h_rdesc = reinterpret_cast<jpeg::RDesc *>(h->h_stage + o_rdesc);
+        h->h_qtab = reinterpret_cast<uint16_t *>(h->h_stage + o_qtab);
+        h->h_qsel = reinterpret_cast<int32_t *>(h->h_stage + o_qsel);
+        h->h_coef = reinterpret_cast<int16_t *>(h->h_stage + o_coef);
+        h->d_desc = reinterpret_cast<jpeg::Desc *>(h->d_stage);
+        h->d_rdesc = reinterpret_cast<jpeg::RDesc *>(h->d_stage + o_rdesc);
+        h->d_qtab = reinterpret_cast<uint16_t *>(h->d_stage + o_qtab);
+        h->d_qsel = reinterpret_cast<int32_t *>(h->d_stage + o_qsel);
+        h->d_coef = reinterpret_cast<int16_t *>(h->d_stage + o_coef);
+        h->stage_used = total;
+    }
+    return total;
+}
+
 extern "C" int rc_jpeg_decoder_create(int device, int max_images, int64_t max_blocks, rc_jpeg_decoder **out) {
     return guard([&] {
         RC_REQUIRE(out && max_images > 0 && max_blocks > 0, RC_ERR_INVALID, "bad decoder size");
@@ -984,17 +1121,10 @@ extern "C" int rc_jpeg_decoder_create(int device, int max_images, int64_t max_bl
         h->max_images = max_images;
         h->max_blocks = max_blocks;
         try {
-            RC_HIP(hipHostMalloc((void **)&h->h_coef, (size_t)max_blocks * 128, hipHostMallocDefault));
-            RC_HIP(hipHostMalloc((void **)&h->h_qsel, (size_t)max_blocks * 4, hipHostMallocDefault));
-            RC_HIP(hipHostMalloc((void **)&h->h_qtab, (size_t)max_images * 3 * 128, hipHostMallocDefault));
-            RC_HIP(hipHostMalloc((void **)&h->h_desc, (size_t)max_images * sizeof(jpeg::Desc), hipHostMallocDefault));
-            h->d_coef = (int16_t *)dmalloc((size_t)max_blocks * 128);
-            h->d_qsel = (int32_t *)dmalloc((size_t)max_blocks * 4);
-            h->d_qtab = (uint16_t *)dmalloc((size_t)max_images * 3 * 128);
-            h->d_desc = (jpeg::Desc *)dmalloc((size_t)max_images * sizeof(jpeg::Desc));
+            h->stage_cap = stage_layout(h, max_images, max_blocks);
+            RC_HIP(hipHostMalloc((void **)&h->h_stage, h->stage_cap, hipHostMallocDefault));
+            h->d_stage = (uint8_t *)dmalloc(h->stage_cap);
             h->d_planes = (uint8_t *)dmalloc((size_t)max_blocks * 64);
-            h->h_rdesc = (jpeg::RDesc *)hmalloc((size_t)max_images * sizeof(jpeg::RDesc));
-            h->d_rdesc = (jpeg::RDesc *)dmalloc((size_t)max_images * sizeof(jpeg::RDesc));
             RC_HIP(hipEventCreateWithFlags(&h->staged, hipEventDisableTiming));
         } catch (...) {
             rc_jpeg_decoder_destroy(h);
@@ -1009,17 +1139,9 @@ extern "C" int rc_jpeg_decoder_destroy(rc_jpeg_decoder *h) {
         if (!h) return;
         DeviceScope ds(h->device);
         if (h->staged) (void)hipEventSynchronize(h->staged);
-        if (h->h_coef) (void)hipHostFree(h->h_coef);
-        if (h->h_qsel) (void)hipHostFree(h->h_qsel);
-        if (h->h_qtab) (void)hipHostFree(h->h_qtab);
-        if (h->h_desc) (void)hipHostFree(h->h_desc);
-        dfree(h->d_coef);
-        dfree(h->d_qsel);
-        dfree(h->d_qtab);
-        dfree(h->d_desc);
+        if (h->h_stage) (void)hipHostFree(h->h_stage);
+        dfree(h->d_stage);
         dfree(h->d_planes);
-        hfree(h->h_rdesc);
-        dfree(h->d_rdesc);
         dfree(h->d_tmp);
         for (auto &kv : h->coeffs) {
             dfree(kv.second.bounds);
@@ -1048,11 +1170,10 @@ namespace {
 
 std::atomic<int> g_active_decodes{0};  // decode calls in their Huffman pass right now (any decoder)
 
-// Header parse, host Huffman (threaded), pinned staging and H2D copies, IDCT into
-// h->d_planes; fills h->h_desc / h->d_desc (rgb_off from rgb_offsets, or 0).  The caller
-// records h->staged after its own uploads from pinned memory and launches the colour pass.
-void stage_idct(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens, const int64_t *rgb_offsets,
-                hipStream_t s, std::vector<jpeg::Header> &hd, int &maxpix) {
+// Header parse, host Huffman (threaded) into the pinned staging; fills h->h_desc (rgb_off from
+// rgb_offsets, or 0) and the tables.  The caller adds its plans (h_rdesc), then upload_idct.
+void stage_host(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int64_t *lens, const int64_t *rgb_offsets,
+                std::vector<jpeg::Header> &hd, int &maxpix, int64_t &nblocks) {
     // headers first (cheap, serial): geometry, block offsets, capacity check
     hd.assign(n, jpeg::Header{});
     std::vector<int64_t> base(n + 1, 0);
@@ -1064,6 +1185,7 @@ void stage_idct(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int
     RC_REQUIRE(base[n] <= h->max_blocks, RC_ERR_INVALID, "batch exceeds the decoder's max_blocks");
     // the pinned staging is reused: wait for the previous call's upload
     RC_HIP(hipEventSynchronize(h->staged));
+    stage_layout(h, n, base[n]);
     // Huffman decode, one image per worker
     std::vector<std::string> errs(n);
     auto work = [&](int i) {
@@ -1116,11 +1238,14 @@ void stage_idct(rc_jpeg_decoder *h, int n, const uint8_t *const *jpgs, const int
         RC_REQUIRE((int64_t)H.width * H.height < (int64_t)1 << 31, RC_ERR_INVALID, "image too large");
         maxpix = std::max(maxpix, H.width * H.height);
     }
-    const int64_t nb = base[n];
-    RC_HIP(hipMemcpyAsync(h->d_coef, h->h_coef, (size_t)nb * 128, hipMemcpyHostToDevice, s));
-    RC_HIP(hipMemcpyAsync(h->d_qsel, h->h_qsel, (size_t)nb * 4, hipMemcpyHostToDevice, s));
-    RC_HIP(hipMemcpyAsync(h->d_qtab, h->h_qtab, (size_t)n * 3 * 128, hipMemcpyHostToDevice, s));
-    RC_HIP(hipMemcpyAsync(h->d_desc, h->h_desc, (size_t)n * sizeof(jpeg::Desc), hipMemcpyHostToDevice, s));
+    nblocks = base[n];
+}
+
+// One H2D copy of the call's staging (descriptors, plans, tables, coefficients), the event the
+// next call waits on before it rewrites the staging, and the IDCT into h->d_planes.
+void upload_idct(rc_jpeg_decoder *h, int64_t nb, hipStream_t s) {
+    RC_HIP(hipMemcpyAsync(h->d_stage, h->h_stage, h->stage_used, hipMemcpyHostToDevice, s));
+    RC_HIP(hipEventRecord(h->staged, s));
     hipLaunchKernelGGL(jpeg::jpeg_idct_kernel, dim3((unsigned)((nb + 7) / 8)), dim3(64), 0, s, h->d_coef, h->d_qsel,
                        h->d_qtab, nb, h->d_planes);
     RC_LAUNCH_CHECK();
@@ -1164,8 +1289,9 @@ extern "C" int rc_jpeg_decode(rc_jpeg_decoder *h, int n, const uint8_t *const *j
         hipStream_t s = (hipStream_t)stream;
         std::vector<jpeg::Header> hd;
         int maxpix = 0;
-        stage_idct(h, n, jpgs, lens, rgb_offsets, s, hd, maxpix);
-        RC_HIP(hipEventRecord(h->staged, s));
+        int64_t nb = 0;
+        stage_host(h, n, jpgs, lens, rgb_offsets, hd, maxpix, nb);
+        upload_idct(h, nb, s);
         hipLaunchKernelGGL(jpeg::jpeg_color_kernel, dim3((unsigned)((maxpix + 255) / 256), (unsigned)n), dim3(256), 0, s,
                            h->d_planes, h->d_desc, rgb);
         RC_LAUNCH_CHECK();
@@ -1186,7 +1312,8 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
         hipStream_t s = (hipStream_t)stream;
         std::vector<jpeg::Header> hd;
         int maxpix = 0;
-        stage_idct(h, n, jpgs, lens, nullptr, s, hd, maxpix);
+        int64_t nb = 0;
+        stage_host(h, n, jpgs, lens, nullptr, hd, maxpix, nb);
         const int S = out_size;
         int64_t tmp_need = 0;
         int maxrows = 1, maxbands = 1, band_lds = 0, max_hk = 0;
@@ -1224,15 +1351,16 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
             }
             r.out_off = (int64_t)i * S * S * 3;
             maxrows = std::max(maxrows, r.Hs);
-            // band height: the tallest band (32 .. 1 output rows) whose LDS (planes' block rows +
-            // colour rows + horizontal pass + band) fits 32 KB, else 64 KB — and no taller than
-            // gives the batch >= 128 blocks (a lone /embed image: 224 / 4 = 56 bands, not 7-14)
+            // band height: the tallest band (32 .. 1 output rows) whose LDS (planes' block rows + the
+            // 4 waves' colour row buffers + horizontal pass) fits 40 KB (4 blocks per CU), else 64 KB
+            // — and no taller than gives the batch >= 128 blocks (a lone /embed image: 224 / 4 = 56
+            // bands, not 7-14)
             r.bh = 0;
             int need = 0;
             int bh_max = 32;
             while (bh_max > 4 && (int64_t)n * ((S + bh_max - 1) / bh_max) < 128) bh_max /= 2;
             const jpeg::Desc &dd = h->h_desc[i];
-            for (const int cap : {32 * 1024, 64 * 1024}) {
+            for (const int cap : {40 * 1024, 64 * 1024}) {
                 for (int bh = bh_max; bh >= 1 && r.bh == 0; bh /= 2) {
                     int worst = 0;
                     for (int yo0 = 0; yo0 < S; yo0 += bh) {
@@ -1240,7 +1368,7 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
                         const int lo = vb ? (*vb)[2 * yo0] : yo0;
                         const int hi = vb ? (*vb)[2 * (yo1 - 1)] + (*vb)[2 * (yo1 - 1) + 1] : yo1;
                         const int pl = jpeg::band_planes_bytes(dd, r.y0 + lo, r.y0 + hi, nullptr);
-                        worst = std::max(worst, jpeg::band_layout(hi - lo, yo1 - yo0, W, S, r.need_h, r.need_v, pl).total);
+                        worst = std::max(worst, jpeg::band_layout(hi - lo, W, S, r.need_h, pl).total);
                     }
                     if (worst <= cap) {
                         r.bh = bh;
@@ -1255,16 +1383,15 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
                 band_lds = std::max(band_lds, need);
             }
         }
+        upload_idct(h, nb, s);  // with the plans
         if (band_ok) {
-            RC_HIP(hipMemcpyAsync(h->d_rdesc, h->h_rdesc, (size_t)n * sizeof(jpeg::RDesc), hipMemcpyHostToDevice, s));
-            RC_HIP(hipEventRecord(h->staged, s));
             const dim3 gr((unsigned)maxbands, (unsigned)n);
             // horizontal taps in registers: 5 (any bicubic upscale, e.g. the fixture's 168 -> 224), 7
-            // (down to 1.5x), else the general form
-            if (max_hk <= 5)
+            // (down to 1.5x), else (or S > 256) the general form
+            if (max_hk <= 5 && S <= 64 * jpeg::BAND_NXO)
                 hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<5>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
                                    h->d_desc, h->d_rdesc, out);
-            else if (max_hk <= 7)
+            else if (max_hk <= 7 && S <= 64 * jpeg::BAND_NXO)
                 hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<7>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
                                    h->d_desc, h->d_rdesc, out);
             else
@@ -1282,8 +1409,6 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
             h->d_tmp = (uint8_t *)dmalloc(want);
             h->tmp_bytes = want;
         }
-        RC_HIP(hipMemcpyAsync(h->d_rdesc, h->h_rdesc, (size_t)n * sizeof(jpeg::RDesc), hipMemcpyHostToDevice, s));
-        RC_HIP(hipEventRecord(h->staged, s));
         hipLaunchKernelGGL(jpeg::jpeg_color_resize_h_kernel, dim3((unsigned)maxrows, (unsigned)n), dim3(256), 0, s,
                            h->d_planes, h->d_desc, h->d_rdesc, h->d_tmp, out);
         RC_LAUNCH_CHECK();
@@ -1292,3 +1417,10 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
         RC_LAUNCH_CHECK();
     });
 }
+
+#if defined(RC_GEMM_ABLATION)
+// diagnostic builds: the band kernel's phase-skip mask (g_band_skip)
+extern "C" int rc_diag_set_band_skip(int mask) {
+    return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(jpeg::g_band_skip), &mask, sizeof(mask))); });
+}
+#endif

@@ -543,7 +543,7 @@ constexpr int I8_SL = 24;  // candidate rows staged in LDS per query per block (
 // LDS atomic add / store as inline asm: written in C++, hipcc cannot tell these words from the
 // LDS-DMA ring in the same __shared__ array and waits vmcnt(0) (the whole ring) before each one.
 // The add's own lgkmcnt(0) is inside the statement, so its result is ready when it ends; the
-// stores are retired by the block barrier before the flush reads them.
+// stores are retired by an explicit lgkmcnt(0) ahead of the block barrier before the flush.
 __device__ __forceinline__ uint32_t lds_add_rtn_u32(uint32_t *p, uint32_t v) {
     uint32_t r;
     asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"((uint32_t)(uintptr_t)p), "v"(v) : "memory");
@@ -786,7 +786,9 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
         }
         load_scales(min(tile + 1, ntiles - 1));  // unconditional: the same wait counts on every path
     }
-    // flush the staged candidates: one global atomic per query that has any
+    // flush the staged candidates: one global atomic per query that has any.  The asm stores are
+    // invisible to the compiler's wait-count tracking, so retire them explicitly before the barrier.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < SB_TILE) {
         const uint32_t n = min(lcnt[tid], (uint32_t)I8_SL);

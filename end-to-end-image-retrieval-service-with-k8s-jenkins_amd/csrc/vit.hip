@@ -523,12 +523,14 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
                                scale * 1.4426950408889634f);
         } else
 #endif
+        // fewer items than CUs: each item's query tiles split over 4 blocks (a lone image: 48 blocks)
+        const int qsplit = items < m->ncu ? 4 : 1;
         if (T == 197) {
-            hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(items), dim3(256), 0, s, qkv, attn, T, c.heads,
-                               scale * 1.4426950408889634f);
+            hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f, qsplit);
         } else {
-            hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(items), dim3(256), 0, s, qkv, attn, T, c.heads,
-                               scale * 1.4426950408889634f);
+            hipLaunchKernelGGL(attention_v2_kernel<0>, dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f, qsplit);
         }
         RC_LAUNCH_CHECK();
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
@@ -878,8 +880,8 @@ extern "C" int rc_diag_set_stamps(void *dev) {
     return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rc_stamps), &dev, sizeof(dev))); });
 }
 
-// diagnostic builds: attention_v2_kernel (2) or attention_v3_kernel (3, the product's) for the
-// full-token layers (A/B; the same bits)
+// diagnostic builds: attention_v2_kernel (2, the product's) or attention_v3_kernel (3, lost the
+// A/B) for the full-token layers (the same bits)
 extern "C" int rc_diag_set_attention(rc_model *m, int form) {
     return guard([&] {
         RC_REQUIRE(m && (form == 2 || form == 3), RC_ERR_INVALID, "attention form must be 2 or 3");

@@ -90,7 +90,7 @@ struct GemmArgs {
 // Partials (round 3): per row, LN_PARTS = 12 blocks of 64 columns, each (mean, M2) —
 // the 64 columns one wave of a tiled GEMM holds per row, so the producer epilogues reduce
 // inside the wave (two permlane swaps) and never across waves.  Canonical order, which
-// every producer (tiled epilogues, ln_emit_kernel, cls_init_kernel) reproduces bit for
+// every producer (tiled epilogues, gemm_skinny_ln_kernel, cls_init_kernel) reproduces bit for
 // bit: "slice" g = 0..3 of a block holds the 16 columns 32c + 16(g & 1) + 8(g >> 1) + k
 // (c = 0, 1; k = 0..7 — after one v_permlane16_swap, the 8 consecutive columns a lane of
 // the accumulator layout holds per 32-column chunk); ln_slice_stats gives its (mean, M2),
@@ -109,7 +109,7 @@ __device__ __forceinline__ int ln_slice_col(int g, int c) { return 32 * c + 16 *
 // (patch GEMM, O-proj, fc2, cls_init) write 3 B per element and the residual epilogues read
 // 3 B (round 2 kept lo as a second bf16: 4 B each way).  Every reader forms x′ with hl_value's
 // arithmetic, and the producers compute the LN statistics from that same x′, so the skinny
-// (ln_emit_kernel) and tiled paths stay bit-identical.
+// (gemm_skinny_ln_kernel) and tiled paths stay bit-identical.
 __device__ __forceinline__ float4 bf16x4_f32(uint2 u) {
     return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                        __uint_as_float(u.y & 0xffff0000u));
@@ -511,15 +511,19 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
 
 // TOK > 0: the token count as a compile-time constant (197 for ViT-B/16 at 224),
 // so only the last key tile carries the padding mask; TOK = 0 reads `tokens`.
+// qsplit > 1 (small batches: a lone image is 12 (image, head) items for 256 CUs): block b is
+// part b % qsplit of item b / qsplit and takes query tiles qs·4 + wave, stepping 4·qsplit — each
+// part stages the head's K and V (L2 hits after the first) and runs the same per-tile arithmetic.
 template <int TOK>
 __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
-                                                          int tokens_rt, int heads, float scale_log2e) {
+                                                          int tokens_rt, int heads, float scale_log2e, int qsplit) {
     constexpr int W = 4, HALF = W / 2, HD = 64, PPW = ATT2_TILES * 2 / HALF;  // 13 DMA pieces per wave
     const int tokens = TOK > 0 ? TOK : tokens_rt;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];
     uint8_t *Ks = lds, *Vs = lds + ATT2_ROWS * 128;
     const int H = heads * HD, H3 = 3 * H;
-    const int img = blockIdx.x / heads, h = blockIdx.x % heads;
+    const int item = blockIdx.x / qsplit, qs = blockIdx.x % qsplit;
+    const int img = item / heads, h = item % heads;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint16_t *base = qkv + (int64_t)img * tokens * H3 + h * HD;
@@ -541,8 +545,9 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     // waves 0-1 stage K (pieces 0-25), waves 2-3 stage V (26-51).  K is waited for before the
     // scores, V only before the first P·V: V's transfer runs under the first tile's QKᵀ and
     // softmax (one block's load is no longer one serial phase ahead of its math).
+    const int t0 = qs * W + wave, tstep = W * qsplit;  // this wave's query tiles
     bf16x8 qf[2];
-    load_q(wave < nqt ? wave : 0, qf);
+    load_q(t0 < nqt ? t0 : 0, qf);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
         // waves 0-1 stage K pieces w PPW + i, waves 2-3 the V pieces
@@ -572,21 +577,21 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     auto pv_store = [&](int qt) { att_pv_store(Vs, st, sum, qt, tokens, out + (int64_t)img * tokens * H + h * HD, H); };
 
     // first tile: scores while V lands, then every wave waits for V once
-    const bool first = wave < nqt;
+    const bool first = t0 < nqt;
     bf16x8 qn[2];
-    if (first && wave + W < nqt) load_q(wave + W, qn);  // the next tile's queries, under the scores
+    if (first && t0 + tstep < nqt) load_q(t0 + tstep, qn);  // the next tile's queries, under the scores
     if (first) scores(qf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V staged (waves HALF..), qn landed
     bar();
     __builtin_amdgcn_sched_barrier(0);
-    if (first) pv_store(wave);
-    for (int qt = wave + W; qt < nqt; qt += W) {
+    if (first) pv_store(t0);
+    for (int qt = t0 + tstep; qt < nqt; qt += tstep) {
         // qn (issued a tile ago) has landed; the previous tile's 4 output stores may still fly
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         qf[0] = qn[0];
         qf[1] = qn[1];
-        if (qt + W < nqt) load_q(qt + W, qn);  // prefetch the next tile's queries
+        if (qt + tstep < nqt) load_q(qt + tstep, qn);  // prefetch the next tile's queries
         scores(qf);
         pv_store(qt);
     }

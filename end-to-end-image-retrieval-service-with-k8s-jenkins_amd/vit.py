@@ -262,13 +262,12 @@ class VitMsnEmbedder:
                     x = torch.stack([torch.as_tensor(np.asarray(images[i], dtype=np.uint8)).to(self.device)
                                      if not isinstance(images[i], torch.Tensor) else images[i].to(self.device)
                                      for i in chunk])
-                r, m = self.embed(x, normalized=normalized)
                 c0 = chunk[0]
-                if chunk == list(range(c0, c0 + len(chunk))):  # in input order: a slice copy, no host sync
-                    raw[c0:c0 + len(chunk)].copy_(r)
-                    if normalized:
-                        nrm[c0:c0 + len(chunk)].copy_(m)
+                if chunk == list(range(c0, c0 + len(chunk))):  # in input order: embedded into its rows
+                    sl = slice(c0, c0 + len(chunk))
+                    self.embed(x, normalized=normalized, out=(raw[sl], nrm[sl] if normalized else None))
                     continue
+                r, m = self.embed(x, normalized=normalized)
                 sel = torch.tensor(chunk, dtype=torch.int64).pin_memory().to(self.device, non_blocking=True)
                 raw.index_copy_(0, sel, r)
                 if normalized:
