@@ -993,11 +993,13 @@ __device__ __forceinline__ int skinny_block(int b, int nwg) {
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
 }
 
+// One wave per block: the loads are address-bound (PMC: the texture addresser busy for the
+// whole launch on the CUs holding blocks), so a tile per CU where 4-wave blocks put four.
 template <int EPI, int NI, int KT>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
+__global__ __launch_bounds__(64) void gemm_skinny_kernel(GemmArgs a) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
     const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
-    const int w = skinny_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    const int w = skinny_block(blockIdx.x, gridDim.x);
     if (w >= nct * nrt) return;
     const int ct = w / nrt, rt = w % nrt;
     const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
@@ -1048,22 +1050,22 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs a) {
 // O-proj / fc2 of a batch of one image, the CLS O-proj): the block-partial statistics are
 // computed in the epilogue (the canonical slices and reduction tree of every producer, bit for bit;
 // round 4 ran them as a second launch, 5 us each at batch 1).
-// A block of 4 waves owns 2 row tiles × one 64-column LayerNorm block (blocks numbered column-
-// block-major through skinny_block: a column block's weights stay in one XCD): wave w computes rows
-// 16·(2·rtp + (w >> 1)) + li, columns 64·blk + 32·(w & 1) + 16·ni + 4g + e (the skinny kernel's
-// tile and K chain), stores as gemm_skinny_kernel does and puts the value each element now stands
-// for (the stored f32, or hl_value of the stored pair) into LDS; then waves 0-1 read the 32 rows'
-// canonical slices (4 lanes per row) and reduce them with ln_block_reduce_quad.
+// A block of 2 waves owns one row tile × one 64-column LayerNorm block (blocks numbered column-
+// block-major through skinny_block: a column block's weights stay in one XCD): wave w computes
+// rows 16·rt + li, columns 64·blk + 32·w + 16·ni + 4g + e (the skinny kernel's tile and K chain),
+// stores as gemm_skinny_kernel does and puts the value each element now stands for (the stored
+// f32, or hl_value of the stored pair) into LDS; then wave 0 reads the 16 rows' canonical slices
+// (4 lanes per row) and reduces them with ln_block_reduce_quad.  (4-wave blocks of two row
+// tiles: 84 blocks for a lone image's fc2, address-bound on 84 CUs at 34 us.)
 template <int EPI, int KT>
-__global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(GemmArgs a) {
+__global__ __launch_bounds__(128) void gemm_skinny_ln_kernel(GemmArgs a) {
     static_assert(epi_resid(EPI), "LayerNorm producers are residual epilogues");
     constexpr int NI = 2, LP = 68;  // LDS row pitch (floats)
-    __shared__ float xs_l[32 * LP];
+    __shared__ float xs_l[16 * LP];
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15, wave = threadIdx.x >> 6;
-    const int nrtp = (a.M + 31) / 32, lb = skinny_block(blockIdx.x, gridDim.x);
-    const int blk = lb / nrtp, rtp = lb % nrtp;  // column-block-major (skinny_block)
-    const int rl = (wave >> 1) * 16 + li;  // row within the block's 32
-    const int K = a.K, n0 = blk * 64 + (wave & 1) * 32, row = rtp * 32 + rl;
+    const int nrt = (a.M + 15) / 16, lb = skinny_block(blockIdx.x, gridDim.x);
+    const int blk = lb / nrt, rt = lb % nrt;  // column-block-major (skinny_block)
+    const int K = a.K, n0 = blk * 64 + wave * 32, row = rt * 16 + li;
     const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;
     const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
     f32x4 acc[NI];
@@ -1090,11 +1092,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(GemmArgs a) {
                 *reinterpret_cast<uint2 *>(a.ln_x + off) = pack_bf16x4(x);
             }
         }
-        *reinterpret_cast<float4 *>(xs_l + rl * LP + (wave & 1) * 32 + ni * 16 + 4 * g) = x;
+        *reinterpret_cast<float4 *>(xs_l + li * LP + wave * 32 + ni * 16 + 4 * g) = x;
     }
     __syncthreads();
-    if (wave >= 2) return;
-    const int item = wave * 64 + lane, r = item >> 2, sg = item & 3;
+    if (wave != 0) return;
+    const int r = lane >> 2, sg = lane & 3;
     float xs[16];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -1104,7 +1106,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(GemmArgs a) {
         xs[8 * c + 4] = v.x, xs[8 * c + 5] = v.y, xs[8 * c + 6] = v.z, xs[8 * c + 7] = v.w;
     }
     const float2 st = ln_block_reduce_quad(ln_slice_stats(xs), sg);
-    const int srow = rtp * 32 + r;
+    const int srow = rt * 16 + r;
     if (sg == 0 && srow < a.M) *reinterpret_cast<float2 *>(a.ln_stats + (int64_t)srow * LN_STRIDE + 2 * blk) = st;
 }
 
@@ -1117,10 +1119,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(GemmArgs a) {
 // Used only on the CLS rows, so batch invariance is unaffected (the full-layer GEMMs of
 // a small batch keep the skinny kernel, bit-identical to the tiled ones).
 template <int NI, int KS, int KT>
-__global__ __launch_bounds__(256) void gemm_skinny_splitk_kernel(GemmArgs a, float *__restrict__ part) {
+__global__ __launch_bounds__(64) void gemm_skinny_splitk_kernel(GemmArgs a, float *__restrict__ part) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
     const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int w = blockIdx.x;  // one wave per block (address-bound loads: spread over CUs)
     if (w >= nct * nrt * KS) return;
     const int ks = w % KS, tile = w / KS;
     const int ct = tile % nct, rt = tile / nct;
@@ -1162,9 +1164,9 @@ inline void launch_skinny_splitk_resid(const GemmArgs &a, float *part, hipStream
                "split-K skinny GEMM: N % 32 == 0, K % 128 == 0, f32 residual");
     const int waves = ((a.M + 15) / 16) * (a.N / 32) * SKINNY_KS;
     if (a.K == 768 * SKINNY_KS)
-        hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS, 768>), dim3((waves + 3) / 4), dim3(256), 0, s, a, part);
+        hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS, 768>), dim3(waves), dim3(64), 0, s, a, part);
     else
-        hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS, 0>), dim3((waves + 3) / 4), dim3(256), 0, s, a, part);
+        hipLaunchKernelGGL((gemm_skinny_splitk_kernel<2, SKINNY_KS, 0>), dim3(waves), dim3(64), 0, s, a, part);
     RC_LAUNCH_CHECK();
     const int64_t n4 = (int64_t)a.M * a.N / 4;
     hipLaunchKernelGGL(skinny_reduce_kernel<SKINNY_KS>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, a, part);
@@ -1260,17 +1262,17 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             if constexpr (epi_resid(EPI)) {
                 if (a.ln_x != nullptr && a.ln_stats != nullptr) {  // LayerNorm-fold producer: partials in the epilogue
                     RC_REQUIRE(a.N == 64 * LN_PARTS, RC_ERR_UNSUPPORTED, "LayerNorm fold needs N = 768");
-                    const dim3 gr(((a.M + 31) / 32) * LN_PARTS);
-                    if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 768>), gr, dim3(256), 0, s, a);
-                    else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 3072>), gr, dim3(256), 0, s, a);
-                    else hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 0>), gr, dim3(256), 0, s, a);
+                    const dim3 gr(((a.M + 15) / 16) * LN_PARTS);
+                    if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 768>), gr, dim3(128), 0, s, a);
+                    else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 3072>), gr, dim3(128), 0, s, a);
+                    else hipLaunchKernelGGL((gemm_skinny_ln_kernel<EPI, 0>), gr, dim3(128), 0, s, a);
                     break;
                 }
             }
-            const dim3 gr((((a.M + 15) / 16) * (a.N / 32) + 3) / 4);
-            if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768>), gr, dim3(256), 0, s, a);
-            else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072>), gr, dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 0>), gr, dim3(256), 0, s, a);
+            const dim3 gr(((a.M + 15) / 16) * (a.N / 32));  // one wave (tile) per block
+            if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768>), gr, dim3(64), 0, s, a);
+            else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072>), gr, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 0>), gr, dim3(64), 0, s, a);
             break;
         }
         case GEMM_PINGPONG: {
