@@ -1184,10 +1184,10 @@ enum GemmVariant { GEMM_AUTO = 0, GEMM_PINGPONG = 4, GEMM_W2 = 8, GEMM_SKINNY = 
 inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_epilogue = false) {
     if (variant != GEMM_AUTO) return variant;  // (100 + ABL / 200 + ABL: ablation builds, RC_GEMM_ABLATION)
     if (a.M <= 256 && !patch_epilogue && a.N % 32 == 0) return GEMM_SKINNY;
-    // The residual producers (O-proj, fc2: N = 768, every row tile one image) on image-aligned
-    // tiles: a batch is n x 3 tiles, whole rounds of the 256 CUs (197-row images make 256-row
-    // tiles 2.31 rounds at any batch).
-    if (a.row_step > 0 && a.N % 256 == 0 && !patch_epilogue) return GEMM_PP_IMG;
+    // (Round 5 built image-aligned 224-row tiles for the residual producers — O-proj / fc2 as whole
+    // rounds, n x 3 tiles: per launch at parts = 1 fc2 276 vs 297 us, but at the product's parts = 2
+    // the two slices already fill each other's last round and the 12 % padded rows cost more:
+    // step 10.08 vs 9.99 ms, twice (profiles/r05/r05p_gemm_ab_p2.log).  Diagnostic builds only.)
     // Short square projections without image alignment (N = K = 768) finish in ~2.3 rounds of
     // 256x256 tiles and carry a heavy epilogue: the two-workgroup kernel overlaps it with the
     // co-resident workgroup's MFMAs.  Everything else streams K at 128 flop/B: ping-pong.
@@ -1281,6 +1281,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             launch_pp<EPI, 0, PP_BM>(a, (a.M + PP_BM - 1) / PP_BM, s);
             break;
         }
+#if defined(RC_GEMM_ABLATION)
         case GEMM_PP_IMG: {
             if constexpr (epi_resid(EPI)) {
                 // a tile computes 224 rows from its image's first row: the A buffer must hold
@@ -1294,7 +1295,6 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
-#if defined(RC_GEMM_ABLATION)
         case 200 + 1: case 200 + 2: case 200 + 4: case 200 + 6: {
             const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
             const dim3 gr(ntm * ntn), bl(256);

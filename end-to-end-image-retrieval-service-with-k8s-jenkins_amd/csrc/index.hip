@@ -171,25 +171,99 @@ __global__ __launch_bounds__(256) void merge_partials_kernel(const uint64_t *__r
     }
 }
 
-// First level of the two-level merge of many partial lists: block (g, qi) merges lists
-// [g·MERGE_L1, g·MERGE_L1 + MERGE_L1) of query qi into out[g][qi][0..k) (local keys; the second
-// level, merge_partials_kernel over those, applies the row map).  One block over ~2000 lists is
-// latency-bound (config 3, 1M rows / 1954 scan blocks: 30.5 us per call); G blocks of 32 lists
-// each, then one block over G lists, run the same per-wave top-k machinery in parallel.
-constexpr int MERGE_L1 = 32;
+// Top-k of many sorted partial lists, one query per block (config 3: 1M rows = 1024 scan blocks,
+// lists of k keys).  The answer's k-th key is at most hk, the k-th smallest of the lists' heads
+// (k heads are <= hk), and a sorted list can only contribute its prefix <= hk: so the block takes
+// the heads' top-k (one load per list, all in flight), then appends the prefixes <= hk of the
+// lists whose head qualifies (usually about k keys in all), then sorts those.  The same keys as
+// merging every list (merge_partial_lists, which loads all nlist·k keys: round 4's one block over
+// ~2000 lists was 30.5 us, the two-level form after it 11 + 12 us); more than CAP candidates
+// (adversarial inputs) fall back to that full merge inside the block.
+constexpr int MERGE_HEADS_MIN = 64;  // fewer lists: merge_partials_kernel (all keys) is as fast
 template <int CAP>
-__global__ __launch_bounds__(256) void merge_stage1_kernel(const uint64_t *__restrict__ partial, int nlist, int nq_total,
-                                                          int k, const int *__restrict__ flags, uint64_t *__restrict__ out) {
+__global__ __launch_bounds__(256) void merge_heads_kernel(const uint64_t *__restrict__ partial, int nlist, int nq_total,
+                                                         int k, int64_t row_base, int64_t row_stride,
+                                                         const int *__restrict__ flags, float *__restrict__ out_scores,
+                                                         int64_t *__restrict__ out_rows) {
     __shared__ uint64_t lds[4][CAP];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = blockIdx.x, qi = blockIdx.y;
+    __shared__ uint64_t cand[CAP];
+    __shared__ uint64_t hk_s;
+    __shared__ int ccount;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int qi = blockIdx.x;
     if (flags != nullptr && flags[qi] == 0) return;  // block-uniform
-    const int l0 = g * MERGE_L1, nl = min(MERGE_L1, nlist - l0);
+    auto at = [&](int l, int t) { return partial[((int64_t)l * nq_total + qi) * k + t]; };
     WaveTopK<CAP> tk;
-    merge_partial_lists<CAP>(partial + (int64_t)l0 * nq_total * k, nl, nq_total, qi, k, lds, tk);
+    tk.init(as_lds(&lds[wave][0]), k);
+    // 1. the heads' top-k: HU heads per lane in flight, then per-wave top-k, then wave 0 over 4·k
+    constexpr int HU = 8;
+    for (int l0 = 0; l0 < nlist; l0 += 256 * HU) {
+        uint64_t h[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+            const int l = l0 + u * 256 + tid;
+            h[u] = l < nlist ? at(l, 0) : KEY_EMPTY;
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+            tk.reserve(64);
+            tk.push(h[u] != KEY_EMPTY, h[u]);
+        }
+    }
+    tk.compact();
+    if (tid == 0) ccount = 0;
+    __syncthreads();
     if (wave == 0) {
-        uint64_t *dst = out + ((int64_t)g * nq_total + qi) * k;
-        for (int j = lane; j < k; j += 64) dst[j] = tk.buf[j];
+        for (int w = 1; w < 4; ++w)
+            for (int j = 0; j < k; j += 64) {
+                const uint64_t key = (j + lane < k) ? as_lds(&lds[w][0])[j + lane] : KEY_EMPTY;
+                tk.reserve(64);
+                tk.push(key != KEY_EMPTY, key);
+            }
+        tk.compact();
+        if (lane == 0) hk_s = tk.count >= k ? tk.buf[k - 1] : KEY_EMPTY;
+    }
+    __syncthreads();
+    const uint64_t hk = hk_s;
+    // 2. the prefixes <= hk of the lists whose head is <= hk (a list is sorted, EMPTY-padded)
+    for (int l = tid; l < nlist; l += 256) {
+        if (at(l, 0) > hk) continue;  // (an L2 hit: loaded in step 1)
+        for (int t0 = 0; t0 < k; t0 += 8) {
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = t0 + u < k ? at(l, t0 + u) : KEY_EMPTY;
+            bool more = true;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (v[u] <= hk && v[u] != KEY_EMPTY) {
+                    const int pos = atomicAdd(&ccount, 1);
+                    if (pos < CAP) cand[pos] = v[u];
+                } else {
+                    more = false;
+                }
+            }
+            if (!more) break;
+        }
+    }
+    __syncthreads();
+    const int nc = ccount;
+    if (nc > CAP) {  // block-uniform: the full merge
+        merge_partial_lists<CAP>(partial, nlist, nq_total, qi, k, lds, tk);
+    } else if (wave == 0) {
+        tk.init(as_lds(&lds[0][0]), k);
+        for (int j = 0; j < nc; j += 64) {
+            tk.reserve(64);
+            tk.push(j + lane < nc, j + lane < nc ? cand[j + lane] : KEY_EMPTY);
+        }
+        tk.compact();
+    }
+    if (wave == 0) {
+        for (int j = lane; j < k; j += 64) {
+            const uint64_t key = tk.buf[j];
+            const bool ok = key != KEY_EMPTY;
+            out_scores[(int64_t)qi * k + j] = ok ? key_score(key) : -INFINITY;
+            out_rows[(int64_t)qi * k + j] = ok ? row_base + (int64_t)key_idx(key) * row_stride : -1;
+        }
     }
 }
 
@@ -275,7 +349,6 @@ struct rc_index {
     int ws_nq = 0, ws_k = 0, ws_nblk = 0;
     float *qn = nullptr;
     uint64_t *partial = nullptr;
-    uint64_t *partial2 = nullptr;   // first-level merge output [kMaxBlocks / MERGE_L1][nq][k]
     unsigned *q1_done = nullptr;    // host-coherent completion word of the polled query1 path
     unsigned q1_seq = 0;
     BatchWs bws;         // batched MFMA search workspace (search_mfma.hip)
@@ -308,13 +381,10 @@ void ensure_workspace(rc_index *h, int nq, int k) {
     const int nq2 = std::max(nq, h->ws_nq), k2 = std::max(k, h->ws_k);
     dfree(h->qn);
     dfree(h->partial);
-    dfree(h->partial2);
     h->qn = nullptr;
     h->partial = nullptr;
-    h->partial2 = nullptr;
     h->qn = (float *)dmalloc((size_t)nq2 * h->ld * sizeof(float));
     h->partial = (uint64_t *)dmalloc((size_t)kMaxBlocks * nq2 * k2 * sizeof(uint64_t));
-    h->partial2 = (uint64_t *)dmalloc((size_t)(kMaxBlocks / MERGE_L1) * nq2 * k2 * sizeof(uint64_t));
     h->ws_nq = nq2;
     h->ws_k = k2;
 }
@@ -376,24 +446,18 @@ void launch_scan(rc_index *h, const ScanArgs &a) {
     }
 }
 
-// Top-k over nlist partial lists per query: one block per query, or — past 2·MERGE_L1 lists,
-// when the first-level buffer covers them (the scan's own h->partial) — two levels
-// (merge_stage1_kernel, then one block over its ceil(nlist / MERGE_L1) lists).  Same keys, same
-// total order: the result is identical either way.
+// Top-k over nlist sorted partial lists per query, one block per query: past MERGE_HEADS_MIN lists
+// through the lists' heads (merge_heads_kernel), else over every key (merge_partials_kernel).  The
+// same keys either way.
 template <int CAP>
 void launch_merge_partials_t(rc_index *h, const uint64_t *partial, const int *flags, int nlist, int nq, int nq_stride, int k,
                              float *scores, int64_t *rows, hipStream_t s) {
-    const bool two = nlist > 2 * MERGE_L1 && nlist <= kMaxBlocks && nq_stride <= h->ws_nq && k <= h->ws_k;
-    if (two) {
-        const int G = (nlist + MERGE_L1 - 1) / MERGE_L1;
-        hipLaunchKernelGGL(merge_stage1_kernel<CAP>, dim3(G, nq), dim3(256), 0, s, partial, nlist, nq_stride, k, flags,
-                           h->partial2);
-        RC_LAUNCH_CHECK();
-        partial = h->partial2;
-        nlist = G;
-    }
-    hipLaunchKernelGGL(merge_partials_kernel<CAP>, dim3(nq), dim3(256), 0, s, partial, nlist, nq_stride, k, h->row_base,
-                       h->row_stride, flags, scores, rows);
+    if (nlist >= MERGE_HEADS_MIN)
+        hipLaunchKernelGGL(merge_heads_kernel<CAP>, dim3(nq), dim3(256), 0, s, partial, nlist, nq_stride, k, h->row_base,
+                           h->row_stride, flags, scores, rows);
+    else
+        hipLaunchKernelGGL(merge_partials_kernel<CAP>, dim3(nq), dim3(256), 0, s, partial, nlist, nq_stride, k, h->row_base,
+                           h->row_stride, flags, scores, rows);
     RC_LAUNCH_CHECK();
 }
 
@@ -586,7 +650,6 @@ int rc_index_create(int device, int dim, int dtype, int64_t capacity, int64_t ro
             dfree(h->norms);
             dfree(h->qn);
             dfree(h->partial);
-            dfree(h->partial2);
             delete h;
             throw;
         }
@@ -606,7 +669,6 @@ int rc_index_destroy(rc_index *h) {
         dfree(h->norms);
         dfree(h->qn);
         dfree(h->partial);
-        dfree(h->partial2);
         if (h->q1_done != nullptr) (void)hipHostFree(h->q1_done);
         delete h;
     });

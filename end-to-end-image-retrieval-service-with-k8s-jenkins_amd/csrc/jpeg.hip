@@ -732,7 +732,7 @@ __host__ __device__ inline BandLayout band_layout(int rows, int W, int S, int ne
     BandLayout L;
     L.tp = (3 * S + 3) & ~3;
     L.rowbuf = pl;
-    L.tmp = pl + (need_h ? al(4 * ((W + 1) & ~1) * 4) : 0);  // 4 waves × W RGBX words (even, 8-B rows)
+    L.tmp = pl + (need_h ? al(4 * 2 * ((W + 1) & ~1) * 4) : 0);  // 4 waves × 2 rows × W RGBX words (8-B rows)
     L.total = L.tmp + al(rows * L.tp);
     return L;
 }
@@ -750,7 +750,9 @@ __host__ __device__ inline int band_planes_bytes(const Desc &d, int y_lo, int y_
     return total;
 }
 
-constexpr int BAND_NXO = 4;  // output columns per lane held in registers (S <= 256)
+constexpr int BAND_NXO = 4;   // output columns per lane held in registers (S <= 256)
+constexpr int BAND_MAXV = 8;  // vertical taps held as uniform constants (coefficient tables padded by this)
+typedef __attribute__((address_space(3))) void jpeg_lds_void_t;
 
 #if defined(RC_GEMM_ABLATION)
 // diagnostic builds: phases of jpeg_band_resize_kernel to skip (1 colour, 2 horizontal, 4 vertical
@@ -792,19 +794,22 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
             pl += pnbr[c] * d.bw[c] * 64;
         }
     }
+    // by LDS-DMA (global_load_lds_dwordx4: no register round trip, every piece of the three
+    // planes in flight at once, waited for once below; a wave writes 1 KB of LDS per instruction)
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (c < d.ncomp) {
-            const uint4 *g = reinterpret_cast<const uint4 *>(planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64);
-            uint4 *l = reinterpret_cast<uint4 *>(lds + poff[c]);
+            const uint8_t *g = planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64;
             const int n16 = pnbr[c] * d.bw[c] * 4;
-#pragma unroll 2
-            for (int i = threadIdx.x; i < n16; i += 256) l[i] = g[i];
+            for (int i0 = wave * 64; i0 < n16; i0 += 256)
+                if (i0 + lane < n16)
+                    __builtin_amdgcn_global_load_lds((const void *)(g + 16 * (i0 + lane)),
+                                                     (jpeg_lds_void_t *)(lds + poff[c] + 16 * i0), 16, 0, 0);
         }
     }
     const BandLayout L = band_layout(rows, W, S, r.need_h, pl);
     const int TP = L.tp;
-    uint32_t *rowbuf = reinterpret_cast<uint32_t *>(lds + L.rowbuf) + wave * ((W + 1) & ~1);
+    uint32_t *rowbuf = reinterpret_cast<uint32_t *>(lds + L.rowbuf) + wave * 2 * ((W + 1) & ~1);
     uint8_t *tmp = lds + L.tmp;
     // horizontal taps of this lane's output columns (MAXT > 0), kept across its wave's rows
     int cf[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1], px[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1];
@@ -822,6 +827,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
             }
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the plane DMA (and the taps) landed
     __syncthreads();
     // jdsample.c's upsampler for one source row y as wave-uniform row offsets into the LDS planes
     // (near / far sample row) and a kind: 0 the sample itself (1x1, or box h2 when the plane is
@@ -904,80 +910,111 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
         w0 = rgbw(y0, b0, r0);
         w1 = rgbw(y1, b1, r1);
     };
-    // 1. colour + horizontal pass, one source row per wave at a time
-    for (int rr = wave; rr < rows; rr += 4) {
-        const int y = r.y0 + lo + rr;
-        RowTap tp[3];
+    // 1. colour + horizontal pass, two source rows per wave at a time (no block barrier): the
+    //    colour items of both rows are one flat range of pixel pairs (a lone 168-px row is 84 pairs,
+    //    2 of 64-lane steps at 66 % use; two rows are 3 steps at 88 %), then the two rows' filter
+    //    outputs.  A pair (2p, 2p + 1) of an odd width's last column computes a pixel past the row
+    //    (its samples clamped in the plane copy's padding) and does not store it.
+#if defined(RC_GEMM_ABLATION)
+    const int skip = g_band_skip;
+#else
+    constexpr int skip = 0;
+#endif
+    const int npair = (W + 1) >> 1, RW = (W + 1) & ~1;
+    for (int r0 = 2 * wave; r0 < rows; r0 += 8) {
+        const int nr = min(2, rows - r0);
+        RowTap ta[3], tb[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-            if (c < d.ncomp) tp[c] = row_tap(c, y);
-        uint8_t *trow = tmp + rr * TP;
-        // pixel pairs (2p, 2p + 1); an odd width's last pair computes a pixel past the row (its
-        // samples clamped in the plane copy's padding) and does not store it
-        const int npair = (W + 1) >> 1;
-        if (!r.need_h) {  // the width already is S: the colour row is the pass's output
-            for (int p = lane; p < npair; p += 64) {
+            if (c < d.ncomp) {
+                ta[c] = row_tap(c, r.y0 + lo + r0);
+                tb[c] = row_tap(c, r.y0 + lo + r0 + nr - 1);
+            }
+        // the item's row taps: the two rows differ only in their row offsets and rounding
+        auto taps_of = [&](bool second, RowTap (&t)[3]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                t[c] = ta[c];
+                t[c].bn = second ? tb[c].bn : ta[c].bn;
+                t[c].bf = second ? tb[c].bf : ta[c].bf;
+                t[c].rnd = second ? tb[c].rnd : ta[c].rnd;
+            }
+        };
+        const int nitems = nr * npair;
+        if (!r.need_h) {  // the width already is S: the colour rows are the pass's output
+            for (int it = lane; it < nitems; it += 64) {
+                const bool second = it >= npair;
+                const int p = second ? it - npair : it;
+                RowTap t[3];
+                taps_of(second, t);
                 uint32_t w[2];
-                pair_rgb(tp, p, w[0], w[1]);
+                pair_rgb(t, p, w[0], w[1]);
+                uint8_t *trow = tmp + (r0 + (second ? 1 : 0)) * TP;
                 for (int e = 0; e < 2 && 2 * p + e < W; ++e)
-                    for (int b = 0; b < 3; ++b) trow[3 * (2 * p + e) + b] = (uint8_t)(w[e] >> (8 * b));
+                    for (int bb = 0; bb < 3; ++bb) trow[3 * (2 * p + e) + bb] = (uint8_t)(w[e] >> (8 * bb));
             }
             continue;
         }
-#if defined(RC_GEMM_ABLATION)
-        const int skip = g_band_skip;
-#else
-        constexpr int skip = 0;
-#endif
 #pragma unroll 1
-        for (int p = lane; p < npair; p += 64) {
+        for (int it = lane; it < nitems; it += 64) {
+            const bool second = it >= npair;
+            const int p = second ? it - npair : it;
             uint32_t w0 = p, w1 = p;
-            if (!(skip & 1)) pair_rgb(tp, p, w0, w1);
-            if (2 * p + 1 < W) *reinterpret_cast<uint2 *>(rowbuf + 2 * p) = make_uint2(w0, w1);
-            else rowbuf[2 * p] = w0;
+            if (!(skip & 1)) {
+                RowTap t[3];
+                taps_of(second, t);
+                pair_rgb(t, p, w0, w1);
+            }
+            uint32_t *rb = rowbuf + (second ? RW : 0) + 2 * p;
+            if (2 * p + 1 < W) *reinterpret_cast<uint2 *>(rb) = make_uint2(w0, w1);
+            else rb[0] = w0;
         }
-        // the row buffer is this wave's alone and LDS executes a wave's accesses in order: no
+        // the row buffers are this wave's alone and LDS executes a wave's accesses in order: no
         // barrier, only no compiler reordering across this point
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (skip & 2) {
-        } else if constexpr (MAXT > 0) {
+        for (int j = 0; j < nr; ++j) {
+            const uint32_t *rbuf = rowbuf + j * RW;
+            uint8_t *trow = tmp + (r0 + j) * TP;
+            if (skip & 2) {
+            } else if constexpr (MAXT > 0) {
 #pragma unroll
-            for (int t = 0; t < BAND_NXO; ++t) {
-                const int xo = lane + 64 * t;
-                if (xo < S) {
+                for (int t = 0; t < BAND_NXO; ++t) {
+                    const int xo = lane + 64 * t;
+                    if (xo < S) {
+                        int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+#pragma unroll
+                        for (int k = 0; k < MAXT; ++k) {
+                            const uint32_t w = rbuf[px[t][k]];
+                            a0 += (int)(w & 255u) * cf[t][k];
+                            a1 += (int)((w >> 8) & 255u) * cf[t][k];
+                            a2 += (int)(w >> 16) * cf[t][k];
+                        }
+                        trow[3 * xo] = clip8_22(a0);
+                        trow[3 * xo + 1] = clip8_22(a1);
+                        trow[3 * xo + 2] = clip8_22(a2);
+                    }
+                }
+            } else {
+                for (int xo = lane; xo < S; xo += 64) {
+                    const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
+                    const int *c = r.hc + xo * r.hk;
                     int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-#pragma unroll
-                    for (int k = 0; k < MAXT; ++k) {
-                        const uint32_t w = rowbuf[px[t][k]];
-                        a0 += (int)(w & 255u) * cf[t][k];
-                        a1 += (int)((w >> 8) & 255u) * cf[t][k];
-                        a2 += (int)(w >> 16) * cf[t][k];
+                    for (int k = 0; k < xn; ++k) {
+                        const uint32_t w = rbuf[xmin + k];
+                        const int ck = c[k];
+                        a0 += (int)(w & 255u) * ck;
+                        a1 += (int)((w >> 8) & 255u) * ck;
+                        a2 += (int)(w >> 16) * ck;
                     }
                     trow[3 * xo] = clip8_22(a0);
                     trow[3 * xo + 1] = clip8_22(a1);
                     trow[3 * xo + 2] = clip8_22(a2);
                 }
             }
-        } else {
-            for (int xo = lane; xo < S; xo += 64) {
-                const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
-                const int *c = r.hc + xo * r.hk;
-                int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-                for (int k = 0; k < xn; ++k) {
-                    const uint32_t w = rowbuf[xmin + k];
-                    const int ck = c[k];
-                    a0 += (int)(w & 255u) * ck;
-                    a1 += (int)((w >> 8) & 255u) * ck;
-                    a2 += (int)(w >> 16) * ck;
-                }
-                trow[3 * xo] = clip8_22(a0);
-                trow[3 * xo + 1] = clip8_22(a1);
-                trow[3 * xo + 2] = clip8_22(a2);
-            }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // the next row rewrites the row buffer
+        __builtin_amdgcn_wave_barrier();  // the next rows rewrite the row buffers
     }
     __syncthreads();
     // 2. vertical pass (or, without one, the rows as they are), one output row per wave at a time
@@ -1005,6 +1042,39 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
         const int yn = r.vb[2 * yo + 1];
 #endif
         const int *c = r.vc + yo * r.vk;
+        auto store = [&](int cw, int a0, int a1, int a2, int a3) __attribute__((always_inline)) {
+            const uint32_t v = (uint32_t)clip8_22(a0) | ((uint32_t)clip8_22(a1) << 8) | ((uint32_t)clip8_22(a2) << 16) |
+                               ((uint32_t)clip8_22(a3) << 24);
+            if (words) *reinterpret_cast<uint32_t *>(grow + 4 * cw) = v;
+            else
+                for (int b = 0; b < 4; ++b)
+                    if (4 * cw + b < rowbytes) grow[4 * cw + b] = (uint8_t)(v >> (8 * b));
+        };
+        if (r.vk <= BAND_MAXV) {
+            // the row's taps as wave-uniform constants loaded once (the table is padded by
+            // BAND_MAXV entries: reads past the row's vk are in bounds), zero past yn, row offsets
+            // clamped into the band — not one scalar load per tap per 4-byte column
+            int cv[BAND_MAXV], ro[BAND_MAXV];
+#pragma unroll
+            for (int k = 0; k < BAND_MAXV; ++k) {
+                cv[k] = k < yn ? c[k] : 0;
+                ro[k] = min(ymin + k, rows - 1) * nw;
+            }
+            for (int cw = lane; cw < nw; cw += 64) {
+                int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
+#pragma unroll
+                for (int k = 0; k < BAND_MAXV; ++k) {
+                    if (k >= r.vk) break;  // uniform: 5 or 7 taps for the usual scales
+                    const uint32_t w = t32[ro[k] + cw];
+                    a0 += (int)(w & 255u) * cv[k];
+                    a1 += (int)((w >> 8) & 255u) * cv[k];
+                    a2 += (int)((w >> 16) & 255u) * cv[k];
+                    a3 += (int)(w >> 24) * cv[k];
+                }
+                store(cw, a0, a1, a2, a3);
+            }
+            continue;
+        }
         for (int cw = lane; cw < nw; cw += 64) {
             const uint32_t *q = t32 + ymin * nw + cw;
             int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
@@ -1016,12 +1086,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                 a2 += (int)((w >> 16) & 255u) * ck;
                 a3 += (int)(w >> 24) * ck;
             }
-            const uint32_t v = (uint32_t)clip8_22(a0) | ((uint32_t)clip8_22(a1) << 8) | ((uint32_t)clip8_22(a2) << 16) |
-                               ((uint32_t)clip8_22(a3) << 24);
-            if (words) *reinterpret_cast<uint32_t *>(grow + 4 * cw) = v;
-            else
-                for (int b = 0; b < 4; ++b)
-                    if (4 * cw + b < rowbytes) grow[4 * cw + b] = (uint8_t)(v >> (8 * b));
+            store(cw, a0, a1, a2, a3);
         }
     }
 }
@@ -1265,6 +1330,8 @@ const rc_jpeg_decoder::Coeffs &resize_coeffs(rc_jpeg_decoder *h, int in_size, in
     d.hbounds = c.bounds;
     d.bounds = (int *)dmalloc(c.bounds.size() * sizeof(int));
     try {
+        // padded by BAND_MAXV zeros: the band kernel reads a row's first BAND_MAXV taps unguarded
+        c.coef.resize(c.coef.size() + jpeg::BAND_MAXV, 0);
         d.coef = (int *)dmalloc(c.coef.size() * sizeof(int));
         RC_HIP(hipMemcpy(d.bounds, c.bounds.data(), c.bounds.size() * sizeof(int), hipMemcpyHostToDevice));
         RC_HIP(hipMemcpy(d.coef, c.coef.data(), c.coef.size() * sizeof(int), hipMemcpyHostToDevice));

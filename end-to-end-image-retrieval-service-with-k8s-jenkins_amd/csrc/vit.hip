@@ -345,14 +345,15 @@ const uint8_t *resize_batch(rc_model *m, const uint8_t *images, int n, int h, in
 
 #if defined(RC_GEMM_ABLATION)
 // Diagnostic builds: the A/B kernel for a full-batch projection.  The residual producers
-// (O-proj, fc2; auto = image-aligned tiles) take GEMM_PINGPONG / GEMM_W2 / GEMM_PP_IMG;
+// (O-proj, fc2; auto = two-workgroup / ping-pong) take GEMM_PINGPONG / GEMM_W2 / GEMM_PP_IMG;
 // ping-pong ablations (100 + ABL) apply where auto picks the 256-row ping-pong kernel.
 int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_epilogue) {
     if (variant == GEMM_AUTO) return variant;
     const int pick = gemm_pick(a, GEMM_AUTO, patch_epilogue, ln_epilogue);
-    if (pick == GEMM_PP_IMG && (variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG)) return variant;
-    if (pick == GEMM_PP_IMG && variant == 11) return a.K <= 768 ? GEMM_W2 : GEMM_PP_IMG;  // O-proj two-workgroup, fc2 image-aligned
-    if (pick == GEMM_PP_IMG && variant == 12) return a.K <= 768 ? GEMM_W2 : GEMM_PINGPONG;  // the round-4 product
+    const bool producer = a.row_step > 0 && pick != GEMM_SKINNY;  // O-proj / fc2 of a full batch
+    if (producer && (variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG)) return variant;
+    if (producer && variant == 11) return a.K <= 768 ? GEMM_W2 : GEMM_PP_IMG;  // O-proj two-workgroup, fc2 image-aligned
+    if (producer && variant == 12) return a.K <= 768 ? GEMM_W2 : GEMM_PINGPONG;  // = auto (rounds 4 and 5)
     if (pick == GEMM_PINGPONG && variant >= 100 && variant < 200) return variant;
     return GEMM_AUTO;
 }
@@ -516,6 +517,8 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
         }
         const int ta = m->timers[T_ATTN].begin(s);
         const int items = n * c.heads;
+        // fewer items than CUs: each item's query tiles split over 4 blocks (a lone image: 48 blocks)
+        const int qsplit = items < m->ncu ? 4 : 1;
 #if defined(RC_GEMM_ABLATION)
         if (m->attn_form == 3) {  // persistent: two blocks per CU walk the (image, head) items
             const int nb = std::min(items, 2 * m->ncu);
@@ -523,8 +526,6 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
                                scale * 1.4426950408889634f);
         } else
 #endif
-        // fewer items than CUs: each item's query tiles split over 4 blocks (a lone image: 48 blocks)
-        const int qsplit = items < m->ncu ? 4 : 1;
         if (T == 197) {
             hipLaunchKernelGGL(attention_v2_kernel<197>, dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f, qsplit);
@@ -536,7 +537,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
         m->timers[T_ATTN].end(ta, s, 4.0 * n * c.heads * (double)T * T * (H / c.heads));
         {
             GemmArgs o = produce(GemmArgs{attn, L.w_o, L.b_o, M, H, H, nullptr, hidden, nullptr, T}, true);
-            o.row_step = T;  // image-aligned tiles (gemm_pp_kernel<.., 224>)
+            o.row_step = T;  // rows per image (diagnostic builds: image-aligned tiles, gemm_pp_kernel<.., 224>)
             resid_gemm(m, o, s, T_OPROJ);
         }
         if (fold) {
@@ -910,8 +911,12 @@ extern "C" int rc_gemm_bf16(int epi, int variant, const uint16_t *A, const uint1
         RC_REQUIRE(A && W && bias && out && M > 0 && N > 0 && K > 0, RC_ERR_INVALID, "bad GEMM arguments");
         GemmArgs a{A, W, bias, M, N, K, (uint16_t *)out, (float *)out, pos, tokens};
         if (variant == GEMM_PP_IMG) {  // image-aligned tiles: `tokens` rows per image (residual epilogue)
+#if defined(RC_GEMM_ABLATION)
             RC_REQUIRE(epi == EPI_RESID_F32 && tokens > 0, RC_ERR_INVALID, "variant 10: epi 2 and tokens (rows per image)");
             a.row_step = tokens;
+#else
+            throw Error(RC_ERR_UNSUPPORTED, "variant 10 (image-aligned tiles) is a diagnostic-build kernel");
+#endif
         }
         hipStream_t s = (hipStream_t)stream;
         switch (epi) {

@@ -145,10 +145,22 @@ def embed_many(blobs: List[bytes]) -> list[list[float]]:
     """Image bytes → raw CLS vectors: GPU JPEG decode where it applies, PIL otherwise.  Each
     vector is a list of Python floats (the /embed body) that also carries its float32 row
     (``index.F32List``), for in-process callers that hand it straight to ``index.query``."""
+    import torch
+
     from ..index import F32List
 
-    raw, _ = embed_many_device(blobs)
-    a = raw.cpu().numpy()
+    emb = get_embedder()
+    if len(blobs) == 1 and not hasattr(emb, "assign_by_location"):
+        # the /embed request: the final kernel writes the vector straight into pinned host memory
+        # (no D2H copy), then one stream sync
+        images = decode_many(blobs)
+        host = torch.empty((1, emb.hidden), dtype=torch.float32, pin_memory=True)
+        emb.embed_images(images, out=(host, None))
+        torch.cuda.current_stream(emb.device).synchronize()
+        a = host.numpy()
+    else:
+        raw, _ = embed_many_device(blobs)
+        a = raw.cpu().numpy()
     return [F32List(row.tolist(), row) for row in a]
 
 

@@ -239,12 +239,17 @@ class VitMsnEmbedder:
         check(self.lib.rc_preprocess(self._h, ptr(x), n, h, w, ptr(out), stream_ptr(stream)))
         return out
 
-    def embed_images(self, images: Sequence, normalized: bool = False):
+    def embed_images(self, images: Sequence, normalized: bool = False, out=None):
         """u8 HWC RGB images of any sizes (device tensors or host arrays) → (raw [n,H], normed [n,H]
-        or None) f32 device tensors in input order; equal-size images share ``rc_embed`` batches."""
+        or None) f32 device tensors in input order; equal-size images share ``rc_embed`` batches.
+        ``out``: caller-owned (raw, normed or None) — device tensors, or for a single image pinned
+        host tensors the kernels write straight into (no D2H copy; the caller synchronises)."""
         n = len(images)
-        raw = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device)
-        nrm = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device) if normalized else None
+        if out is not None:
+            raw, nrm = out
+        else:
+            raw = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device)
+            nrm = torch.empty((n, self.hidden), dtype=torch.float32, device=self.device) if normalized else None
         groups: dict[tuple[int, int], list[int]] = {}
         for i, im in enumerate(images):
             groups.setdefault((int(im.shape[0]), int(im.shape[1])), []).append(i)

@@ -298,10 +298,10 @@ def test_from_pretrained_v5_layout_matches_golden(vitmod, cuda, tmp_path):
 
 
 def test_image_aligned_tiles_batch_invariant(vitmod, weights12, cuda):
-    """O-proj and fc2 run on image-aligned 224-row tiles (tile t = the rows of image t), the other
-    projections on 256-row tiles and a lone image on the skinny kernels: every kernel accumulates
-    K in the same order, so an image's 12-layer embedding is the same bits whatever batch, slice
-    or tile it lands in — a batch of 300 in one or two slices, three batches of 100, single images."""
+    """Full batches run the 256-row ping-pong and the two-workgroup 128-row tiles (image rows at any
+    position in a tile), a lone image the skinny kernels: every kernel accumulates K in the same
+    order, so an image's 12-layer embedding is the same bits whatever batch, slice or tile it lands
+    in — a batch of 300 in one or two slices, three batches of 100, single images."""
     import torch
 
     rng = np.random.default_rng(21)

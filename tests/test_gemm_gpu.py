@@ -84,10 +84,20 @@ def test_patch_epilogue_scatter(cuda, variant):
 
 @pytest.mark.parametrize("M,K", [(5 * 197, 768), (5 * 197 + 50, 3072), (2 * 197, 768), (197 + 1, 3072)])
 def test_image_aligned_tiles_match_torch_fp32(cuda, M, K):
-    """Variant 10 (the model's O-proj / fc2 kernel): 224-row tiles, tile t = rows [197 t, 197 t + 197),
-    f32 residual epilogue; a ragged last image (M not a multiple of 197) and rows >= M untouched.
-    The A buffer holds 224 - 197 rows past the last tile's start (the model pads 256)."""
+    """Variant 10 (diagnostic builds; it lost the in-model A/B at parts = 2): 224-row tiles, tile t =
+    rows [197 t, 197 t + 197), f32 residual epilogue; a ragged last image (M not a multiple of 197)
+    and rows >= M untouched.  The A buffer holds 224 - 197 rows past the last tile's start (the
+    model pads 256).  The product library refuses the variant."""
     import torch
+
+    L = import_pkg("_lib")
+    lib = L.load()
+    if getattr(lib, "rc_diag_set_gemm_variant", None) is None:  # the product build
+        dummy = torch.zeros(256, 768, dtype=torch.bfloat16, device=cuda)
+        rc = lib.rc_gemm_bf16(EPI_RESID, 10, dummy.data_ptr(), dummy.data_ptr(), dummy.data_ptr(), 197, 768, 768,
+                              dummy.data_ptr(), None, 197, torch.cuda.current_stream().cuda_stream)
+        assert rc != 0 and b"diagnostic" in lib.rc_last_error()
+        return
 
     N, T = 768, 197
     g = torch.Generator(device=cuda).manual_seed(M + K)
@@ -99,8 +109,7 @@ def test_image_aligned_tiles_match_torch_fp32(cuda, M, K):
     ref = A[:M].float() @ W.float().T + bias
     resid = torch.randn(Mp, N, device=cuda, generator=g)
     out = resid.clone()
-    L = import_pkg("_lib")
-    L.check(L.load().rc_gemm_bf16(EPI_RESID, 10, A.data_ptr(), W.data_ptr(), bias.data_ptr(), M, N, K, out.data_ptr(),
+    L.check(lib.rc_gemm_bf16(EPI_RESID, 10, A.data_ptr(), W.data_ptr(), bias.data_ptr(), M, N, K, out.data_ptr(),
                                   None, T, torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     assert torch.allclose(out[:M], resid[:M] + ref, atol=1e-4, rtol=1e-4)

@@ -19,17 +19,18 @@ __global__ __launch_bounds__(256, 4) void stream_kernel(const float *__restrict_
 #pragma unroll
         for (int e = 0; e < 4; ++e) qr[i][e] = q[(sub + 16 * i) * 4 + e];
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(n_rows, r0 + rows_per_block);
-    const float4 *b4 = reinterpret_cast<const float4 *>(rows);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v *b4 = reinterpret_cast<const f4v *>(rows);
     float best = -1e30f;
     for (int64_t g = r0 + wave * 4 * U; g < r1; g += 16 * U) {
-        float4 x[U][CPL];
+        f4v x[U][CPL];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t r = g + u * 4 + rg;
             const int64_t rr = r < r1 ? r : r0;
 #pragma unroll
             for (int i = 0; i < CPL; ++i) {
-                const float4 *p = b4 + rr * 128 + sub + 16 * i;
+                const f4v *p = b4 + rr * 128 + sub + 16 * i;
                 if constexpr (NT) x[u][i] = __builtin_nontemporal_load(p);
                 else x[u][i] = *p;
             }
