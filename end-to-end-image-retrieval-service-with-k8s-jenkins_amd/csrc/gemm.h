@@ -968,6 +968,85 @@ __device__ __forceinline__ void skinny_chain_t(const uint16_t *Ar, const uint16_
         }
     }
 }
+// The skinny K chain through an LDS-DMA ring (K = 768 / 3072): per 64-deep K block the wave copies
+// its 16 A rows and 16·NI W rows, 128 B each, with global_load_lds_dwordx4 — 8 whole rows per
+// instruction (8 full 128-B lines) where the register form's fragment loads touch 16 rows × 64 B
+// (16 half lines) per instruction: the loads are address-bound (PMC), the bytes are not.  Rows
+// are 128 B in LDS with the 16-B chunk XOR-swizzled by (row >> 1) & 7 on the source address
+// (conflict-free ds_read_b128 fragments, as the tiled kernels).  The ring is SK stages deep (the
+// copy of block kb + SK − 1 issued while block kb is consumed); one wave per ring, no barrier: a
+// counted vmcnt says a block has landed, and its fragments are read with inline-asm ds_reads (as
+// C++ loads hipcc would wait for the whole DMA ring first).  The MFMAs run in the same k order as
+// every other kernel: the same bits.
+constexpr int SKINNY_DMA_STAGES = 6;
+template <int NI>
+constexpr int skinny_dma_stage_bytes() { return (16 + 16 * NI) * 128; }
+
+template <int NI, int NKB>
+__device__ __forceinline__ void skinny_chain_dma(const uint16_t *__restrict__ A, int row_a0, int M, const uint16_t *__restrict__ W,
+                                                 int n0, int K, uint8_t *ring, f32x4 (&acc)[NI]) {
+    constexpr int SK = SKINNY_DMA_STAGES, SB = skinny_dma_stage_bytes<NI>(), NA = 2, NW = 2 * NI, NP = NA + NW;
+    static_assert(NKB >= SK, "the ring is primed with SK - 1 blocks");
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    // copy sources: instruction i (A: i < 2, W: i >= 2) moves rows 8(i mod ..) + lane / 8, chunk lane % 8
+    const uint16_t *src[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int r = (i < NA ? i : i - NA) * 8 + (lane >> 3);  // row within the A or W block
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const uint16_t *rowp = i < NA ? A + (int64_t)min(row_a0 + r, M - 1) * K : W + (int64_t)(n0 + r) * K;
+        src[i] = rowp + c * 8;
+    }
+    auto issue = [&](int kb) __attribute__((always_inline)) {
+        uint8_t *st = ring + (kb % SK) * SB;
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + kb * 64), (lds_void_t *)(st + i * 1024), 16, 0, 0);
+    };
+    // fragment addresses within a stage: A row li, W row 16 ni + li; logical chunk 4 s + g
+    uint32_t fa[2], fw[2][NI];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const int c = (4 * s2 + g) ^ ((li >> 1) & 7);
+        fa[s2] = (uint32_t)(li * 128 + c * 16);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) fw[s2][ni] = (uint32_t)((16 + 16 * ni + li) * 128 + c * 16);
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < SK - 1; ++kb) issue(kb);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        // block kb landed: younger copies in flight are those of blocks kb + 1 .. min(kb + SK - 2, NKB - 1)
+        constexpr int X = NP;
+        const int younger = min(SK - 2, NKB - 1 - kb);
+        if (younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * X) : "memory");
+        else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * X) : "memory");
+        else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * X) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t st = (uint32_t)(uintptr_t)(ring + (kb % SK) * SB);
+        bf16x8 a[2], w[2][NI];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            asm volatile("ds_read_b128 %0, %1" : "=v"(a[s2]) : "v"(st + fa[s2]));
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) asm volatile("ds_read_b128 %0, %1" : "=v"(w[s2][ni]) : "v"(st + fw[s2][ni]));
+        }
+        static_assert(NI == 2, "the wait below ties 2 + 4 fragments");
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1]));
+        // the stage block kb - 1 used is free (its reads retired a block ago): refill it
+        if (kb + SK - 1 < NKB) issue(kb + SK - 1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+                acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[s2][ni], a[s2], acc[ni], 0, 0, 0);
+    }
+}
+
 // K (per chain) 768 / 3072: straight-line chains; otherwise the looped form (K % 64 == 0)
 template <int NI, int KT>
 __device__ __forceinline__ void skinny_chain(const uint16_t *Ar, const uint16_t *Wr, int K, int nk, f32x4 (&acc)[NI]) {
@@ -1003,10 +1082,15 @@ __global__ __launch_bounds__(64) void gemm_skinny_kernel(GemmArgs a) {
     if (w >= nct * nrt) return;
     const int ct = w / nrt, rt = w % nrt;
     const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
-    const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
-    const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
     f32x4 acc[NI];
-    skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
+    if constexpr (KT > 0) {
+        __shared__ __attribute__((aligned(16))) uint8_t ring[SKINNY_DMA_STAGES * skinny_dma_stage_bytes<NI>()];
+        skinny_chain_dma<NI, KT / 64>(a.A, rt * 16, a.M, a.W, n0, K, ring, acc);
+    } else {
+        const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
+        const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
+        skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
+    }
     if (row >= a.M) return;
     float2 lrs;  // LayerNorm fold: this row's (rstd, -rstd*mu), as gemm_pp_kernel computes it
     if constexpr (epi_ln(EPI)) lrs = ln_row_scale(a.ln_stats + (int64_t)row * LN_STRIDE, a.ln_eps);
@@ -1066,10 +1150,15 @@ __global__ __launch_bounds__(128) void gemm_skinny_ln_kernel(GemmArgs a) {
     const int nrt = (a.M + 15) / 16, lb = skinny_block(blockIdx.x, gridDim.x);
     const int blk = lb / nrt, rt = lb % nrt;  // column-block-major (skinny_block)
     const int K = a.K, n0 = blk * 64 + wave * 32, row = rt * 16 + li;
-    const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;
-    const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
     f32x4 acc[NI];
-    skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
+    if constexpr (KT > 0) {
+        __shared__ __attribute__((aligned(16))) uint8_t ring[2][SKINNY_DMA_STAGES * skinny_dma_stage_bytes<NI>()];
+        skinny_chain_dma<NI, KT / 64>(a.A, rt * 16, a.M, a.W, n0, K, ring[wave], acc);
+    } else {
+        const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;
+        const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
+        skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
+    }
     const bool valid = row < a.M;
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
