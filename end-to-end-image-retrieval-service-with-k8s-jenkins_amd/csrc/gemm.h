@@ -1292,6 +1292,143 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool l
 // it by 2 %).
 inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
 
+// The patch embedding of a small batch (M <= 256 patch rows, the bf16-pair stream: one image is
+// 196 rows, and patch_gemm_kernel's 128 x 256 tiles put it on 6 workgroups, 33 us): the skinny
+// form.  Block = 2 waves = one 16-row tile x one 64-column LayerNorm block (as
+// gemm_skinny_ln_kernel); wave w takes columns 32w..32w+31.  A fragments are built in registers
+// from the u8 images — lane (g, li), K-step s: patch row 16 rt + li, K = 32 s + 8 g .. + 7 in
+// (ky, kx, c) order, 8 bytes of one image row, each bf16(fma(u, pre_a[k mod 3], pre_b[k mod 3]))
+// exactly as patch_gemm_kernel converts them — and the W rows stream through the LDS-DMA ring;
+// the MFMAs run in the same K order (the same bits).  Epilogue: x = (acc + bias) + position
+// embedding at the patch's token row, stored as the bf16 pair, LN partials of the 64-column
+// block through LDS (f32_rows_epilogue's values and canonical slices).
+template <int EPI>
+__global__ __launch_bounds__(128) void patch_skinny_kernel(GemmArgs a) {
+    static_assert(EPI == EPI_PATCH_HL, "the bf16-pair stream");
+    constexpr int NI = 2, P = 16, KC = 3 * P * P, NKB = KC / 64, LP = 68;
+    constexpr int SK = SKINNY_DMA_STAGES, SB = 16 * NI * 128;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[2][SK * SB];
+    __shared__ float xs_l[16 * LP];
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15, wave = threadIdx.x >> 6;
+    const int nrt = (a.M + 15) / 16, lb = skinny_block(blockIdx.x, gridDim.x);
+    const int blk = lb / nrt, rt = lb % nrt;
+    const int n0 = blk * 64 + wave * 32, row = rt * 16 + li;
+    // this lane's patch row: 8 image bytes per K-step, all 24 steps loaded up front
+    const int S = a.img_size, gp = S / P, np = gp * gp;
+    const int m = min(row, a.M - 1);
+    const int b = m / np, pi = m - b * np, py = pi / gp, px = pi - py * gp;
+    const uint8_t *abase = a.img + (((int64_t)b * S + py * P) * S + px * P) * 3;
+    uint2 ab[2 * NKB];
+#pragma unroll
+    for (int st = 0; st < 2 * NKB; ++st) {
+        const int k0 = 32 * st + 8 * g, ky = k0 / (3 * P), off = k0 - ky * (3 * P);
+        ab[st] = *reinterpret_cast<const uint2 *>(abase + ky * S * 3 + off);
+    }
+    // every A fragment converted up front (24 x 16 B per lane; constant indices below)
+    const float pa[3] = {a.pre_a[0], a.pre_a[1], a.pre_a[2]}, pb[3] = {a.pre_b[0], a.pre_b[1], a.pre_b[2]};
+    bf16x8 af[2 * NKB];
+#pragma unroll
+    for (int st = 0; st < 2 * NKB; ++st) {
+        const int c0 = (32 * st + 8 * g) % 3;  // channel of byte 0 (k mod 3; 3P = 48 keeps rows aligned)
+        // the (a, b) pair of byte e is ((c0 + e) mod 3): rotate once, then constant indices
+        const float ra[3] = {c0 == 0 ? pa[0] : (c0 == 1 ? pa[1] : pa[2]), c0 == 0 ? pa[1] : (c0 == 1 ? pa[2] : pa[0]),
+                             c0 == 0 ? pa[2] : (c0 == 1 ? pa[0] : pa[1])};
+        const float rb[3] = {c0 == 0 ? pb[0] : (c0 == 1 ? pb[1] : pb[2]), c0 == 0 ? pb[1] : (c0 == 1 ? pb[2] : pb[0]),
+                             c0 == 0 ? pb[2] : (c0 == 1 ? pb[0] : pb[1])};
+        const uint32_t w[2] = {ab[st].x, ab[st].y};
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 2 * j;
+            const float uA = (float)((w[e >> 2] >> (8 * (e & 3))) & 0xffu);
+            const float uB = (float)((w[(e + 1) >> 2] >> (8 * ((e + 1) & 3))) & 0xffu);
+            o[j] = pack_bf16x2(fmaf(uA, ra[e % 3], rb[e % 3]), fmaf(uB, ra[(e + 1) % 3], rb[(e + 1) % 3]));
+        }
+        af[st] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+    }
+    // W rows n0 .. n0 + 31 by LDS-DMA (skinny_chain_dma's ring, without the A half)
+    uint8_t *rg = ring[wave];
+    const uint16_t *src[2 * NI];
+#pragma unroll
+    for (int i = 0; i < 2 * NI; ++i) {
+        const int r = i * 8 + (lane >> 3);
+        src[i] = a.W + (int64_t)(n0 + r) * KC + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+    }
+    auto issue = [&](int kb) __attribute__((always_inline)) {
+        uint8_t *stg = rg + (kb % SK) * SB;
+#pragma unroll
+        for (int i = 0; i < 2 * NI; ++i)
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + kb * 64), (lds_void_t *)(stg + i * 1024), 16, 0, 0);
+    };
+    uint32_t fw[2][NI];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) fw[s2][ni] = (uint32_t)((16 * ni + li) * 128 + (((4 * s2 + g) ^ ((li >> 1) & 7)) * 16));
+    f32x4 acc[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the image bytes (older than every DMA below)
+#pragma unroll
+    for (int kb = 0; kb < SK - 1; ++kb) issue(kb);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        constexpr int X = 2 * NI;
+        const int younger = min(SK - 2, NKB - 1 - kb);
+        if (younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * X) : "memory");
+        else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * X) : "memory");
+        else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * X) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t st = (uint32_t)(uintptr_t)(rg + (kb % SK) * SB);
+        bf16x8 w[2][NI];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) asm volatile("ds_read_b128 %0, %1" : "=v"(w[s2][ni]) : "v"(st + fw[s2][ni]));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1]));
+        if (kb + SK - 1 < NKB) issue(kb + SK - 1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+                acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[s2][ni], af[2 * kb + s2], acc[ni], 0, 0, 0);
+    }
+    // epilogue: f32_rows_epilogue's values, per element
+    const bool valid = row < a.M;
+    const int img = m / np, p = m - img * np;
+    const int64_t orow = (int64_t)img * a.tokens + 1 + p;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+        const int c = n0 + ni * 16 + 4 * g;
+        const float4 bb = *reinterpret_cast<const float4 *>(a.bias + c);
+        const float4 ps = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + c);
+        const float4 xf = make_float4((acc[ni][0] + bb.x) + ps.x, (acc[ni][1] + bb.y) + ps.y, (acc[ni][2] + bb.z) + ps.z,
+                                      (acc[ni][3] + bb.w) + ps.w);
+        const uint4 pr = hl_split(xf);
+        if (valid) hl_store(pr, a.ln_x + orow * a.N + c, a.res_lo + orow * a.N + c);
+        *reinterpret_cast<float4 *>(xs_l + li * LP + wave * 32 + ni * 16 + 4 * g) = hl_value(pr);
+    }
+    if (a.ln_stats == nullptr) return;  // block-uniform
+    __syncthreads();
+    if (wave != 0) return;
+    const int r = lane >> 2, sg = lane & 3;
+    float xs[16];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+        const float *q = xs_l + r * LP + ln_slice_col(sg, cc);
+        const float4 u = *reinterpret_cast<const float4 *>(q), v = *reinterpret_cast<const float4 *>(q + 4);
+        xs[8 * cc] = u.x, xs[8 * cc + 1] = u.y, xs[8 * cc + 2] = u.z, xs[8 * cc + 3] = u.w;
+        xs[8 * cc + 4] = v.x, xs[8 * cc + 5] = v.y, xs[8 * cc + 6] = v.z, xs[8 * cc + 7] = v.w;
+    }
+    const float2 stt = ln_block_reduce_quad(ln_slice_stats(xs), sg);
+    const int srow = rt * 16 + r;
+    if (sg == 0 && srow < a.M) {
+        const int sm = srow, simg = sm / np, sp = sm - simg * np;
+        *reinterpret_cast<float2 *>(a.ln_stats + ((int64_t)simg * a.tokens + 1 + sp) * LN_STRIDE + 2 * blk) = stt;
+    }
+}
+
 // Implicit-GEMM patch embedding: M = images × patches rows, N = hidden, K = 3·P² (P = 16)
 inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
     RC_REQUIRE(a.img && a.img_size % 16 == 0 && a.N % 256 == 0 && a.K == 3 * 16 * 16 && a.M >= 1,
@@ -1299,7 +1436,10 @@ inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
     const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
     if (a.res_lo != nullptr) {
         RC_REQUIRE(a.ln_x != nullptr, RC_ERR_INVALID, "bf16-pair residual stream needs ln_x");
-        hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_HL>), dim3(ntm * ntn), dim3(256), 0, s, a);
+        if (a.M <= 256 && a.N == 64 * LN_PARTS)  // a small batch: the skinny form (same bits)
+            hipLaunchKernelGGL((patch_skinny_kernel<EPI_PATCH_HL>), dim3(((a.M + 15) / 16) * LN_PARTS), dim3(128), 0, s, a);
+        else
+            hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_HL>), dim3(ntm * ntn), dim3(256), 0, s, a);
     } else {
         hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_F32>), dim3(ntm * ntn), dim3(256), 0, s, a);
     }

@@ -14,7 +14,7 @@ fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python -u bench.py --no-cpu --no-latency --steps 5 --warmup 2 --parts 1 --ingest-images 32768 > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
 find gpurun_out/prof_$TAG -name '*kernel_trace.csv' -delete
-bash tools/pmc_collect.sh gpurun_out/pmc_$TAG -- python -u bench.py --no-cpu --no-latency --ingest-images 0 --jpeg-images 0 --steps 2 --warmup 1 --batch-reps 1 --search-queries 4 --parts 1 || exit $?
+bash tools/pmc_collect.sh gpurun_out/pmc_$TAG -- python -u bench.py --no-cpu --no-latency --ingest-images 0 --jpeg-images 512 --steps 2 --warmup 1 --batch-reps 1 --search-queries 4 --parts 1 || exit $?
 python tools/pmc_summary.py gpurun_out/pmc_$TAG --json gpurun_out/pmc_$TAG/summary.json --latest gpurun_out/pmc_$TAG/pmc_latest.json > gpurun_out/pmc_$TAG/summary.txt
 echo "pmc summary rc=$?"
 rm -rf gpurun_out/pmc_$TAG/p[0-9]*/
