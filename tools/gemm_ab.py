@@ -1,6 +1,6 @@
 """Interleaved A/B of the full-batch projection GEMM kernels inside the real embed (one process).
 
-For each round and each variant: rc_model_set_gemm_variant, then (a) `steps` timed embeds of a
+For each round and each variant: rc_diag_set_gemm_variant (diagnostic build, RC_LIB_PATH), then (a) `steps` timed embeds of a
 batch-256 at the bench's --parts (whole-step wall time) and (b) per-GEMM HIP-event timings on
 the unsplit batch.  Prints one JSON line per round and a summary (median over rounds).
     python tools/gemm_ab.py [VARIANTS=4,5,6] [ROUNDS=5] [STEPS=10] [ROLES=qkv,oproj,fc1,fc2]
