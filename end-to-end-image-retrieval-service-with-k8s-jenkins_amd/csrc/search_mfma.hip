@@ -939,6 +939,9 @@ int batch_stage_ratio(int k, int cap, int inflation) {
 // stage filters the next g-times-larger row range against the running thresholds, then
 // rescore_kernel merges its candidates.  filter(c0, c1, nchunk) enqueues one filter
 // dispatch over rows [c0, c1) split into nchunk row chunks.
+#if defined(RC_GEMM_ABLATION)
+int g_diag_filter_split_log2 = 31;
+#endif
 template <typename T, typename F>
 void run_stages(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer, int g, int64_t row_bytes, F &&filter) {
     const int nqb = (p.nq + SB_TILE - 1) / SB_TILE;
@@ -952,7 +955,12 @@ void run_stages(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *tim
     // progress drifts apart by more than the L2 holds (memory-side reads 2.8x the rows
     // at 125M rows).  Sub-launches of <= 2 GB of rows realign them: reads fall to 1.05x
     // and the filter runs 3-5 % faster (profiles/r02/r02_ab_results.txt).
-    const int64_t split = nqb > 1 ? std::max<int64_t>(SB_TILE, ((int64_t)1 << 31) / row_bytes / SB_TILE * SB_TILE)
+#if defined(RC_GEMM_ABLATION)
+    const int split_log2 = g_diag_filter_split_log2;  // diagnostic builds: the sub-launch size A/B
+#else
+    constexpr int split_log2 = 31;
+#endif
+    const int64_t split = nqb > 1 ? std::max<int64_t>(SB_TILE, ((int64_t)1 << split_log2) / row_bytes / SB_TILE * SB_TILE)
                                   : (int64_t)0;
     while (b0 < p.n_rows) {
         for (int64_t c0 = b0; c0 < b1;) {
@@ -1093,3 +1101,13 @@ void BatchWs::release() {
 }
 
 }  // namespace rc
+
+#if defined(RC_GEMM_ABLATION)
+// diagnostic builds: log2 of the bytes of rows per filter sub-launch (31 = the product's 2 GB)
+extern "C" int rc_diag_set_filter_split(int log2_bytes) {
+    return rc::guard([&] {
+        RC_REQUIRE(log2_bytes >= 24 && log2_bytes <= 40, RC_ERR_INVALID, "log2 bytes in [24, 40]");
+        rc::g_diag_filter_split_log2 = log2_bytes;
+    });
+}
+#endif

@@ -1,0 +1,42 @@
+"""Interleaved A/B of the int8 filter's sub-launch size (diagnostic build: rc_diag_set_filter_split,
+log2 bytes of int8 rows per launch; 31 = the product's 2 GB) on the config-4 shard
+(125M x 512 fp16 + int8 copy, 1024 queries, top-100).  Prints median ms per batch per setting
+and checks every setting returns the same rows."""
+import importlib
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+L = importlib.import_module("end-to-end-image-retrieval-service-with-k8s-jenkins_amd._lib")
+index = importlib.import_module("end-to-end-image-retrieval-service-with-k8s-jenkins_amd.index")
+lib = L.load()
+settings = [int(v) for v in os.environ.get("SPLITS", "31,30,32,33").split(",")]
+rounds = int(os.environ.get("ROUNDS", "4"))
+rows = int(os.environ.get("ROWS", "125000000"))
+d = index.DeviceIndex(512, dtype="float16", capacity=rows, device=0)
+d.fill_random(4, 0, rows)
+d.set_filter("i8")
+q = torch.randn((1024, 512), device="cuda", generator=torch.Generator(device="cuda").manual_seed(6))
+res = {v: [] for v in settings}
+ref = None
+for r in range(rounds):
+    for v in settings:
+        assert lib.rc_diag_set_filter_split(v) == 0
+        d.search(q, 100, rows, mode="mfma")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = d.search(q, 100, rows, mode="mfma")
+        torch.cuda.synchronize()
+        res[v].append((time.perf_counter() - t0) * 1e3)
+        if ref is None:
+            ref = out[1].clone()
+        assert torch.equal(out[1], ref), v
+    print(json.dumps({"round": r, **{str(v): round(res[v][-1], 2) for v in settings}}), flush=True)
+assert lib.rc_diag_set_filter_split(31) == 0
+print(json.dumps({"median_ms_per_batch": {str(v): round(statistics.median(x), 2) for v, x in res.items()},
+                  "queries_per_s": {str(v): round(1024 / statistics.median(x) * 1e3) for v, x in res.items()}}))
