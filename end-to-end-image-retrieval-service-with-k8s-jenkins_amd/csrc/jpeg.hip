@@ -756,7 +756,8 @@ typedef __attribute__((address_space(3))) void jpeg_lds_void_t;
 
 #if defined(RC_GEMM_ABLATION)
 // diagnostic builds: phases of jpeg_band_resize_kernel to skip (1 colour, 2 horizontal, 4 vertical
-// math; the stores stay), for a per-phase time split (tools/jpeg_phase.py); wrong pixels
+// math, 8 the plane copy, 16 the vertical pass and its stores), for a per-phase time split
+// (tools/jpeg_phase.py); wrong pixels
 __device__ int g_band_skip = 0;
 #endif
 
@@ -801,6 +802,9 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
         if (c < d.ncomp) {
             const uint8_t *g = planes + (d.blk0[c] + (int64_t)pbr0[c] * d.bw[c]) * 64;
             const int n16 = pnbr[c] * d.bw[c] * 4;
+#if defined(RC_GEMM_ABLATION)
+            if (g_band_skip & 8) continue;
+#endif
             for (int i0 = wave * 64; i0 < n16; i0 += 256)
                 if (i0 + lane < n16)
                     __builtin_amdgcn_global_load_lds((const void *)(g + 16 * (i0 + lane)),
@@ -860,33 +864,47 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     auto col = [](int i) { return ((i >> 3) << 6) + (i & 7); };
     // the component's samples at the pixel pair (2p, 2p + 1): a fancy h2 pair shares its centre
     // column and reads one neighbour each side (3 column reads instead of 4, colsums once)
-    auto sample2 = [&](const RowTap &t, int p, int &v0, int &v1) {
+    // The column offsets of pair p, computed once for every component: c2 = the pair's first
+    // full-resolution column, cp / cl / cr = the h2 centre, left and right neighbour (clamped into
+    // the plane: component 1's width; component 2's when it differs)
+    struct PairCols {
+        int c2, cp, cl, cr1, cr2;
+    };
+    auto pair_cols = [&](int p, const RowTap *tp) {
+        PairCols pc;
+        pc.c2 = col(2 * p);
+        pc.cp = col(p);
+        pc.cl = col(max(p - 1, 0));
+        const int dwa = tp[d.ncomp > 1 ? 1 : 0].dw1, dwb = tp[d.ncomp > 2 ? 2 : 0].dw1;
+        pc.cr1 = col(min(p + 1, dwa));
+        pc.cr2 = dwb == dwa ? pc.cr1 : col(min(p + 1, dwb));  // (uniform branch)
+        return pc;
+    };
+    // component sample pair; bn / bf / rnd: this item's row (the wave's two rows differ only there)
+    auto sample2 = [&](const RowTap &t, int bn, int bf, int rnd, int p, const PairCols &pc, int cr, int &v0, int &v1) {
         if (t.kind == 0) {
             if (t.sx) {
-                v0 = v1 = (int)lds[t.bn + col(p)];
+                v0 = v1 = (int)lds[bn + pc.cp];
             } else {  // x = 2p is even: 2p and 2p + 1 are neighbours within one 8-sample block row
-                const int c0 = col(2 * p);
-                v0 = (int)lds[t.bn + c0];
-                v1 = (int)lds[t.bn + c0 + 1];
+                v0 = (int)lds[bn + pc.c2];
+                v1 = (int)lds[bn + pc.c2 + 1];
             }
             return;
         }
         if (t.kind == 1) {
-            const int c0 = col(2 * p);
-            v0 = (3 * (int)lds[t.bn + c0] + (int)lds[t.bf + c0] + t.rnd) >> 2;
-            v1 = (3 * (int)lds[t.bn + c0 + 1] + (int)lds[t.bf + c0 + 1] + t.rnd) >> 2;
+            v0 = (3 * (int)lds[bn + pc.c2] + (int)lds[bf + pc.c2] + rnd) >> 2;
+            v1 = (3 * (int)lds[bn + pc.c2 + 1] + (int)lds[bf + pc.c2 + 1] + rnd) >> 2;
             return;
         }
-        const int c0 = col(p), cl = col(max(p - 1, 0)), cr = col(min(p + 1, t.dw1));
         if (t.kind == 2) {
-            const int s0 = 3 * (int)lds[t.bn + c0];
-            v0 = (s0 + (int)lds[t.bn + cl] + 1) >> 2;
-            v1 = (s0 + (int)lds[t.bn + cr] + 2) >> 2;
+            const int s0 = 3 * (int)lds[bn + pc.cp];
+            v0 = (s0 + (int)lds[bn + pc.cl] + 1) >> 2;
+            v1 = (s0 + (int)lds[bn + cr] + 2) >> 2;
             return;
         }
-        const int cs0 = 3 * (3 * (int)lds[t.bn + c0] + (int)lds[t.bf + c0]);
-        const int csl = 3 * (int)lds[t.bn + cl] + (int)lds[t.bf + cl];
-        const int csr = 3 * (int)lds[t.bn + cr] + (int)lds[t.bf + cr];
+        const int cs0 = 3 * (3 * (int)lds[bn + pc.cp] + (int)lds[bf + pc.cp]);
+        const int csl = 3 * (int)lds[bn + pc.cl] + (int)lds[bf + pc.cl];
+        const int csr = 3 * (int)lds[bn + cr] + (int)lds[bf + cr];
         v0 = (cs0 + csl + 8) >> 4;
         v1 = (cs0 + csr + 7) >> 4;
     };
@@ -900,12 +918,22 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
         const int B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
         return (uint32_t)R | ((uint32_t)G << 8) | ((uint32_t)B << 16);
     };
-    auto pair_rgb = [&](const RowTap *tp, int p, uint32_t &w0, uint32_t &w1) {
-        int y0, y1, b0 = 0, b1 = 0, r0 = 0, r1 = 0;
-        sample2(tp[0], p, y0, y1);
+    // the pair of row ta (second = false) or tb; only the fields a kind reads are selected
+    auto pair_rgb = [&](const RowTap *ta, const RowTap *tb, bool second, int p, uint32_t &w0, uint32_t &w1) {
+        const PairCols pc = pair_cols(p, ta);
+        auto sel = [&](int c, int &bn, int &bf, int &rnd) __attribute__((always_inline)) {
+            bn = second ? tb[c].bn : ta[c].bn;
+            bf = ta[c].kind & 1 ? (second ? tb[c].bf : ta[c].bf) : 0;   // kinds 1 and 3 read the far row
+            rnd = ta[c].kind == 1 ? (second ? tb[c].rnd : ta[c].rnd) : 0;  // kind 1 rounds by row parity
+        };
+        int y0, y1, b0 = 0, b1 = 0, r0 = 0, r1 = 0, bn, bf, rnd;
+        sel(0, bn, bf, rnd);
+        sample2(ta[0], bn, bf, rnd, p, pc, pc.cr1, y0, y1);
         if (d.ncomp != 1) {
-            sample2(tp[1], p, b0, b1);
-            sample2(tp[2], p, r0, r1);
+            sel(1, bn, bf, rnd);
+            sample2(ta[1], bn, bf, rnd, p, pc, pc.cr1, b0, b1);
+            sel(2, bn, bf, rnd);
+            sample2(ta[2], bn, bf, rnd, p, pc, pc.cr2, r0, r1);
         }
         w0 = rgbw(y0, b0, r0);
         w1 = rgbw(y1, b1, r1);
@@ -930,25 +958,13 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                 ta[c] = row_tap(c, r.y0 + lo + r0);
                 tb[c] = row_tap(c, r.y0 + lo + r0 + nr - 1);
             }
-        // the item's row taps: the two rows differ only in their row offsets and rounding
-        auto taps_of = [&](bool second, RowTap (&t)[3]) __attribute__((always_inline)) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                t[c] = ta[c];
-                t[c].bn = second ? tb[c].bn : ta[c].bn;
-                t[c].bf = second ? tb[c].bf : ta[c].bf;
-                t[c].rnd = second ? tb[c].rnd : ta[c].rnd;
-            }
-        };
         const int nitems = nr * npair;
         if (!r.need_h) {  // the width already is S: the colour rows are the pass's output
             for (int it = lane; it < nitems; it += 64) {
                 const bool second = it >= npair;
                 const int p = second ? it - npair : it;
-                RowTap t[3];
-                taps_of(second, t);
                 uint32_t w[2];
-                pair_rgb(t, p, w[0], w[1]);
+                pair_rgb(ta, tb, second, p, w[0], w[1]);
                 uint8_t *trow = tmp + (r0 + (second ? 1 : 0)) * TP;
                 for (int e = 0; e < 2 && 2 * p + e < W; ++e)
                     for (int bb = 0; bb < 3; ++bb) trow[3 * (2 * p + e) + bb] = (uint8_t)(w[e] >> (8 * bb));
@@ -960,11 +976,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
             const bool second = it >= npair;
             const int p = second ? it - npair : it;
             uint32_t w0 = p, w1 = p;
-            if (!(skip & 1)) {
-                RowTap t[3];
-                taps_of(second, t);
-                pair_rgb(t, p, w0, w1);
-            }
+            if (!(skip & 1)) pair_rgb(ta, tb, second, p, w0, w1);
             uint32_t *rb = rowbuf + (second ? RW : 0) + 2 * p;
             if (2 * p + 1 < W) *reinterpret_cast<uint2 *>(rb) = make_uint2(w0, w1);
             else rb[0] = w0;
@@ -1037,9 +1049,12 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
         }
         const int ymin = r.vb[2 * yo] - lo;
 #if defined(RC_GEMM_ABLATION)
+        if (g_band_skip & 16) continue;
         const int yn = (g_band_skip & 4) ? 0 : r.vb[2 * yo + 1];
+        const int vk = (g_band_skip & 4) ? 0 : r.vk;
 #else
         const int yn = r.vb[2 * yo + 1];
+        const int vk = r.vk;
 #endif
         const int *c = r.vc + yo * r.vk;
         auto store = [&](int cw, int a0, int a1, int a2, int a3) __attribute__((always_inline)) {
@@ -1064,7 +1079,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                 int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
 #pragma unroll
                 for (int k = 0; k < BAND_MAXV; ++k) {
-                    if (k >= r.vk) break;  // uniform: 5 or 7 taps for the usual scales
+                    if (k >= vk) break;  // uniform: 5 or 7 taps for the usual scales
                     const uint32_t w = t32[ro[k] + cw];
                     a0 += (int)(w & 255u) * cv[k];
                     a1 += (int)((w >> 8) & 255u) * cv[k];

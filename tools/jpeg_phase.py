@@ -1,14 +1,14 @@
 """Per-phase time split of jpeg_band_resize_kernel (diagnostic; needs the diagnostic build,
 RC_LIB_PATH=.../lib/diag/libretrieval_core.so, under rocprofv3 --kernel-trace): 256 fixture-shaped
 JPEGs decoded with phase-skip masks (rc_diag_set_band_skip: 1 colour, 2 horizontal, 4 vertical
-math skipped), REPS calls per mask in the order printed.  --parse <kernel_trace.csv> then folds
+math, 8 plane copy, 16 vertical pass + stores skipped), REPS calls per mask in the order printed.  --parse <kernel_trace.csv> then folds
 the band kernel's durations into per-mask medians."""
 import importlib
 import json
 import os
 import sys
 
-MASKS = [0, 1, 2, 4, 3, 7]
+MASKS = [0, 1, 2, 4, 3, 7, 15, 31]
 REPS = 12
 
 if len(sys.argv) > 2 and sys.argv[1] == "--parse":
@@ -22,7 +22,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--parse":
     for i, m in enumerate(MASKS):
         x = sorted(d[i * REPS + 2:(i + 1) * REPS])  # first two calls of a mask: warm-up
         out[f"skip{m}"] = round(x[len(x) // 2], 2)
-    print(json.dumps({"band_kernel_us_median": out, "masks": "1 colour, 2 horizontal, 4 vertical math skipped"}))
+    print(json.dumps({"band_kernel_us_median": out, "masks": "1 colour, 2 horizontal, 4 vertical math, 8 plane copy, 16 vertical pass + stores skipped"}))
     sys.exit(0)
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
