@@ -553,6 +553,7 @@ __device__ __forceinline__ void att_coop_tile(uint8_t *Ks, const uint8_t *Vs, Lo
     float *xch = reinterpret_cast<float *>(Ks);  // [4 waves][16 queries] maxima, then sums
     bar();  // every score read of K is done: the K region is free
     if (g == 0) xch[wave * 16 + li] = mx;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // s_barrier alone does not retire LDS writes
     bar();
     mx = fmaxf(fmaxf(xch[li], xch[16 + li]), fmaxf(xch[32 + li], xch[48 + li]));
     const float nmc = -mx * scale_log2e;
@@ -586,6 +587,7 @@ __device__ __forceinline__ void att_coop_tile(uint8_t *Ks, const uint8_t *Vs, Lo
     if (g == 0) xch[64 + wave * 16 + li] = sum;
 #pragma unroll
     for (int d = 0; d < 4; ++d) part[(wave * 4 + d) * 64 + lane] = o[d];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     if (wave != 0) return;
     const float tot = (xch[64 + li] + xch[80 + li]) + (xch[96 + li] + xch[112 + li]);

@@ -134,7 +134,10 @@ def decode_many(blobs: List[bytes]) -> list:
 
 def embed_many_device(blobs: List[bytes], normalized: bool = False):
     """Image bytes → (raw [n,768], normed or None) device tensors (the batched ingest path)."""
-    images = decode_many(blobs)
+    return _embed_decoded(decode_many(blobs), normalized)
+
+
+def _embed_decoded(images: list, normalized: bool = False):
     emb = get_embedder()
     if hasattr(emb, "assign_by_location"):  # a pool: embed each image on the GPU that decoded it
         return emb.embed_images(images, normalized=normalized, assign=emb.assign_by_location(images))
@@ -149,17 +152,17 @@ def embed_many(blobs: List[bytes]) -> list[list[float]]:
 
     from ..index import F32List
 
+    images = decode_many(blobs)  # validates first: a non-image is a 400 before the model loads
     emb = get_embedder()
     if len(blobs) == 1 and not hasattr(emb, "assign_by_location"):
         # the /embed request: the final kernel writes the vector straight into pinned host memory
         # (no D2H copy), then one stream sync
-        images = decode_many(blobs)
         host = torch.empty((1, emb.hidden), dtype=torch.float32, pin_memory=True)
         emb.embed_images(images, out=(host, None))
         torch.cuda.current_stream(emb.device).synchronize()
         a = host.numpy()
     else:
-        raw, _ = embed_many_device(blobs)
+        raw, _ = _embed_decoded(images)
         a = raw.cpu().numpy()
     return [F32List(row.tolist(), row) for row in a]
 
