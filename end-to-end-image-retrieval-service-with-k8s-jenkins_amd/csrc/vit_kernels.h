@@ -509,103 +509,6 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
     }
 }
 
-// The cooperative last query tile of attention_v2_kernel (qt, partial: tokens % 16 queries):
-// wave w takes key tiles w, w + 4, ... — their scores (att_scores' MFMAs and masking, the same
-// bits), the per-query max over the block (LDS exchange: max is exact, so every p = exp2(s·c −
-// max·c) equals the one-wave form's), its partial exp-sum and partial O = Σ p·V over its key
-// tiles (16x16x16 MFMA per key tile); wave 0 adds the four partial sums and outputs in wave order,
-// normalises and stores.  All 4 waves enter (block-uniform); K / V stay staged until the last
-// score reads, after which the K region holds the exchanges.
-template <int TOK, typename LoadQ, typename Bar>
-__device__ __forceinline__ void att_coop_tile(uint8_t *Ks, const uint8_t *Vs, LoadQ &&load_q, int qt, int tokens,
-                                              float scale_log2e, uint16_t *obase, int H, int wave, Bar &&bar) {
-    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-    constexpr int KPW = (ATT2_TILES + 3) / 4;  // key tiles per wave, at most
-    bf16x8 qc[2];
-    load_q(qc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this Q, and every own-tile store retired
-    bar();  // every wave is past its own tiles (K, V still intact)
-    __builtin_amdgcn_sched_barrier(0);
-    f32x4 sp[KPW];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < KPW; ++i) {
-        const int t = wave + 4 * i;
-        sp[i] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        if (t < ATT2_TILES) {
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            const int r = t * 16 + li;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int c = s2 * 4 + g;
-                const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Ks + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qc[s2], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (t * 16 + g * 4 + j >= tokens) acc[j] = -INFINITY;
-            sp[i] = acc;
-            mx = fmaxf(mx, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    float *xch = reinterpret_cast<float *>(Ks);  // [4 waves][16 queries] maxima, then sums
-    bar();  // every score read of K is done: the K region is free
-    if (g == 0) xch[wave * 16 + li] = mx;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // s_barrier alone does not retire LDS writes
-    bar();
-    mx = fmaxf(fmaxf(xch[li], xch[16 + li]), fmaxf(xch[32 + li], xch[48 + li]));
-    const float nmc = -mx * scale_log2e;
-    float sum = 0.f;
-    f32x4 o[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int qq = li >> 2, pp = li & 3;
-#pragma unroll
-    for (int i = 0; i < KPW; ++i) {
-        const int t = wave + 4 * i;
-        if (t >= ATT2_TILES) continue;
-        s16x4 pf4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float pv = __builtin_amdgcn_exp2f(fmaf(sp[i][j], scale_log2e, nmc));
-            sum += pv;
-            pf4[j] = __builtin_bit_cast(short, (__bf16)pv);
-        }
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const int row = t * 16 + g * 4 + qq;
-            const int chunk = (2 * d + (pp >> 1)) ^ (((row >> 1) & 3) << 1);
-            const s16x4 v4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(Vs + row * 128 + chunk * 16 + (pp & 1) * 8));
-            o[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(v4, pf4, o[d], 0, 0, 0);
-        }
-    }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
-    f32x4 *part = reinterpret_cast<f32x4 *>(Ks + 512);  // [4 waves][4 dims][64 lanes] after the maxima and sums
-    if (g == 0) xch[64 + wave * 16 + li] = sum;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) part[(wave * 4 + d) * 64 + lane] = o[d];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    if (wave != 0) return;
-    const float tot = (xch[64 + li] + xch[80 + li]) + (xch[96 + li] + xch[112 + li]);
-    const int q = qt * 16 + li;
-    if (q >= tokens) return;
-    const float inv = 1.0f / tot;
-    uint16_t *orow = obase + (int64_t)q * H;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const f32x4 a = part[(0 * 4 + d) * 64 + lane], b = part[(1 * 4 + d) * 64 + lane];
-        const f32x4 c = part[(2 * 4 + d) * 64 + lane], e = part[(3 * 4 + d) * 64 + lane];
-        f32x4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = ((a[j] + b[j]) + (c[j] + e[j])) * inv;
-        *reinterpret_cast<uint2 *>(orow + d * 16 + g * 4) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-    }
-}
-
 // TOK > 0: the token count as a compile-time constant (197 for ViT-B/16 at 224),
 // so only the last key tile carries the padding mask; TOK = 0 reads `tokens`.
 // qsplit > 1 (small batches: a lone image is 12 (image, head) items for 256 CUs): block b is
@@ -673,33 +576,25 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     auto scores = [&](const bf16x8 (&qf)[2]) { att_scores<TOK>(Ks, qf, tokens, scale_log2e, st, sum); };
     auto pv_store = [&](int qt) { att_pv_store(Vs, st, sum, qt, tokens, out + (int64_t)img * tokens * H + h * HD, H); };
 
-    // The last query tile, when partial (197 tokens: 5 queries), is not one wave's: the 4 waves of
-    // the block that owns it split its 13 key tiles (§ attention_v2 cooperative tile below) —
-    // otherwise wave 0 walks 4 tiles against 3 for the others, a quarter longer critical path.
-    const bool coop = (tokens & 15) != 0;
-    const int ql = nqt - 1, nown = coop ? ql : nqt;  // this wave's own tiles: t0, t0 + tstep, ... < nown
     // first tile: scores while V lands, then every wave waits for V once
-    const bool first = t0 < nown;
+    const bool first = t0 < nqt;
     bf16x8 qn[2];
-    if (first && t0 + tstep < nown) load_q(t0 + tstep, qn);  // the next tile's queries, under the scores
+    if (first && t0 + tstep < nqt) load_q(t0 + tstep, qn);  // the next tile's queries, under the scores
     if (first) scores(qf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V staged (waves HALF..), qn landed
     bar();
     __builtin_amdgcn_sched_barrier(0);
     if (first) pv_store(t0);
-    for (int qt = t0 + tstep; qt < nown; qt += tstep) {
+    for (int qt = t0 + tstep; qt < nqt; qt += tstep) {
         // qn (issued a tile ago) has landed; the previous tile's 4 output stores may still fly
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         qf[0] = qn[0];
         qf[1] = qn[1];
-        if (qt + tstep < nown) load_q(qt + tstep, qn);  // prefetch the next tile's queries
+        if (qt + tstep < nqt) load_q(qt + tstep, qn);  // prefetch the next tile's queries
         scores(qf);
         pv_store(qt);
     }
-    if (coop && (ql / W) % qsplit == qs)  // block-uniform: this block owns the partial tile
-        att_coop_tile<TOK>(Ks, Vs, [&](bf16x8 (&qv)[2]) { load_q(ql, qv); }, ql, tokens, scale_log2e,
-                           out + (int64_t)img * tokens * H + h * HD, H, wave, bar);
 }
 
 // Self-attention v3: the per-(image, head) arithmetic of attention_v2_kernel (att_scores /
