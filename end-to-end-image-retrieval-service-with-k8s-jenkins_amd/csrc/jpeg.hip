@@ -756,7 +756,8 @@ typedef __attribute__((address_space(3))) void jpeg_lds_void_t;
 
 #if defined(RC_GEMM_ABLATION)
 // diagnostic builds: phases of jpeg_band_resize_kernel to skip (1 colour, 2 horizontal, 4 vertical
-// math, 8 the plane copy, 16 the vertical pass and its stores), for a per-phase time split
+// math, 8 the plane copy, 16 the vertical pass and its stores; 32 / 64: return after the
+// descriptors / after the plane DMA and tap loads), for a per-phase time split
 // (tools/jpeg_phase.py); wrong pixels
 __device__ int g_band_skip = 0;
 #endif
@@ -782,6 +783,9 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     const int lo = r.need_v ? r.vb[2 * yo0] : yo0;
     const int hi = r.need_v ? r.vb[2 * (yo1 - 1)] + r.vb[2 * (yo1 - 1) + 1] : yo1;
     const int rows = hi - lo, W = d.W;
+#if defined(RC_GEMM_ABLATION)
+    if (g_band_skip & 32) return;  // launch + descriptors only
+#endif
     // 0. planes (components unrolled with constant indices: a runtime-indexed Desc / offset array
     //    would live in scratch memory, one scratch load per sample read)
     int poff[3], pbr0[3], pnbr[3];
@@ -833,6 +837,9 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the plane DMA (and the taps) landed
     __syncthreads();
+#if defined(RC_GEMM_ABLATION)
+    if (g_band_skip & 64) return;  // + plane DMA and tap loads
+#endif
     // jdsample.c's upsampler for one source row y as wave-uniform row offsets into the LDS planes
     // (near / far sample row) and a kind: 0 the sample itself (1x1, or box h2 when the plane is
     // <= 2 samples wide), 1 h1v2, 2 h2v1, 3 h2v2 fancy.  The fancy forms read the neighbour

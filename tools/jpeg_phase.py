@@ -8,7 +8,7 @@ import json
 import os
 import sys
 
-MASKS = [0, 1, 2, 4, 3, 7, 15, 31]
+MASKS = [0, 1, 2, 4, 3, 7, 15, 31, 32, 64, 72]
 REPS = 12
 
 if len(sys.argv) > 2 and sys.argv[1] == "--parse":
@@ -22,7 +22,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--parse":
     for i, m in enumerate(MASKS):
         x = sorted(d[i * REPS + 2:(i + 1) * REPS])  # first two calls of a mask: warm-up
         out[f"skip{m}"] = round(x[len(x) // 2], 2)
-    print(json.dumps({"band_kernel_us_median": out, "masks": "1 colour, 2 horizontal, 4 vertical math, 8 plane copy, 16 vertical pass + stores skipped"}))
+    print(json.dumps({"band_kernel_us_median": out, "masks": "1 colour, 2 horizontal, 4 vertical math, 8 plane copy, 16 vertical pass + stores skipped, 32 return after descriptors, 64 return after plane DMA + taps"}))
     sys.exit(0)
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
