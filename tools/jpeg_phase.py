@@ -2,13 +2,13 @@
 RC_LIB_PATH=.../lib/diag/libretrieval_core.so, under rocprofv3 --kernel-trace): 256 fixture-shaped
 JPEGs decoded with phase-skip masks (rc_diag_set_band_skip: 1 colour, 2 horizontal, 4 vertical
 math, 8 plane copy, 16 vertical pass + stores skipped), REPS calls per mask in the order printed.  --parse <kernel_trace.csv> then folds
-the band kernel's durations into per-mask medians."""
+the band kernel's durations into per-mask medians.  RC_PHASE_MASKS=0,31 picks the masks."""
 import importlib
 import json
 import os
 import sys
 
-MASKS = [0, 1, 2, 4, 3, 7, 15, 31, 32, 64, 72]
+MASKS = [int(x) for x in os.environ.get("RC_PHASE_MASKS", "0,1,2,4,3,7,15,31,32,64,72").split(",")]
 REPS = 12
 
 if len(sys.argv) > 2 and sys.argv[1] == "--parse":
