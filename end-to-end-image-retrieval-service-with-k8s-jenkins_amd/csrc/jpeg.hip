@@ -819,19 +819,20 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     const int TP = L.tp;
     uint32_t *rowbuf = reinterpret_cast<uint32_t *>(lds + L.rowbuf) + wave * 2 * ((W + 1) & ~1);
     uint8_t *tmp = lds + L.tmp;
-    // horizontal taps of this lane's output columns (MAXT > 0), kept across its wave's rows
-    int cf[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1], px[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1];
+    // horizontal taps of this lane's output columns (MAXT > 0), kept across its wave's rows: the
+    // coefficients and the first tap's pixel xm; tap k reads word xm + k of the row buffer (one
+    // address per column, the taps as immediate offsets).  Taps past a column's count have
+    // coefficient 0, so the words they read past the row's end (at most MAXT - 1: the next row
+    // buffer, or the tmp area after the last) only add 0.
+    int cf[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1], xm[MAXT > 0 ? BAND_NXO : 1];
     if constexpr (MAXT > 0) {
         if (r.need_h) {
 #pragma unroll
             for (int t = 0; t < BAND_NXO; ++t) {
                 const int xo = min(lane + 64 * t, S - 1);
-                const int xmin = r.hb[2 * xo];
+                xm[t] = r.hb[2 * xo];
 #pragma unroll
-                for (int k = 0; k < MAXT; ++k) {
-                    cf[t][k] = k < r.hk ? r.hc[xo * r.hk + k] : 0;
-                    px[t][k] = min(xmin + k, W - 1);
-                }
+                for (int k = 0; k < MAXT; ++k) cf[t][k] = k < r.hk ? r.hc[xo * r.hk + k] : 0;
             }
         }
     }
@@ -1002,9 +1003,10 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                     const int xo = lane + 64 * t;
                     if (xo < S) {
                         int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+                        const uint32_t *rp = rbuf + xm[t];
 #pragma unroll
                         for (int k = 0; k < MAXT; ++k) {
-                            const uint32_t w = rbuf[px[t][k]];
+                            const uint32_t w = rp[k];
                             a0 += (int)(w & 255u) * cf[t][k];
                             a1 += (int)((w >> 8) & 255u) * cf[t][k];
                             a2 += (int)(w >> 16) * cf[t][k];
