@@ -34,6 +34,7 @@
 
 #include <map>
 #include <tuple>
+#include <type_traits>
 
 #include "rc_common.h"
 #include "resample.h"
@@ -576,9 +577,9 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t *__restri
     }
     const int cb = upsampled(planes, d, 1, x, y) - 128, cr = upsampled(planes, d, 2, x, y) - 128;
     // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert (SCALEBITS 16)
-    const int R = Y + ((91881 * cr + 32768) >> 16);
-    const int G = Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
-    const int B = Y + ((116130 * cb + 32768) >> 16);
+    const int R = Y + ((__mul24(91881, cr) + 32768) >> 16);
+    const int G = Y + ((__mul24(-22554, cb) + 32768 - __mul24(46802, cr)) >> 16);
+    const int B = Y + ((__mul24(116130, cb) + 32768) >> 16);
     o[0] = (uint8_t)min(max(R, 0), 255);
     o[1] = (uint8_t)min(max(G, 0), 255);
     o[2] = (uint8_t)min(max(B, 0), 255);
@@ -608,9 +609,9 @@ __device__ __forceinline__ void ycc_rgb(const uint8_t *__restrict__ planes, cons
         return;
     }
     const int cb = upsampled(planes, d, 1, x, y) - 128, cr = upsampled(planes, d, 2, x, y) - 128;
-    R = min(max(Y + ((91881 * cr + 32768) >> 16), 0), 255);
-    G = min(max(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16), 0), 255);
-    B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
+    R = min(max(Y + ((__mul24(91881, cr) + 32768) >> 16), 0), 255);
+    G = min(max(Y + ((__mul24(-22554, cb) + 32768 - __mul24(46802, cr)) >> 16), 0), 255);
+    B = min(max(Y + ((__mul24(116130, cb) + 32768) >> 16), 0), 255);
 }
 
 constexpr int RS_WIN = 16384;  // source pixels of one row staged in LDS at a time (48 KB)
@@ -670,9 +671,9 @@ __global__ __launch_bounds__(256) void jpeg_color_resize_h_kernel(const uint8_t 
             int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
             for (int k = 0; k < xn; ++k) {
                 const uint8_t *p = row + 3 * (xmin + k);
-                a0 += p[0] * c[k];
-                a1 += p[1] * c[k];
-                a2 += p[2] * c[k];
+                a0 = resample_tap(a0, p[0], c[k]);
+                a1 = resample_tap(a1, p[1], c[k]);
+                a2 = resample_tap(a2, p[2], c[k]);
             }
             dst[3 * xo] = clip8_22(a0);
             dst[3 * xo + 1] = clip8_22(a1);
@@ -698,9 +699,9 @@ __global__ __launch_bounds__(256) void jpeg_resize_v_kernel(const RDesc *__restr
     int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
     for (int k = 0; k < yn; ++k) {
         const uint8_t *q = col + (int64_t)k * S * 3;
-        a0 += q[0] * c[k];
-        a1 += q[1] * c[k];
-        a2 += q[2] * c[k];
+        a0 = resample_tap(a0, q[0], c[k]);
+        a1 = resample_tap(a1, q[1], c[k]);
+        a2 = resample_tap(a2, q[2], c[k]);
     }
     uint8_t *o = out + r.out_off + (int64_t)p * 3;
     o[0] = clip8_22(a0);
@@ -774,14 +775,19 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const Desc d = descs[blockIdx.y];
     const RDesc r = rdescs[blockIdx.y];
+    // the coefficient tables through global-address-space pointers: global (not flat) loads,
+    // counted by vmcnt alone
+    typedef const __attribute__((address_space(1))) int gint_t;
+    const gint_t *hb = (const gint_t *)r.hb, *hc = (const gint_t *)r.hc, *vb = (const gint_t *)r.vb,
+                 *vc = (const gint_t *)r.vc;
     const int S = r.S, yo0 = (int)blockIdx.x * r.bh;
     if (yo0 >= S) return;  // block-uniform: this image has fewer bands
     const int yo1 = min(S, yo0 + r.bh), nout = yo1 - yo0;
     // wave-uniform in an SGPR: the row-dependent upsampler offsets below then stay scalar
     const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     // source rows of the band (relative to r.y0; Pillow's bounds are monotone in the output row)
-    const int lo = r.need_v ? r.vb[2 * yo0] : yo0;
-    const int hi = r.need_v ? r.vb[2 * (yo1 - 1)] + r.vb[2 * (yo1 - 1) + 1] : yo1;
+    const int lo = r.need_v ? vb[2 * yo0] : yo0;
+    const int hi = r.need_v ? vb[2 * (yo1 - 1)] + vb[2 * (yo1 - 1) + 1] : yo1;
     const int rows = hi - lo, W = d.W;
 #if defined(RC_GEMM_ABLATION)
     if (g_band_skip & 32) return;  // launch + descriptors only
@@ -830,9 +836,9 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
 #pragma unroll
             for (int t = 0; t < BAND_NXO; ++t) {
                 const int xo = min(lane + 64 * t, S - 1);
-                xm[t] = r.hb[2 * xo];
+                xm[t] = hb[2 * xo];
 #pragma unroll
-                for (int k = 0; k < MAXT; ++k) cf[t][k] = k < r.hk ? r.hc[xo * r.hk + k] : 0;
+                for (int k = 0; k < MAXT; ++k) cf[t][k] = k < r.hk ? hc[xo * r.hk + k] : 0;
             }
         }
     }
@@ -918,12 +924,13 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     };
     // jdcolor.c ycc_rgb_convert, as ycc_rgb: RGB of one pixel as the word R | G << 8 | B << 16
     auto rgbw = [&](int Y, int cb, int cr) {
-        if (d.ncomp == 1) return (uint32_t)Y * 0x010101u;
+        if (d.ncomp == 1) return (uint32_t)__mul24(Y, 0x010101);
         cb -= 128;
         cr -= 128;
-        const int R = min(max(Y + ((91881 * cr + 32768) >> 16), 0), 255);
-        const int G = min(max(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16), 0), 255);
-        const int B = min(max(Y + ((116130 * cb + 32768) >> 16), 0), 255);
+        // 24-bit products (|cb|, |cr| <= 128): full-rate v_mad_i32_i24, the same bits
+        const int R = min(max(Y + ((__mul24(91881, cr) + 32768) >> 16), 0), 255);
+        const int G = min(max(Y + ((__mul24(-22554, cb) + 32768 - __mul24(46802, cr)) >> 16), 0), 255);
+        const int B = min(max(Y + ((__mul24(116130, cb) + 32768) >> 16), 0), 255);
         return (uint32_t)R | ((uint32_t)G << 8) | ((uint32_t)B << 16);
     };
     // the pair of row ta (second = false) or tb; only the fields a kind reads are selected
@@ -946,6 +953,28 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
         w0 = rgbw(y0, b0, r0);
         w1 = rgbw(y1, b1, r1);
     };
+    // The common 4:2:0 layout (Y full size; Cb, Cr h2v2 fancy-upsampled, as wide as each other and
+    // > 2 samples): pair_rgb's arithmetic with the kinds known — the pair's 13 LDS reads (Y as one
+    // 16-bit read) issued together, then the sums, instead of a kind dispatch and a wait per
+    // component.  Block-uniform; the kinds do not depend on the row.
+    auto pair_rgb420 = [&](const RowTap *ta, const RowTap *tb, bool second, int p, uint32_t &w0, uint32_t &w1) {
+        const int bny = second ? tb[0].bn : ta[0].bn;
+        const int bn1 = second ? tb[1].bn : ta[1].bn, bf1 = second ? tb[1].bf : ta[1].bf;
+        const int bn2 = second ? tb[2].bn : ta[2].bn, bf2 = second ? tb[2].bf : ta[2].bf;
+        const int c2 = col(2 * p), cp = col(p), cl = col(max(p - 1, 0)), cr = col(min(p + 1, ta[1].dw1));
+        const uint32_t yy = *reinterpret_cast<const uint16_t *>(lds + bny + c2);  // 2p, 2p + 1: one block row
+        const int n1p = lds[bn1 + cp], f1p = lds[bf1 + cp], n1l = lds[bn1 + cl], f1l = lds[bf1 + cl];
+        const int n1r = lds[bn1 + cr], f1r = lds[bf1 + cr];
+        const int n2p = lds[bn2 + cp], f2p = lds[bf2 + cp], n2l = lds[bn2 + cl], f2l = lds[bf2 + cl];
+        const int n2r = lds[bn2 + cr], f2r = lds[bf2 + cr];
+        const int s1 = 3 * (3 * n1p + f1p), s2 = 3 * (3 * n2p + f2p);
+        const int b0 = (s1 + 3 * n1l + f1l + 8) >> 4, b1 = (s1 + 3 * n1r + f1r + 7) >> 4;
+        const int r0 = (s2 + 3 * n2l + f2l + 8) >> 4, r1 = (s2 + 3 * n2r + f2r + 7) >> 4;
+        w0 = rgbw((int)(yy & 255u), b0, r0);
+        w1 = rgbw((int)(yy >> 8), b1, r1);
+    };
+    const bool f420 = d.ncomp == 3 && d.rx[0] == 1 && d.ry[0] == 1 && d.rx[1] == 2 && d.ry[1] == 2 &&
+                      d.rx[2] == 2 && d.ry[2] == 2 && d.dw[1] > 2 && d.dw[1] == d.dw[2];
     // 1. colour + horizontal pass, two source rows per wave at a time (no block barrier): the
     //    colour items of both rows are one flat range of pixel pairs (a lone 168-px row is 84 pairs,
     //    2 of 64-lane steps at 66 % use; two rows are 3 steps at 88 %), then the two rows' filter
@@ -972,7 +1001,8 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                 const bool second = it >= npair;
                 const int p = second ? it - npair : it;
                 uint32_t w[2];
-                pair_rgb(ta, tb, second, p, w[0], w[1]);
+                if (f420) pair_rgb420(ta, tb, second, p, w[0], w[1]);
+                else pair_rgb(ta, tb, second, p, w[0], w[1]);
                 uint8_t *trow = tmp + (r0 + (second ? 1 : 0)) * TP;
                 for (int e = 0; e < 2 && 2 * p + e < W; ++e)
                     for (int bb = 0; bb < 3; ++bb) trow[3 * (2 * p + e) + bb] = (uint8_t)(w[e] >> (8 * bb));
@@ -984,7 +1014,9 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
             const bool second = it >= npair;
             const int p = second ? it - npair : it;
             uint32_t w0 = p, w1 = p;
-            if (!(skip & 1)) pair_rgb(ta, tb, second, p, w0, w1);
+            if (skip & 1) {
+            } else if (f420) pair_rgb420(ta, tb, second, p, w0, w1);
+            else pair_rgb(ta, tb, second, p, w0, w1);
             uint32_t *rb = rowbuf + (second ? RW : 0) + 2 * p;
             if (2 * p + 1 < W) *reinterpret_cast<uint2 *>(rb) = make_uint2(w0, w1);
             else rb[0] = w0;
@@ -1007,9 +1039,9 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
 #pragma unroll
                         for (int k = 0; k < MAXT; ++k) {
                             const uint32_t w = rp[k];
-                            a0 += (int)(w & 255u) * cf[t][k];
-                            a1 += (int)((w >> 8) & 255u) * cf[t][k];
-                            a2 += (int)(w >> 16) * cf[t][k];
+                            a0 = resample_tap(a0, (int)(w & 255u), cf[t][k]);
+                            a1 = resample_tap(a1, (int)((w >> 8) & 255u), cf[t][k]);
+                            a2 = resample_tap(a2, (int)(w >> 16), cf[t][k]);
                         }
                         trow[3 * xo] = clip8_22(a0);
                         trow[3 * xo + 1] = clip8_22(a1);
@@ -1018,15 +1050,15 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                 }
             } else {
                 for (int xo = lane; xo < S; xo += 64) {
-                    const int xmin = r.hb[2 * xo], xn = r.hb[2 * xo + 1];
+                    const int xmin = hb[2 * xo], xn = hb[2 * xo + 1];
                     const int *c = r.hc + xo * r.hk;
                     int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
                     for (int k = 0; k < xn; ++k) {
                         const uint32_t w = rbuf[xmin + k];
                         const int ck = c[k];
-                        a0 += (int)(w & 255u) * ck;
-                        a1 += (int)((w >> 8) & 255u) * ck;
-                        a2 += (int)(w >> 16) * ck;
+                        a0 = resample_tap(a0, (int)(w & 255u), ck);
+                        a1 = resample_tap(a1, (int)((w >> 8) & 255u), ck);
+                        a2 = resample_tap(a2, (int)(w >> 16), ck);
                     }
                     trow[3 * xo] = clip8_22(a0);
                     trow[3 * xo + 1] = clip8_22(a1);
@@ -1056,16 +1088,16 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
             }
             continue;
         }
-        const int ymin = r.vb[2 * yo] - lo;
+        const int ymin = vb[2 * yo] - lo;
 #if defined(RC_GEMM_ABLATION)
         if (g_band_skip & 16) continue;
-        const int yn = (g_band_skip & 4) ? 0 : r.vb[2 * yo + 1];
+        const int yn = (g_band_skip & 4) ? 0 : vb[2 * yo + 1];
         const int vk = (g_band_skip & 4) ? 0 : r.vk;
 #else
-        const int yn = r.vb[2 * yo + 1];
+        const int yn = vb[2 * yo + 1];
         const int vk = r.vk;
 #endif
-        const int *c = r.vc + yo * r.vk;
+        const gint_t *c = vc + yo * r.vk;
         auto store = [&](int cw, int a0, int a1, int a2, int a3) __attribute__((always_inline)) {
             const uint32_t v = (uint32_t)clip8_22(a0) | ((uint32_t)clip8_22(a1) << 8) | ((uint32_t)clip8_22(a2) << 16) |
                                ((uint32_t)clip8_22(a3) << 24);
@@ -1084,19 +1116,27 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
                 cv[k] = k < yn ? c[k] : 0;
                 ro[k] = min(ymin + k, rows - 1) * nw;
             }
-            for (int cw = lane; cw < nw; cw += 64) {
-                int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
+            // a column's taps: all T words read first, then the sums (no wait between taps);
+            // T = 4 or BAND_MAXV, the taps past vk reading clamped rows with coefficient 0
+            auto vcols = [&](auto tn) __attribute__((always_inline)) {
+                constexpr int T = decltype(tn)::value;
+                for (int cw = lane; cw < nw; cw += 64) {
+                    uint32_t w[T];
 #pragma unroll
-                for (int k = 0; k < BAND_MAXV; ++k) {
-                    if (k >= vk) break;  // uniform: 5 or 7 taps for the usual scales
-                    const uint32_t w = t32[ro[k] + cw];
-                    a0 += (int)(w & 255u) * cv[k];
-                    a1 += (int)((w >> 8) & 255u) * cv[k];
-                    a2 += (int)((w >> 16) & 255u) * cv[k];
-                    a3 += (int)(w >> 24) * cv[k];
+                    for (int k = 0; k < T; ++k) w[k] = t32[ro[k] + cw];
+                    int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
+#pragma unroll
+                    for (int k = 0; k < T; ++k) {
+                        a0 = resample_tap(a0, (int)(w[k] & 255u), cv[k]);
+                        a1 = resample_tap(a1, (int)((w[k] >> 8) & 255u), cv[k]);
+                        a2 = resample_tap(a2, (int)((w[k] >> 16) & 255u), cv[k]);
+                        a3 = resample_tap(a3, (int)(w[k] >> 24), cv[k]);
+                    }
+                    store(cw, a0, a1, a2, a3);
                 }
-                store(cw, a0, a1, a2, a3);
-            }
+            };
+            if (vk <= 4) vcols(std::integral_constant<int, 4>{});
+            else vcols(std::integral_constant<int, BAND_MAXV>{});
             continue;
         }
         for (int cw = lane; cw < nw; cw += 64) {
@@ -1105,10 +1145,10 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
             for (int k = 0; k < yn; ++k) {
                 const uint32_t w = q[k * nw];
                 const int ck = c[k];
-                a0 += (int)(w & 255u) * ck;
-                a1 += (int)((w >> 8) & 255u) * ck;
-                a2 += (int)((w >> 16) & 255u) * ck;
-                a3 += (int)(w >> 24) * ck;
+                a0 = resample_tap(a0, (int)(w & 255u), ck);
+                a1 = resample_tap(a1, (int)((w >> 8) & 255u), ck);
+                a2 = resample_tap(a2, (int)((w >> 16) & 255u), ck);
+                a3 = resample_tap(a3, (int)(w >> 24), ck);
             }
             store(cw, a0, a1, a2, a3);
         }

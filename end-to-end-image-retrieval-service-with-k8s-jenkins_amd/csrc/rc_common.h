@@ -173,6 +173,11 @@ struct KernelTimer {
 #if defined(__HIPCC__)
 namespace rc {
 
+// Pillow's fixed-point resample tap acc + pixel·coef: the pixel is a byte and |coef| < 2^23
+// (precompute_coeffs checks it), so the product is v_mad_i32_i24's — a full-rate op, where the
+// 32-bit multiply hipcc emits otherwise (v_mul_lo_u32 / v_mad_u64_u32) issues at a quarter rate.
+// The same bits: the exact product fits 32 bits either way.
+__device__ __forceinline__ int resample_tap(int acc, int pixel, int coef) { return __mul24(pixel, coef) + acc; }
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
 // f32 → bf16 bits, round to nearest even (finite inputs; hipcc lowers a plain

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cmath>
+#include <stdexcept>
 #include <vector>
 
 #include "retrieval_core.h"
@@ -62,6 +63,9 @@ inline ResampleCoeffs precompute_coeffs(int in_size, int out_size, int resample)
         for (int x = 0; x < r.ksize; ++x) {
             const double v = x < xmax ? k[x] : 0.0;
             r.coef[(size_t)xx * r.ksize + x] = v < 0 ? (int)(-0.5 + v * (1 << 22)) : (int)(0.5 + v * (1 << 22));
+            // the device taps multiply in 24 bits (resample_tap): |coef| < 2^23, i.e. |weight| < 2
+            if (r.coef[(size_t)xx * r.ksize + x] >= (1 << 23) || r.coef[(size_t)xx * r.ksize + x] < -(1 << 23))
+                throw std::runtime_error("resample weight out of the 24-bit tap range");
         }
         r.bounds[2 * xx] = xmin;
         r.bounds[2 * xx + 1] = xmax;

@@ -850,9 +850,9 @@ __global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t *__restrict
         int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
         for (int k = 0; k < xn; ++k) {
             const int c = coef[x * ks + k];
-            a0 += row[3 * k] * c;
-            a1 += row[3 * k + 1] * c;
-            a2 += row[3 * k + 2] * c;
+            a0 = resample_tap(a0, row[3 * k], c);
+            a1 = resample_tap(a1, row[3 * k + 1], c);
+            a2 = resample_tap(a2, row[3 * k + 2], c);
         }
         uint8_t *o = dst + i * 3;
         o[0] = clip8_fixed(a0);
@@ -876,9 +876,9 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t *__restrict
         for (int k = 0; k < yn; ++k) {
             const int c = coef[y * ks + k];
             const uint8_t *p = col + (int64_t)k * W * 3;
-            a0 += p[0] * c;
-            a1 += p[1] * c;
-            a2 += p[2] * c;
+            a0 = resample_tap(a0, p[0], c);
+            a1 = resample_tap(a1, p[1], c);
+            a2 = resample_tap(a2, p[2], c);
         }
         uint8_t *o = dst + i * 3;
         o[0] = clip8_fixed(a0);
