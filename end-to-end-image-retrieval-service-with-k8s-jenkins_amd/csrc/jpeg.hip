@@ -725,6 +725,7 @@ __global__ __launch_bounds__(256) void jpeg_resize_v_kernel(const RDesc *__restr
 //      as one word (a wave writes 256 contiguous bytes of an output row; the band's rows and
 //      their taps are wave-uniform).
 // dynamic LDS = the largest per-image need (band_layout, host and device alike).
+constexpr int BAND_WAVES = 8;  // waves per band block
 struct BandLayout {
     int rowbuf, tmp, total, tp;
 };
@@ -733,7 +734,7 @@ __host__ __device__ inline BandLayout band_layout(int rows, int W, int S, int ne
     BandLayout L;
     L.tp = (3 * S + 3) & ~3;
     L.rowbuf = pl;
-    L.tmp = pl + (need_h ? al(4 * 2 * ((W + 1) & ~1) * 4) : 0);  // 4 waves × 2 rows × W RGBX words (8-B rows)
+    L.tmp = pl + (need_h ? al(BAND_WAVES * 2 * ((W + 1) & ~1) * 4) : 0);  // per wave 2 rows × W RGBX words (8-B rows)
     L.total = L.tmp + al(rows * L.tp);
     return L;
 }
@@ -769,7 +770,7 @@ __device__ int g_band_skip = 0;
 // its wave filters (taps past a column's count have coefficient 0, and their pixel index is
 // clamped into the row: exact).  MAXT = 0: the general form (coefficients read per output).
 template <int MAXT>
-__global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
+__global__ __launch_bounds__(64 * BAND_WAVES) __attribute__((amdgpu_waves_per_eu(MAXT == 7 ? 7 : 8, 8))) void jpeg_band_resize_kernel(const uint8_t *__restrict__ planes,
                                                               const Desc *__restrict__ descs,
                                                               const RDesc *__restrict__ rdescs, uint8_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -815,7 +816,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
 #if defined(RC_GEMM_ABLATION)
             if (g_band_skip & 8) continue;
 #endif
-            for (int i0 = wave * 64; i0 < n16; i0 += 256)
+            for (int i0 = wave * 64; i0 < n16; i0 += 64 * BAND_WAVES)
                 if (i0 + lane < n16)
                     __builtin_amdgcn_global_load_lds((const void *)(g + 16 * (i0 + lane)),
                                                      (jpeg_lds_void_t *)(lds + poff[c] + 16 * i0), 16, 0, 0);
@@ -986,7 +987,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     constexpr int skip = 0;
 #endif
     const int npair = (W + 1) >> 1, RW = (W + 1) & ~1;
-    for (int r0 = 2 * wave; r0 < rows; r0 += 8) {
+    for (int r0 = 2 * wave; r0 < rows; r0 += 2 * BAND_WAVES) {
         const int nr = min(2, rows - r0);
         RowTap ta[3], tb[3];
 #pragma unroll
@@ -1075,7 +1076,7 @@ __global__ __launch_bounds__(256, 4) void jpeg_band_resize_kernel(const uint8_t 
     const bool words = (rowbytes & 3) == 0;  // out_off = i·S·S·3 is then 4-aligned as well
     uint8_t *gimg = out + r.out_off;
     const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tmp);
-    for (int j = wave; j < nout; j += 4) {
+    for (int j = wave; j < nout; j += BAND_WAVES) {
         const int yo = yo0 + j;
         uint8_t *grow = gimg + (int64_t)yo * rowbytes;
         if (!r.need_v) {
@@ -1520,13 +1521,13 @@ extern "C" int rc_jpeg_decode_resized(rc_jpeg_decoder *h, int n, const uint8_t *
             // horizontal taps in registers: 5 (any bicubic upscale, e.g. the fixture's 168 -> 224), 7
             // (down to 1.5x), else (or S > 256) the general form
             if (max_hk <= 5 && S <= 64 * jpeg::BAND_NXO)
-                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<5>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<5>, gr, dim3(64 * jpeg::BAND_WAVES), (size_t)band_lds, s, h->d_planes,
                                    h->d_desc, h->d_rdesc, out);
             else if (max_hk <= 7 && S <= 64 * jpeg::BAND_NXO)
-                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<7>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<7>, gr, dim3(64 * jpeg::BAND_WAVES), (size_t)band_lds, s, h->d_planes,
                                    h->d_desc, h->d_rdesc, out);
             else
-                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<0>, gr, dim3(256), (size_t)band_lds, s, h->d_planes,
+                hipLaunchKernelGGL(jpeg::jpeg_band_resize_kernel<0>, gr, dim3(64 * jpeg::BAND_WAVES), (size_t)band_lds, s, h->d_planes,
                                    h->d_desc, h->d_rdesc, out);
             RC_LAUNCH_CHECK();
             return;
