@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(64 * BAND_WAVES) __attribute__((amdgpu_waves_per_eu
                 ro[k] = min(ymin + k, rows - 1) * nw;
             }
             // a column's taps: all T words read first, then the sums (no wait between taps);
-            // T = 4 or BAND_MAXV, the taps past vk reading clamped rows with coefficient 0
+            // T = 3, 5, 7 or BAND_MAXV >= vk, the taps past vk reading clamped rows with coefficient 0
             auto vcols = [&](auto tn) __attribute__((always_inline)) {
                 constexpr int T = decltype(tn)::value;
                 for (int cw = lane; cw < nw; cw += 64) {
@@ -1136,7 +1136,9 @@ __global__ __launch_bounds__(64 * BAND_WAVES) __attribute__((amdgpu_waves_per_eu
                     store(cw, a0, a1, a2, a3);
                 }
             };
-            if (vk <= 4) vcols(std::integral_constant<int, 4>{});
+            if (vk <= 3) vcols(std::integral_constant<int, 3>{});  // bicubic / bilinear upscale, bilinear to 1.5x
+            else if (vk <= 5) vcols(std::integral_constant<int, 5>{});
+            else if (vk <= 7) vcols(std::integral_constant<int, 7>{});  // bicubic down to 1.5x
             else vcols(std::integral_constant<int, BAND_MAXV>{});
             continue;
         }
