@@ -607,12 +607,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // [64w, 64w + 64)): acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + w*64 + ni*16 + 4g + j].
 // The bf16 epilogues stage through `smem` (>= 64 KB; the caller's main loop must be done
 // with it); the f32 ones store from the accumulators.
-template <int EPI>
-__device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4], uint8_t *smem, int m0, int n0) {
+template <int EPI, int MI = 8>
+__device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][4], uint8_t *smem, int m0, int n0) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        static_assert(MI == 8, "bf16 epilogues stage a 128-row tile");
         float4 bias[4];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
@@ -657,8 +658,12 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
         bq[c][0] = *reinterpret_cast<const float4 *>(bp);
         bq[c][1] = *reinterpret_cast<const float4 *>(bp + 4);
     }
+    // 4 rows per lane per pass; a 10-row-block tile (BM = 160) in passes of 2, fewer live registers
+    // beside its 160 accumulator VGPRs
+    static_assert(MI % 4 == 0 || MI % 4 == 2, "row blocks in passes of 4, or of 2");
+    constexpr int N4 = MI % 4 == 0 ? MI / 4 : 0;
 #pragma unroll
-    for (int h4 = 0; h4 < 2; ++h4) {
+    for (int h4 = 0; h4 < N4; ++h4) {
         f32x4 A[4][2][2];
         int rows[4];
 #pragma unroll
@@ -670,6 +675,20 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
                 for (int h = 0; h < 2; ++h) A[r][c][h] = acc[h4 * 4 + r][2 * c + h];
         }
         f32_rows_epilogue<EPI, 4>(a, A, rows, n0 + wave * 64, g, bq, a.M);
+    }
+#pragma unroll
+    for (int m2 = 4 * N4; m2 < MI; m2 += 2) {
+        f32x4 A[2][2][2];
+        int rows[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            rows[r] = m0 + (m2 + r) * 16 + li;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) A[r][c][h] = acc[m2 + r][2 * c + h];
+        }
+        f32_rows_epilogue<EPI, 2>(a, A, rows, n0 + wave * 64, g, bq, a.M);
     }
 }
 
@@ -694,12 +713,16 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[8][4
 // every wave finished reading before the barrier), 12 fragment reads, 32 MFMAs.
 // ABL (diagnostic builds only, as gemm_pp_kernel): bit0 no DMA in the K loop,
 // bit1 no MFMA, bit2 no epilogue.
-template <int EPI, int ABL = 0>
+// BM = 160 (the residual epilogues of large M: 10 row blocks, acc[10][4], 78 KB of ring): a batch
+// of 256 images is 316 x 3 = 948 tiles = 1.85 rounds of 512 workgroup slots, where 128-row tiles are
+// 1 182 = 2.31 rounds (the third 31 % full); launch_gemm picks the BM with the fewer row-rounds.
+template <int EPI, int ABL = 0, int BM = 128>
 __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
-    constexpr int BM = 128, BN = 256, BK = 32, NSLOT = 3;
-    constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 KB + 16 KB
-    constexpr int PIECES = SLOT / 1024, PPW = PIECES / 4;              // 24 pieces, 6 per wave
-    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * SLOT];  // 72 KB
+    constexpr int BN = 256, BK = 32, NSLOT = 3, MI = BM / 16;
+    constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 (10) KB + 16 KB
+    constexpr int PIECES = SLOT / 1024;                                  // 24 (26) pieces: A then W
+    constexpr int PPW = (PIECES + 3) / 4, PPW_LO = PIECES / 4;           // pieces of waves < PIECES % 4 / the rest
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * SLOT];  // 72 (78) KB
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -721,7 +744,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
     const uint16_t *Ag = a.A + (int64_t)m0 * K;
     const uint16_t *Wg = a.W + (int64_t)n0 * K;
 
-    // piece p (1 KB = 16 rows x 64 B): 0-7 A rows 16p.., 8-23 W rows 16(p-8)..
+    // piece p (1 KB = 16 rows x 64 B): 0..MI-1 A rows 16p.., then W rows 16(p-MI)..
     // lane l writes LDS bytes [16 l, 16 l + 16) of the piece: row l >> 2, stored
     // chunk l & 3, which holds source chunk (l & 3) ^ (((l >> 5) & 1) << 1).
     const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
@@ -730,8 +753,9 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
             const int piece = wave + 4 * i;  // wave-uniform
-            const uint16_t *src = piece < 8 ? Ag + (int64_t)(piece * 16 + prow) * K
-                                            : Wg + (int64_t)((piece - 8) * 16 + prow) * K;
+            if (piece >= PIECES) continue;
+            const uint16_t *src = piece < MI ? Ag + (int64_t)(piece * 16 + prow) * K
+                                             : Wg + (int64_t)((piece - MI) * 16 + prow) * K;
             __builtin_amdgcn_global_load_lds((const void *)(src + k0 + pchunk * 8), (lds_void_t *)(base + piece * 1024),
                                              16, 0, 0);
         }
@@ -739,9 +763,9 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
     // fragment of rows r0 + li (r0 % 16 == 0), k chunk g: 16 B at row*64 + (g ^ h(li))*16
     const int fchunk = (g ^ (((li >> 3) & 1) << 1)) << 4;
 
-    f32x4 acc[8][4];
+    f32x4 acc[MI][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -750,44 +774,49 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
     if (nk > 1) stage(1, BK);
     for (int kt = 0; kt < nk; ++kt) {
         // a raw s_barrier: __syncthreads() would add a full vmcnt(0) drain (its
-        // release fence), emptying the DMA pipeline every K-step
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // release fence), emptying the DMA pipeline every K-step.  The next slot's pieces of this
+        // wave may still fly: PPW, or PPW_LO for the waves with one piece fewer (wave-uniform).
+        if (kt + 1 < nk) {
+            if (PPW == PPW_LO || wave < PIECES % 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW_LO) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (!(ABL & 1) && kt + 2 < nk) stage((kt + 2) % NSLOT, (kt + 2) * BK);
         const uint8_t *As = smem + (kt % NSLOT) * SLOT;
         const uint8_t *Ws = As + A_BYTES;
-        bf16x8 wf[4], af[8];
+        bf16x8 wf[4], af[MI];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
             wf[ni] = *reinterpret_cast<const bf16x8 *>(Ws + (wave * 64 + ni * 16 + li) * 64 + fchunk);
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
             af[mi] = *reinterpret_cast<const bf16x8 *>(As + (mi * 16 + li) * 64 + fchunk);
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
                 if constexpr (!(ABL & 2))
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
                 else
                     asm volatile("" ::"v"(wf[ni]), "v"(af[mi]));
-        // all 12 fragment reads first (in source order), then the 32 MFMAs: the
+        // all 4 + MI fragment reads first (in source order), then the 4·MI MFMAs: the
         // compiler's counted lgkmcnt waits let MFMA (mi, *) start once af[mi] lands
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 + MI, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * MI, 0);
     }
 
     if constexpr ((ABL & 4) != 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
         return;
     }
-    w2_epilogue<EPI>(a, acc, smem, m0, n0);
+    w2_epilogue<EPI, MI>(a, acc, smem, m0, n0);
 }
 
 // ------------------------------------------- implicit-GEMM patch embedding ----
@@ -1480,8 +1509,18 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             if constexpr (!epi_ln(EPI)) {
                 RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
                 RC_REQUIRE(a.K % 32 == 0, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 32");
-                const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
-                hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3(ntm * ntn), dim3(256), 0, s, a);
+                const int ntn = a.N / 256;
+                if constexpr (epi_resid(EPI)) {
+                    // 160-row tiles when they take fewer row-rounds of the chip's workgroup slots
+                    // (2 per CU): rounds x BM, the time of one slot's chain
+                    const int slots = 2 * device_cu_count();
+                    const int t128 = (a.M + 127) / 128 * ntn, t160 = (a.M + 159) / 160 * ntn;
+                    if ((int64_t)((t160 + slots - 1) / slots) * 160 < (int64_t)((t128 + slots - 1) / slots) * 128) {
+                        hipLaunchKernelGGL((gemm_w2_kernel<EPI, 0, 160>), dim3(t160), dim3(256), 0, s, a);
+                        break;
+                    }
+                }
+                hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3((a.M + 127) / 128 * ntn), dim3(256), 0, s, a);
             }
             break;
         }
@@ -1522,6 +1561,11 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             } else {
                 throw Error(RC_ERR_UNSUPPORTED, "image-aligned GEMM tiles: residual epilogues only");
             }
+            break;
+        }
+        case 300: {  // the two-workgroup kernel on 128-row tiles whatever M (A/B of the 160-row pick)
+            if constexpr (!epi_ln(EPI))
+                hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3((a.M + 127) / 128 * (a.N / 256)), dim3(256), 0, s, a);
             break;
         }
         case 200 + 1: case 200 + 2: case 200 + 4: case 200 + 6: {

@@ -36,6 +36,24 @@ void set_last_error(const std::string &msg);
 
 #define RC_LAUNCH_CHECK() RC_HIP(hipGetLastError())
 
+// compute units of the current device (cached per device id; launch-shape decisions)
+inline int device_cu_count() {
+    static std::atomic<int> cache[16] = {};
+    int dev = 0;
+    RC_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 16) {
+        int n = 0;
+        RC_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        return n;
+    }
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n == 0) {
+        RC_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        cache[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+
 template <class F>
 int guard(F &&f) {
     try {

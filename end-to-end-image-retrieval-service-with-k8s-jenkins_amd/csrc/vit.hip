@@ -354,6 +354,8 @@ int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_ep
     if (producer && (variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG)) return variant;
     if (producer && variant == 11) return a.K <= 768 ? GEMM_W2 : GEMM_PP_IMG;  // O-proj two-workgroup, fc2 image-aligned
     if (producer && variant == 12) return a.K <= 768 ? GEMM_W2 : GEMM_PINGPONG;  // = auto (rounds 4 and 5)
+    if (producer && variant == 13) return a.K <= 768 ? 300 : GEMM_PINGPONG;      // O-proj on 128-row W2 tiles only
+    if (producer && variant == 14) return GEMM_W2;                                // fc2 on the two-workgroup kernel too
     if (pick == GEMM_PINGPONG && variant >= 100 && variant < 200) return variant;
     return GEMM_AUTO;
 }
@@ -897,8 +899,9 @@ extern "C" int rc_diag_set_gemm_variant(rc_model *m, int variant) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG ||
-                       variant == 11 || variant == 12 || (variant >= 100 && variant < 200),
-                   RC_ERR_INVALID, "GEMM variant: 0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 100 + ABL");
+                       (variant >= 11 && variant <= 14) || (variant >= 100 && variant < 200),
+                   RC_ERR_INVALID, "GEMM variant: 0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 11-14 producer "
+                                   "mixes, 100 + ABL");
         std::lock_guard<std::mutex> lk(m->mu);
         m->gemm_variant = variant;
     });
