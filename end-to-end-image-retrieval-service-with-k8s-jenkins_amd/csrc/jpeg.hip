@@ -826,20 +826,26 @@ __global__ __launch_bounds__(64 * BAND_WAVES) __attribute__((amdgpu_waves_per_eu
     const int TP = L.tp;
     uint32_t *rowbuf = reinterpret_cast<uint32_t *>(lds + L.rowbuf) + wave * 2 * ((W + 1) & ~1);
     uint8_t *tmp = lds + L.tmp;
-    // horizontal taps of this lane's output columns (MAXT > 0), kept across its wave's rows: the
-    // coefficients and the first tap's pixel xm; tap k reads word xm + k of the row buffer (one
-    // address per column, the taps as immediate offsets).  Taps past a column's count have
-    // coefficient 0, so the words they read past the row's end (at most MAXT - 1: the next row
-    // buffer, or the tmp area after the last) only add 0.
+    // horizontal taps of this lane's output columns (MAXT > 0), kept across its wave's rows and
+    // loaded beside the plane DMA (one wait for both): the coefficients and the first tap's pixel
+    // xm; tap k reads word xm + k of the row buffer (one address per column, the taps as immediate
+    // offsets).  Taps past a column's count have coefficient 0, so the words they read past the
+    // row's end (at most MAXT - 1: the next row buffer, or the tmp area after the last) only add 0.
     int cf[MAXT > 0 ? BAND_NXO : 1][MAXT > 0 ? MAXT : 1], xm[MAXT > 0 ? BAND_NXO : 1];
     if constexpr (MAXT > 0) {
         if (r.need_h) {
+            __builtin_assume(r.hk >= 1);  // (a resize has taps): no branch around the first load
 #pragma unroll
             for (int t = 0; t < BAND_NXO; ++t) {
                 const int xo = min(lane + 64 * t, S - 1);
                 xm[t] = hb[2 * xo];
+                // unguarded loads (the table is padded by BAND_MAXV >= MAXT entries), then the
+                // selects: guarded, each load became a branch with its own vmcnt(0)
+                int v[MAXT];
 #pragma unroll
-                for (int k = 0; k < MAXT; ++k) cf[t][k] = k < r.hk ? hc[xo * r.hk + k] : 0;
+                for (int k = 0; k < MAXT; ++k) v[k] = hc[xo * r.hk + k];
+#pragma unroll
+                for (int k = 0; k < MAXT; ++k) cf[t][k] = k < r.hk ? v[k] : 0;
             }
         }
     }
@@ -1113,8 +1119,10 @@ __global__ __launch_bounds__(64 * BAND_WAVES) __attribute__((amdgpu_waves_per_eu
             // clamped into the band — not one scalar load per tap per 4-byte column
             int cv[BAND_MAXV], ro[BAND_MAXV];
 #pragma unroll
+            for (int k = 0; k < BAND_MAXV; ++k) cv[k] = c[k];  // unguarded loads, then the selects
+#pragma unroll
             for (int k = 0; k < BAND_MAXV; ++k) {
-                cv[k] = k < yn ? c[k] : 0;
+                cv[k] = k < yn ? cv[k] : 0;
                 ro[k] = min(ymin + k, rows - 1) * nw;
             }
             // a column's taps: all T words read first, then the sums (no wait between taps);
