@@ -118,3 +118,28 @@ def test_image_aligned_tiles_match_torch_fp32(cuda, M, K):
     out4 = resid.clone()
     run(EPI_RESID, 4, A, W, bias, M, out4)
     assert torch.equal(out[:M], out4[:M])
+
+
+def test_two_workgroup_160_row_tiles_match_pingpong(cuda):
+    """M = 25 216 (a 128-image slice of a batch): the two-workgroup kernel (variant 8) takes
+    160-row tiles when they need fewer row-rounds of the chip's workgroup slots (on 256 CUs one
+    round of 474 tiles, against two of 591 128-row tiles).  The residual epilogue's values equal
+    the ping-pong kernel's bit for bit (both accumulate K in the same 16x16x32 MFMA order) and
+    fp32 to summation rounding; rows >= M stay untouched."""
+    import torch
+
+    M, N, K = 25216, 768, 768
+    g = torch.Generator(device=cuda).manual_seed(160)
+    Mp = (M + 255) // 256 * 256
+    A = (torch.randn(Mp, K, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
+    A[M:] = 0
+    W = (torch.randn(N, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    resid = torch.randn(Mp, N, device=cuda, generator=g)
+    out_w2, out_pp = resid.clone(), resid.clone()
+    run(EPI_RESID, 8, A, W, bias, M, out_w2)
+    run(EPI_RESID, 4, A, W, bias, M, out_pp)
+    assert torch.equal(out_w2, out_pp)
+    ref = A[:M].float() @ W.float().T + bias
+    assert torch.allclose(out_w2[:M], resid[:M] + ref, atol=1e-4, rtol=1e-4)
+    assert torch.equal(out_w2[M:], resid[M:])
