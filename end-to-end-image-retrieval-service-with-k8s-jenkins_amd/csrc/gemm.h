@@ -80,19 +80,18 @@ __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
 // pair gives lane g the 8 consecutive columns colw + 32c + ln_slice_col(g) — 16-B loads and
 // stores, and exactly the canonical LayerNorm slice of the lane (LN_PARTS), so the block
 // partial is two more swaps (ln_block_reduce_rows).  bq: the bias of those 8 columns.
-// Values: x = (acc + bias) + residual (or + position), the skinny kernel's order.  HL: the
-// residual stream is the bf16 pair (a.ln_x, a.res_lo); otherwise f32 a.out_f32, plus the
-// bf16 copy in a.ln_x and the partials when a.ln_x is set.  All lanes run the swaps; rows
+// Values: x = (acc + bias) + residual (or + position), the skinny kernel's order.  BS: the
+// residual stream is bf16 in a.ln_x (the statistics from the rounded values); otherwise f32
+// a.out_f32, plus the bf16 copy in a.ln_x and the partials when a.ln_x is set.  All lanes run the swaps; rows
 // >= mlim (M, or the end of an image-aligned tile's image) load a clamped row and store nothing.
 template <int EPI, int NR>
 __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4 (&A)[NR][2][2], const int (&rows)[NR],
                                                   int colw, int g, const float4 (&bq)[2][2], int mlim) {
-    constexpr bool HL = epi_hl(EPI);
-    const bool stats = HL ? a.ln_stats != nullptr : a.ln_x != nullptr;
+    constexpr bool BS = epi_bf16_stream(EPI);
+    const bool stats = BS ? a.ln_stats != nullptr : a.ln_x != nullptr;
     const int cl = ln_slice_col(g, 0);
     // every source load of the NR rows first (16 B each), then the arithmetic and stores
     uint4 sh[NR][2];
-    uint2 sl[NR][2];
     float4 sf[NR][2][2];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -102,9 +101,8 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
             const int col = colw + 32 * c + cl;
             if constexpr (epi_resid(EPI)) {
                 const int64_t off = (int64_t)rr * a.N + col;
-                if constexpr (HL) {
+                if constexpr (BS) {
                     sh[r][c] = *reinterpret_cast<const uint4 *>(a.ln_x + off);
-                    sl[r][c] = *reinterpret_cast<const uint2 *>(a.res_lo + off);
                 } else {
                     sf[r][c][0] = *reinterpret_cast<const float4 *>(a.out_f32 + off);
                     sf[r][c][1] = *reinterpret_cast<const float4 *>(a.out_f32 + off + 4);
@@ -141,8 +139,8 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
             const float b[8] = {bq[c][0].x, bq[c][0].y, bq[c][0].z, bq[c][0].w,
                                 bq[c][1].x, bq[c][1].y, bq[c][1].z, bq[c][1].w};
             float add[8];
-            if constexpr (EPI == EPI_RESID_HL) {
-                hl8_value(sh[r][c], sl[r][c], add);
+            if constexpr (EPI == EPI_RESID_BF16) {
+                bf16x8_unpack(sh[r][c], add);
             } else {
                 const float4 s0 = sf[r][c][0], s1 = sf[r][c][1];
                 add[0] = s0.x, add[1] = s0.y, add[2] = s0.z, add[3] = s0.w;
@@ -152,15 +150,11 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
 #pragma unroll
             for (int k = 0; k < 8; ++k) x[k] = (v[k] + b[k]) + add[k];
             const int64_t off = orow * a.N + colw + 32 * c + cl;
-            if constexpr (HL) {
-                uint4 h;
-                uint2 l;
+            if constexpr (BS) {
+                const uint4 h = bf16x8_pack(x);
+                if (ok) *reinterpret_cast<uint4 *>(a.ln_x + off) = h;
                 float xv[8];
-                hl8_split(x, h, l, xv);
-                if (ok) {
-                    *reinterpret_cast<uint4 *>(a.ln_x + off) = h;
-                    *reinterpret_cast<uint2 *>(a.res_lo + off) = l;
-                }
+                bf16x8_unpack(h, xv);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
             } else {
@@ -741,23 +735,29 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
     const int tm = grp * GM + in % gm, tn = in / gm;
     const int m0 = tm * BM, n0 = tn * BN;
     const int K = a.K;
-    const uint16_t *Ag = a.A + (int64_t)m0 * K;
     const uint16_t *Wg = a.W + (int64_t)n0 * K;
 
     // piece p (1 KB = 16 rows x 64 B): 0..MI-1 A rows 16p.., then W rows 16(p-MI)..
     // lane l writes LDS bytes [16 l, 16 l + 16) of the piece: row l >> 2, stored
     // chunk l & 3, which holds source chunk (l & 3) ^ (((l >> 5) & 1) << 1).
+    // A rows past M are clamped to row M - 1 (their results are never stored): a 160-row tile
+    // may reach past the round_up(M, 256) rows the ABI asks callers to provide.
     const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    const uint16_t *srcp[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int piece = wave + 4 * i;  // wave-uniform
+        srcp[i] = piece < MI ? a.A + (int64_t)min(m0 + piece * 16 + prow, a.M - 1) * K
+                             : Wg + (int64_t)((piece - MI) * 16 + prow) * K;
+        srcp[i] += pchunk * 8;
+    }
     auto stage = [&](int slot, int k0) {
         uint8_t *base = smem + slot * SLOT;
 #pragma unroll
         for (int i = 0; i < PPW; ++i) {
             const int piece = wave + 4 * i;  // wave-uniform
             if (piece >= PIECES) continue;
-            const uint16_t *src = piece < MI ? Ag + (int64_t)(piece * 16 + prow) * K
-                                             : Wg + (int64_t)((piece - MI) * 16 + prow) * K;
-            __builtin_amdgcn_global_load_lds((const void *)(src + k0 + pchunk * 8), (lds_void_t *)(base + piece * 1024),
-                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(srcp[i] + k0), (lds_void_t *)(base + piece * 1024), 16, 0, 0);
         }
     };
     // fragment of rows r0 + li (r0 % 16 == 0), k chunk g: 16 B at row*64 + (g ^ h(li))*16
@@ -834,7 +834,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
 // shares), two workgroups per CU; both operands register-staged (one 16-B A load
 // and four 16-B W loads per lane per 32-deep K-step, issued two steps ahead and
 // written to the other LDS slot after the MFMAs of the step before their own).
-// EPI: EPI_PATCH_F32 or EPI_PATCH_HL (the residual stream as bf16 pairs).
+// EPI: EPI_PATCH_F32 or EPI_PATCH_BF16 (the residual stream in bf16).
 template <int P, int EPI>
 __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(GemmArgs a) {
     constexpr int BM = 128, BN = 256, BK = 32, KC = 3 * P * P;
@@ -1137,10 +1137,10 @@ __global__ __launch_bounds__(64) void gemm_skinny_kernel(GemmArgs a) {
         } else {
             v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
         }
-        if constexpr (EPI == EPI_RESID_HL) {  // residual stream as bf16 pairs (LN producers: gemm_skinny_ln_kernel)
+        if constexpr (EPI == EPI_RESID_BF16) {  // residual stream in bf16 (LN producers: gemm_skinny_ln_kernel)
             const int64_t off = (int64_t)row * a.N + c;
-            const float4 r = hl_value(hl_load(a.ln_x + off, a.res_lo + off));
-            hl_store(hl_split(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w)), a.ln_x + off, a.res_lo + off);
+            const float4 r = rs_load4(a.ln_x + off);
+            rs_store4(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w), a.ln_x + off, true);
         } else if constexpr (EPI == EPI_RESID_F32) {
             float4 *o = reinterpret_cast<float4 *>(a.out_f32 + (int64_t)row * a.N + c);
             const float4 r = *o;
@@ -1167,7 +1167,7 @@ __global__ __launch_bounds__(64) void gemm_skinny_kernel(GemmArgs a) {
 // block-major through skinny_block: a column block's weights stay in one XCD): wave w computes
 // rows 16·rt + li, columns 64·blk + 32·w + 16·ni + 4g + e (the skinny kernel's tile and K chain),
 // stores as gemm_skinny_kernel does and puts the value each element now stands for (the stored
-// f32, or hl_value of the stored pair) into LDS; then wave 0 reads the 16 rows' canonical slices
+// f32 or bf16) into LDS; then wave 0 reads the 16 rows' canonical slices
 // (4 lanes per row) and reduces them with ln_block_reduce_quad.  (4-wave blocks of two row
 // tiles: 84 blocks for a lone image's fc2, address-bound on 84 CUs at 34 us.)
 template <int EPI, int KT>
@@ -1196,11 +1196,9 @@ __global__ __launch_bounds__(128) void gemm_skinny_ln_kernel(GemmArgs a) {
         const float v0 = acc[ni][0] + b.x, v1 = acc[ni][1] + b.y, v2 = acc[ni][2] + b.z, v3 = acc[ni][3] + b.w;
         const int64_t off = (int64_t)min(row, a.M - 1) * a.N + c;
         float4 x;
-        if constexpr (EPI == EPI_RESID_HL) {
-            const float4 r = hl_value(hl_load(a.ln_x + off, a.res_lo + off));
-            const uint4 p = hl_split(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w));
-            if (valid) hl_store(p, a.ln_x + off, a.res_lo + off);
-            x = hl_value(p);
+        if constexpr (EPI == EPI_RESID_BF16) {
+            const float4 r = rs_load4(a.ln_x + off);
+            x = rs_store4(make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w), a.ln_x + off, valid);
         } else {
             float4 *o = reinterpret_cast<float4 *>(a.out_f32 + off);
             const float4 r = *o;
@@ -1321,7 +1319,7 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool l
 // it by 2 %).
 inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
 
-// The patch embedding of a small batch (M <= 256 patch rows, the bf16-pair stream: one image is
+// The patch embedding of a small batch (M <= 256 patch rows, the bf16 stream: one image is
 // 196 rows, and patch_gemm_kernel's 128 x 256 tiles put it on 6 workgroups, 33 us): the skinny
 // form.  Block = 2 waves = one 16-row tile x one 64-column LayerNorm block (as
 // gemm_skinny_ln_kernel); wave w takes columns 32w..32w+31.  A fragments are built in registers
@@ -1329,11 +1327,11 @@ inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
 // (ky, kx, c) order, 8 bytes of one image row, each bf16(fma(u, pre_a[k mod 3], pre_b[k mod 3]))
 // exactly as patch_gemm_kernel converts them — and the W rows stream through the LDS-DMA ring;
 // the MFMAs run in the same K order (the same bits).  Epilogue: x = (acc + bias) + position
-// embedding at the patch's token row, stored as the bf16 pair, LN partials of the 64-column
+// embedding at the patch's token row, stored to the bf16 stream, LN partials of the 64-column
 // block through LDS (f32_rows_epilogue's values and canonical slices).
 template <int EPI>
 __global__ __launch_bounds__(128) void patch_skinny_kernel(GemmArgs a) {
-    static_assert(EPI == EPI_PATCH_HL, "the bf16-pair stream");
+    static_assert(EPI == EPI_PATCH_BF16, "the bf16 stream");
     constexpr int NI = 2, P = 16, KC = 3 * P * P, NKB = KC / 64, LP = 68;
     constexpr int SK = SKINNY_DMA_STAGES, SB = 16 * NI * 128;
     __shared__ __attribute__((aligned(16))) uint8_t ring[2][SK * SB];
@@ -1434,9 +1432,7 @@ __global__ __launch_bounds__(128) void patch_skinny_kernel(GemmArgs a) {
         const float4 ps = *reinterpret_cast<const float4 *>(a.pos + (int64_t)(1 + p) * a.N + c);
         const float4 xf = make_float4((acc[ni][0] + bb.x) + ps.x, (acc[ni][1] + bb.y) + ps.y, (acc[ni][2] + bb.z) + ps.z,
                                       (acc[ni][3] + bb.w) + ps.w);
-        const uint4 pr = hl_split(xf);
-        if (valid) hl_store(pr, a.ln_x + orow * a.N + c, a.res_lo + orow * a.N + c);
-        *reinterpret_cast<float4 *>(xs_l + li * LP + wave * 32 + ni * 16 + 4 * g) = hl_value(pr);
+        *reinterpret_cast<float4 *>(xs_l + li * LP + wave * 32 + ni * 16 + 4 * g) = rs_store4(xf, a.ln_x + orow * a.N + c, valid);
     }
     if (a.ln_stats == nullptr) return;  // block-uniform
     __syncthreads();
@@ -1463,12 +1459,12 @@ inline void launch_patch_gemm(const GemmArgs &a, hipStream_t s) {
     RC_REQUIRE(a.img && a.img_size % 16 == 0 && a.N % 256 == 0 && a.K == 3 * 16 * 16 && a.M >= 1,
                RC_ERR_UNSUPPORTED, "patch GEMM: 16x16 patches, N % 256 == 0");
     const int ntm = (a.M + 127) / 128, ntn = a.N / 256;
-    if (a.res_lo != nullptr) {
-        RC_REQUIRE(a.ln_x != nullptr, RC_ERR_INVALID, "bf16-pair residual stream needs ln_x");
+    if (a.resid_bf16) {
+        RC_REQUIRE(a.ln_x != nullptr, RC_ERR_INVALID, "bf16 residual stream needs ln_x");
         if (a.M <= 256 && a.N == 64 * LN_PARTS)  // a small batch: the skinny form (same bits)
-            hipLaunchKernelGGL((patch_skinny_kernel<EPI_PATCH_HL>), dim3(((a.M + 15) / 16) * LN_PARTS), dim3(128), 0, s, a);
+            hipLaunchKernelGGL((patch_skinny_kernel<EPI_PATCH_BF16>), dim3(((a.M + 15) / 16) * LN_PARTS), dim3(128), 0, s, a);
         else
-            hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_HL>), dim3(ntm * ntn), dim3(256), 0, s, a);
+            hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_BF16>), dim3(ntm * ntn), dim3(256), 0, s, a);
     } else {
         hipLaunchKernelGGL((patch_gemm_kernel<16, EPI_PATCH_F32>), dim3(ntm * ntn), dim3(256), 0, s, a);
     }
@@ -1493,8 +1489,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     const int pick = gemm_pick(a, variant, epi_patch(EPI), epi_ln(EPI));
     RC_REQUIRE(a.ldc == 0 || (a.ldc >= a.N && epi_bf16_out(EPI)), RC_ERR_UNSUPPORTED,
                "an output row stride (ldc) needs a bf16 epilogue");
-    if constexpr (epi_hl(EPI)) {
-        RC_REQUIRE(a.ln_x && a.res_lo, RC_ERR_UNSUPPORTED, "bf16-pair residual epilogues need ln_x + res_lo");
+    if constexpr (epi_bf16_stream(EPI)) {
+        RC_REQUIRE(a.ln_x, RC_ERR_UNSUPPORTED, "bf16-stream residual epilogues need ln_x");
     }
     if constexpr (epi_ln(EPI)) {
         bool ln_ok = pick == GEMM_PINGPONG || pick == GEMM_SKINNY;

@@ -2,14 +2,14 @@
 // behind rc_embed (replaces embedding/main.py:97-114's ViTImageProcessor +
 // ViTMSNModel + CLS extraction).
 //
-// HBM layout per model (bf16 GEMM operands, f32 residual stream):
+// HBM layout per model (bf16 GEMM operands, bf16 residual stream under the LayerNorm fold):
 //   weights   W_qkv [3H][H] (q,k,v rows concatenated), W_o [H][H], W_fc1 [MLP][H],
 //             W_fc2 [H][MLP] — bf16, nn.Linear [out][in]; W_patch [H][P·P·3] bf16 with
 //             K ordered (ky, kx, c) for the implicit-GEMM patch embedding;
 //             biases / LayerNorm params / cls / pos — f32
 //   workspace (sized for max_batch images, rows padded to the GEMM tile):
-//             residual stream: under the LayerNorm fold the bf16 pair ln = RNE(x),
-//             res_lo = the low byte of x around ln [Mp][H] u8 with ln_stats f32 [Mp][LN_PARTS][2]; without it
+//             residual stream: under the LayerNorm fold ln = RNE_bf16(x) [Mp][H] with
+//             ln_stats f32 [Mp][LN_PARTS][2]; without it
 //             hidden f32 [Mp][H] and ln bf16 [Mp][H] = LayerNorm output; qkv bf16
 //             [Mp][3H], attn bf16 [Mp][H], mlp bf16 [Mp][MLP]
 #include <algorithm>
@@ -77,7 +77,6 @@ struct rc_model {
     int Mp = 0;
     uint16_t *ln = nullptr, *qkv = nullptr, *attn = nullptr, *mlp = nullptr;
     float *hidden = nullptr;
-    uint8_t *res_lo = nullptr;   // LayerNorm fold: the residual stream's low bytes (vit_kernels.h)
     float *ln_stats = nullptr;     // [Mp][LN_PARTS][2] LayerNorm-fold partials (per 64-column block: mean, M2)
     bool ln_fold = true;           // rc_model_set_ln_fold: LN folded into QKV / fc1 for M > 256 rows
     // last layer on the CLS rows only (compact [max_batch + pad][·] streams)
@@ -376,9 +375,9 @@ void gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role = -1) {
     m->timers[T_GEMM].end(t0, s, flops);
 }
 
-// residual-stream producer GEMM (O-proj, fc2): f32 stream, or bf16 pairs under the fold
+// residual-stream producer GEMM (O-proj, fc2): f32 stream, or bf16 under the fold
 void resid_gemm(rc_model *m, const GemmArgs &a, hipStream_t s, int role) {
-    if (a.res_lo != nullptr) gemm<EPI_RESID_HL>(m, a, s, role);
+    if (a.resid_bf16) gemm<EPI_RESID_BF16>(m, a, s, role);
     else gemm<EPI_RESID_F32>(m, a, s, role);
 }
 
@@ -396,7 +395,7 @@ void layernorm(rc_model *m, const float *x, const float *g, const float *b, uint
 // full-batch ones (a GEMM row's result does not depend on M), so a CLS row gets
 // the same arithmetic as in the full layer except attention's summation order.
 void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *qkv, const float *hidden,
-                    const uint16_t *hi, const uint8_t *lo, const float *st_rows, float scale, hipStream_t s) {
+                    const uint16_t *hi, const float *st_rows, float scale, hipStream_t s) {
     const auto &c = m->cfg;
     const int H = c.hidden, T = m->tokens;
     float *hc = m->cls_hidden + (int64_t)i0 * H;
@@ -408,7 +407,7 @@ void last_layer_cls(rc_model *m, const Layer &L, int i0, int n, const uint16_t *
     const bool q_cls = m->ln_fold && hi != nullptr;
     float *cst = m->cls_stats + (int64_t)i0 * LN_STRIDE;
     uint16_t *qc = m->cls_mlp + (int64_t)i0 * c.mlp;  // [n][H] compact queries (fc1 overwrites it later)
-    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, hi, lo, T, hc, q_cls ? lc : nullptr,
+    hipLaunchKernelGGL(gather_cls_kernel, dim3(n), dim3(H / 4), 0, s, hidden, hi, T, hc, q_cls ? lc : nullptr,
                        st_rows, cst);
     RC_LAUNCH_CHECK();
     if (q_cls) {
@@ -468,18 +467,17 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
     // M <= 256 included), so an image's embedding does not depend on its batch.
     const bool fold = m->ln_fold;
     float *st = m->ln_stats + r0 * LN_STRIDE;
-    uint8_t *lo = fold ? m->res_lo + r0 * H : nullptr;  // the residual stream is the pair (ln, lo)
     auto produce = [&](GemmArgs a, bool emit) {
-        if (fold) {
+        if (fold) {  // the residual stream is `ln` itself (bf16)
             a.ln_x = ln;
-            a.res_lo = lo;
+            a.resid_bf16 = true;
             a.ln_stats = emit ? st : nullptr;
         }
         return a;
     };
     // 2. embeddings: CLS + pos, patch GEMM (+bias +pos) into the residual stream
     hipLaunchKernelGGL(cls_init_kernel, dim3(n), dim3(256), 0, s, hidden, T, H, m->cls, m->pos, fold ? ln : nullptr,
-                       fold ? st : nullptr, lo);
+                       fold ? st : nullptr);
     RC_LAUNCH_CHECK();
     {
         GemmArgs a = produce(GemmArgs{nullptr, m->w_patch, m->b_patch, n * m->npatch, H, m->kpatch, nullptr, hidden, m->pos,
@@ -514,7 +512,7 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             gemm<EPI_BF16>(m, GemmArgs{ln, L.w_qkv, L.b_qkv, M, 3 * H, H, qkv, nullptr, nullptr, T}, s, T_QKV);
         }
         if (m->cls_only_last && l == c.layers - 1) {
-            last_layer_cls(m, L, i0, n, qkv, hidden, fold ? ln : nullptr, lo, st, scale, s);
+            last_layer_cls(m, L, i0, n, qkv, hidden, fold ? ln : nullptr, st, scale, s);
             break;
         }
         const int ta = m->timers[T_ATTN].begin(s);
@@ -561,8 +559,8 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
     }
     // 4. final LayerNorm on the CLS rows → raw (the /embed body) and L2-normalised copy
     const float *fin = m->cls_only_last ? m->cls_hidden + (int64_t)i0 * H : hidden;
-    const bool pair = fold && !m->cls_only_last;
-    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, fin, pair ? ln : nullptr, pair ? lo : nullptr,
+    const bool bf16_rows = fold && !m->cls_only_last;
+    hipLaunchKernelGGL(cls_final_kernel<3>, dim3(n), dim3(64), 0, s, fin, bf16_rows ? ln : nullptr,
                        m->cls_only_last ? 1 : T, m->lnf_w, m->lnf_b,
                        c.ln_eps,
                        raw + (int64_t)i0 * H, normed ? normed + (int64_t)i0 * H : nullptr);
@@ -626,7 +624,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             m->ln_stats = (float *)m->alloc((size_t)m->Mp * LN_STRIDE * 4);
             RC_HIP(hipMemset(m->ln_stats, 0, (size_t)m->Mp * LN_STRIDE * 4));  // pad rows: finite scales
             m->ln = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
-            m->res_lo = (uint8_t *)m->alloc((size_t)m->Mp * H);
             m->qkv = (uint16_t *)m->alloc((size_t)m->Mp * 3 * H * 2);
             m->attn = (uint16_t *)m->alloc((size_t)m->Mp * H * 2);
             m->mlp = (uint16_t *)m->alloc((size_t)m->Mp * cfg->mlp * 2);
@@ -646,7 +643,6 @@ int rc_model_create(int device, const rc_vit_config *cfg, rc_model **out) {
             // pad rows are read by the GEMM tiles: keep them finite (zero) forever
             RC_HIP(hipMemset(m->hidden, 0, (size_t)m->Mp * H * 4));
             RC_HIP(hipMemset(m->ln, 0, (size_t)m->Mp * H * 2));
-            RC_HIP(hipMemset(m->res_lo, 0, (size_t)m->Mp * H));
             RC_HIP(hipMemset(m->qkv, 0, (size_t)m->Mp * 3 * H * 2));
             RC_HIP(hipMemset(m->attn, 0, (size_t)m->Mp * H * 2));
             RC_HIP(hipMemset(m->mlp, 0, (size_t)m->Mp * cfg->mlp * 2));

@@ -26,14 +26,14 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
 
 // EPI_BF16_LN / EPI_GELU_BF16_LN: the bf16 epilogues as consumers of the LayerNorm fold
-// EPI_RESID_HL / EPI_PATCH_HL: the residual-stream producers with the stream kept as bf16
-// pairs (see "Residual stream as bf16 pairs"; GemmArgs::res_lo)
+// EPI_RESID_BF16 / EPI_PATCH_BF16: the residual-stream producers with the stream kept in bf16
+// (see "Residual stream in bf16"; GemmArgs::ln_x)
 enum GemmEpi { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2, EPI_PATCH_F32 = 3, EPI_BF16_LN = 4, EPI_GELU_BF16_LN = 5,
-               EPI_RESID_HL = 6, EPI_PATCH_HL = 7 };
+               EPI_RESID_BF16 = 6, EPI_PATCH_BF16 = 7 };
 constexpr bool epi_bf16_out(int e) { return e == EPI_BF16 || e == EPI_GELU_BF16 || e == EPI_BF16_LN || e == EPI_GELU_BF16_LN; }
-constexpr bool epi_resid(int e) { return e == EPI_RESID_F32 || e == EPI_RESID_HL; }
-constexpr bool epi_patch(int e) { return e == EPI_PATCH_F32 || e == EPI_PATCH_HL; }
-constexpr bool epi_hl(int e) { return e == EPI_RESID_HL || e == EPI_PATCH_HL; }
+constexpr bool epi_resid(int e) { return e == EPI_RESID_F32 || e == EPI_RESID_BF16; }
+constexpr bool epi_patch(int e) { return e == EPI_PATCH_F32 || e == EPI_PATCH_BF16; }
+constexpr bool epi_bf16_stream(int e) { return e == EPI_RESID_BF16 || e == EPI_PATCH_BF16; }
 constexpr bool epi_gelu(int e) { return e == EPI_GELU_BF16 || e == EPI_GELU_BF16_LN; }
 constexpr bool epi_ln(int e) { return e == EPI_BF16_LN || e == EPI_GELU_BF16_LN; }
 
@@ -59,10 +59,10 @@ struct GemmArgs {
     //     epilogue applies rstd·(acc − μ·c) + bias with μ, rstd from ln_stats[row][LN_PARTS][2]
     uint16_t *ln_x = nullptr;
     float *ln_stats = nullptr;
-    //   EPI_RESID_HL / EPI_PATCH_HL: the residual stream is the pair (ln_x, res_lo) instead
-    //     of out_f32 (see "Residual stream as bf16 pairs"): the residual is read from and the
-    //     result written to the pair; the statistics only when ln_stats != null
-    uint8_t *res_lo = nullptr;
+    //   EPI_RESID_BF16 / EPI_PATCH_BF16 (resid_bf16): the residual stream is ln_x itself, bf16,
+    //     instead of out_f32 (see "Residual stream in bf16"): the residual is read from and the
+    //     result written to ln_x; the statistics only when ln_stats != null
+    bool resid_bf16 = false;
     const float *ln_c = nullptr;
     float ln_eps = 1e-6f;
     // implicit-GEMM patch embedding (patch_gemm_kernel): A[m][k] is read from the u8
@@ -100,65 +100,27 @@ constexpr int LN_PARTS = 12;            // 768 columns / 64
 constexpr int LN_STRIDE = 2 * LN_PARTS;  // floats of partials per row
 __device__ __forceinline__ int ln_slice_col(int g, int c) { return 32 * c + 16 * (g & 1) + 8 * (g >> 1); }
 
-// ------------------------------------------- Residual stream as bf16 pairs
-// Under the LayerNorm fold the residual stream x is kept as hi = RNE_bf16(x) — exactly the
-// bf16(x) the QKV / fc1 GEMMs read as A — plus a one-byte low part: the residual x − hi,
-// which RNE bounds by half an ulp of hi, as q = rint((x − hi) / s) with s = ulp(hi) / 256
-// (|q| <= 127).  The value is x′ = hi + q·s (exact in f32), 16 significant bits (|x − x′|
-// <= ulp(hi) / 512 <= 2⁻¹⁶|x|, against the 2⁻⁹ of the bf16 GEMM operands).  Producers
-// (patch GEMM, O-proj, fc2, cls_init) write 3 B per element and the residual epilogues read
-// 3 B (round 2 kept lo as a second bf16: 4 B each way).  Every reader forms x′ with hl_value's
-// arithmetic, and the producers compute the LN statistics from that same x′, so the skinny
-// (gemm_skinny_ln_kernel) and tiled paths stay bit-identical.
+// ------------------------------------------- Residual stream in bf16
+// Under the LayerNorm fold the residual stream x is kept as bf16 RNE(x) alone — exactly the
+// bf16(x) the QKV / fc1 GEMMs read as A.  Producers (patch GEMM, O-proj, fc2, cls_init) round
+// once and write 2 B per element; the residual epilogues read 2 B.  Every producer computes the
+// LN statistics from the rounded value it stored, so the skinny (gemm_skinny_ln_kernel) and
+// tiled paths stay bit-identical.  (Rounds 2-5 kept a low part beside it — a second bf16, then
+// one byte, ~2^-16 relative — at 6 B per element per epilogue and ~20 more VALU ops per element;
+// the bf16 stream costs 1.8e-4 cosine against the fp32 oracle where the pair gave 1.0e-4,
+// tools/resid_precision_sim.py, inside the 1e-3 fp32 tier.)
 __device__ __forceinline__ float4 bf16x4_f32(uint2 u) {
     return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                        __uint_as_float(u.y & 0xffff0000u));
 }
 __device__ __forceinline__ uint2 pack_bf16x4(float4 v) { return make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)); }
-// s = ulp(h) / 256 = 2^(E − 142) for h's biased exponent E (0 below E = 16: one saturating
-// subtract of the exponent field), and 1 / s = 2^(142 − E).  Below E = 16 (|h| < 2^-111) the
-// inverse is a meaningless finite number: the byte it yields is never used, since s = 0 there.
-__device__ __forceinline__ float hl_step(float h) {
-    const uint32_t e = __float_as_uint(h) & 0x7f800000u;
-    return __uint_as_float(__builtin_elementwise_sub_sat(e, 15u << 23));
-}
-__device__ __forceinline__ float hl_inv_step(float h) {
-    const uint32_t e = __float_as_uint(h) & 0x7f800000u;
-    return __uint_as_float((269u << 23) - e);
-}
-// q = rint((x − h) / s) clamped to [−127, 127], as a float (exact)
-__device__ __forceinline__ float hl_qf(float x, float h) {
-    return fminf(fmaxf(rintf((x - h) * hl_inv_step(h)), -127.f), 127.f);
-}
-// the low byte of x around h = RNE_bf16(x), and the value a (h, byte) pair stands for
-__device__ __forceinline__ uint32_t hl_code(float x, float h) { return (uint32_t)(int)hl_qf(x, h) & 0xffu; }
-// the low bytes of four codes (as ints) packed little-endian: three v_perm_b32
-__device__ __forceinline__ uint32_t hl_pack4(int c0, int c1, int c2, int c3) {
-    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)c1, (uint32_t)c0, 0x0c0c0400u);
-    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)c3, (uint32_t)c2, 0x0c0c0400u);
-    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-}
-__device__ __forceinline__ float hl_decode(float h, uint32_t byte) {
-    return fmaf((float)(int)(int8_t)(uint8_t)byte, hl_step(h), h);
-}
-// four consecutive elements: (hi.x, hi.y, the four lo bytes, unused)
-__device__ __forceinline__ uint4 hl_split(float4 x) {
+// four consecutive stream elements -> f32
+__device__ __forceinline__ float4 rs_load4(const uint16_t *p) { return bf16x4_f32(*reinterpret_cast<const uint2 *>(p)); }
+// round four values to the stream, store them when `valid`; returns the value stored
+__device__ __forceinline__ float4 rs_store4(float4 x, uint16_t *p, bool valid) {
     const uint2 h = pack_bf16x4(x);
-    const float4 hf = bf16x4_f32(h);
-    const uint32_t lo = hl_pack4((int)hl_qf(x.x, hf.x), (int)hl_qf(x.y, hf.y), (int)hl_qf(x.z, hf.z), (int)hl_qf(x.w, hf.w));
-    return make_uint4(h.x, h.y, lo, 0u);
-}
-__device__ __forceinline__ float4 hl_value(uint4 p) {
-    const float4 h = bf16x4_f32(make_uint2(p.x, p.y));
-    return make_float4(hl_decode(h.x, p.z), hl_decode(h.y, p.z >> 8), hl_decode(h.z, p.z >> 16), hl_decode(h.w, p.z >> 24));
-}
-__device__ __forceinline__ uint4 hl_load(const uint16_t *hi, const uint8_t *lo) {
-    const uint2 h = *reinterpret_cast<const uint2 *>(hi);
-    return make_uint4(h.x, h.y, *reinterpret_cast<const uint32_t *>(lo), 0u);
-}
-__device__ __forceinline__ void hl_store(uint4 p, uint16_t *hi, uint8_t *lo) {
-    *reinterpret_cast<uint2 *>(hi) = make_uint2(p.x, p.y);
-    *reinterpret_cast<uint32_t *>(lo) = p.z;
+    if (valid) *reinterpret_cast<uint2 *>(p) = h;
+    return bf16x4_f32(h);
 }
 
 // 8 bf16 (one 16-B load) <-> 8 f32
@@ -173,28 +135,6 @@ __device__ __forceinline__ void bf16x8_unpack(uint4 u, float (&f)[8]) {
 __device__ __forceinline__ uint4 bf16x8_pack(const float (&f)[8]) {
     return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
 }
-// the pair of 8 consecutive elements (16 B of hi, 8 B of lo bytes) -> x′ (hl_value's arithmetic)
-__device__ __forceinline__ void hl8_value(uint4 hi, uint2 lo, float (&x)[8]) {
-    float h[8];
-    bf16x8_unpack(hi, h);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = hl_decode(h[k], (k < 4 ? lo.x : lo.y) >> (8 * (k & 3)));
-}
-// hl_split of 8 elements; xv receives the value the pair stands for (hl_value of the result)
-__device__ __forceinline__ void hl8_split(const float (&x)[8], uint4 &hi, uint2 &lo, float (&xv)[8]) {
-    hi = bf16x8_pack(x);
-    float hf[8];
-    bf16x8_unpack(hi, hf);
-    int c[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {  // the decode reuses q as a float: hl_decode's value, no byte round trip
-        const float qf = hl_qf(x[k], hf[k]);
-        c[k] = (int)qf;
-        xv[k] = fmaf(qf, hl_step(hf[k]), hf[k]);
-    }
-    lo = make_uint2(hl_pack4(c[0], c[1], c[2], c[3]), hl_pack4(c[4], c[5], c[6], c[7]));
-}
-
 // (mean, M2) of one canonical 16-column slice (x[8c + k] = column 32c + slice offset + k).
 // Written with explicit fmaf and no multiply-add left to the compiler's contraction, so
 // every kernel that inlines it rounds identically.
@@ -303,9 +243,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
 
 // Final LayerNorm of the CLS row of each image + the two /embed outputs.
 template <int NV>
-// hi != null: the rows are the bf16 pairs (hi, lo) instead of `hidden`.
+// hi != null: the rows are the bf16 residual stream `hi` instead of `hidden`.
 __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
-                                                      const uint8_t *__restrict__ lo, int tokens,
+                                                      int tokens,
                                                       const float *__restrict__ g, const float *__restrict__ b,
                                                       float eps, float *__restrict__ raw, float *__restrict__ normed) {
     constexpr int H = 256 * NV;
@@ -317,7 +257,7 @@ __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-        v[i] = hi ? hl_value(hl_load(hi + r0 + 4 * (lane + 64 * i), lo + r0 + 4 * (lane + 64 * i))) : xr[lane + 64 * i];
+        v[i] = hi ? rs_load4(hi + r0 + 4 * (lane + 64 * i)) : xr[lane + 64 * i];
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
     const float mean = wave_sum(s) * (1.0f / H);
@@ -352,18 +292,17 @@ __global__ __launch_bounds__(64) void cls_final_kernel(const float *__restrict__
     }
 }
 
-// hidden[img*tokens + 0] = cls + pos[0]; with ln_x: also its bf16 copy and LN partials
-// (the LayerNorm fold's producer for the CLS rows; H = 768: 48 lanes, one canonical
-// slice each, see LN_PARTS); with lo: the row as the bf16 pair (ln_x, lo) and no f32 row
+// hidden[img*tokens + 0] = cls + pos[0]; with ln_x: the row into the bf16 residual stream
+// instead, plus its LN partials (the LayerNorm fold's producer for the CLS rows; H = 768: 48
+// lanes, one canonical slice each, see LN_PARTS)
 __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidden, int tokens, int H,
                                                       const float *__restrict__ cls, const float *__restrict__ pos,
-                                                      uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats,
-                                                      uint8_t *__restrict__ lo) {
+                                                      uint16_t *__restrict__ ln_x, float *__restrict__ ln_stats) {
     const int img = blockIdx.x;
     const int64_t row = (int64_t)img * tokens;
-    if (lo == nullptr) {
+    if (ln_x == nullptr) {
         for (int c = threadIdx.x; c < H; c += 256) hidden[row * H + c] = cls[c] + pos[c];
-        if (ln_x == nullptr) return;
+        return;
     }
     if (threadIdx.x >= 64) return;  // one wave: lanes 0-47 = (block, slice), 48-63 only join the shuffles
     const int t = threadIdx.x, g = t & 3, ok = t < 4 * LN_PARTS;
@@ -375,22 +314,12 @@ __global__ __launch_bounds__(256) void cls_init_kernel(float *__restrict__ hidde
         float x[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) x[k] = cls[col + k] + pos[col + k];
-        if (lo != nullptr) {
-            uint4 h;
-            uint2 l;
-            float xv[8];
-            hl8_split(x, h, l, xv);
-            if (ok) {
-                *reinterpret_cast<uint4 *>(ln_x + row * H + col) = h;
-                *reinterpret_cast<uint2 *>(lo + row * H + col) = l;
-            }
+        const uint4 h = bf16x8_pack(x);
+        if (ok) *reinterpret_cast<uint4 *>(ln_x + row * H + col) = h;
+        float xv[8];
+        bf16x8_unpack(h, xv);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
-        } else {
-            if (ok) *reinterpret_cast<uint4 *>(ln_x + row * H + col) = bf16x8_pack(x);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) xs[8 * c + k] = x[k];
-        }
+        for (int k = 0; k < 8; ++k) xs[8 * c + k] = xv[k];
     }
     const float2 st = ln_block_reduce_quad(ln_slice_stats(xs), g);
     if (ok && g == 0) *reinterpret_cast<float2 *>(ln_stats + row * LN_STRIDE + 2 * blk) = st;
@@ -709,7 +638,7 @@ __global__ __launch_bounds__(256, 2) void attention_v3_kernel(const uint16_t *__
 // With hc_ln: also the CLS rows' bf16 hi and LN statistics, compact (the A operand and
 // row scales of the last layer's CLS-only Q GEMM).
 __global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict__ hidden, const uint16_t *__restrict__ hi,
-                                                        const uint8_t *__restrict__ lo, int tokens, float *__restrict__ hc,
+                                                        int tokens, float *__restrict__ hc,
                                                         uint16_t *__restrict__ hc_ln, const float *__restrict__ st,
                                                         float *__restrict__ hc_st) {
     constexpr int H = 768;
@@ -721,7 +650,7 @@ __global__ __launch_bounds__(192) void gather_cls_kernel(const float *__restrict
             hc_st[img * LN_STRIDE + threadIdx.x] = st[(int64_t)img * tokens * LN_STRIDE + threadIdx.x];
     }
     reinterpret_cast<float4 *>(hc + (int64_t)img * H)[threadIdx.x] =
-        hi ? hl_value(hl_load(hi + r0 + 4 * threadIdx.x, lo + r0 + 4 * threadIdx.x))
+        hi ? rs_load4(hi + r0 + 4 * threadIdx.x)
            : reinterpret_cast<const float4 *>(hidden + r0)[threadIdx.x];
 }
 

@@ -143,3 +143,24 @@ def test_two_workgroup_160_row_tiles_match_pingpong(cuda):
     ref = A[:M].float() @ W.float().T + bias
     assert torch.allclose(out_w2[:M], resid[:M] + ref, atol=1e-4, rtol=1e-4)
     assert torch.equal(out_w2[M:], resid[M:])
+
+
+def test_two_workgroup_160_row_tiles_clamp_rows_past_m(cuda):
+    """M = 25 344 = 99 * 256: the 160-row tiles (159 row tiles) reach 96 rows past M, beyond the
+    round_up(M, 256) = M rows the ABI asks the caller for.  The kernel clamps those A rows to row
+    M - 1 (results never stored), so an A buffer of exactly M rows is enough; the outputs equal
+    the ping-pong kernel's bit for bit."""
+    import torch
+
+    M, N, K = 25344, 768, 768
+    g = torch.Generator(device=cuda).manual_seed(161)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    resid = torch.randn(M, N, device=cuda, generator=g)
+    out_w2, out_pp = resid.clone(), resid.clone()
+    run(EPI_RESID, 8, A, W, bias, M, out_w2)
+    run(EPI_RESID, 4, A, W, bias, M, out_pp)
+    assert torch.equal(out_w2, out_pp)
+    ref = A.float() @ W.float().T + bias
+    assert torch.allclose(out_w2, resid + ref, atol=1e-4, rtol=1e-4)
