@@ -204,6 +204,46 @@ def cpu_jpeg_baseline(datas: list[bytes], budget_s: float = 4.0):
             "sample": f"{done} decodes of the same 224x224 JPEGs with Pillow (the reference's own decode), {el:.1f}s"}
 
 
+def cpu_ingest_baseline(total_images: int, budget_s: float = 15.0, index_rows: int = 10_000):
+    """Config 5's CPU baseline: the reference's per-image ingest path (ingesting/main.py:101-168 —
+    one upload at a time: PIL decode, the embedding pod's ViTImageProcessor + fp32 ViTMSNModel at
+    batch 1 (embedding/main.py:97-114), then index.upsert of one vector) on the host cores, with a
+    numpy array standing in for Pinecone's upsert (L2-normalised row written at its slot; GCS upload
+    and HTTP hops omitted, which only flatters the CPU).  Timed on a bounded sample of synthetic
+    224x224 JPEGs and extrapolated linearly to `total_images`."""
+    import torch
+    from PIL import Image
+
+    from oracle.preprocess import preprocess
+    from oracle.weights import seeded_vit_msn_weights
+
+    threads = _torch_threads()
+    sd = {k: torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32)) for k, v in seeded_vit_msn_weights(0).items()}
+    fwd = torch_vit_forward_pixels(sd)
+    datas = synthetic_jpegs(16, seed=55)
+    X = np.zeros((index_rows, 768), np.float32)
+
+    def one(i):
+        im = np.asarray(Image.open(io.BytesIO(datas[i % len(datas)])).convert("RGB"))
+        with torch.inference_mode():
+            v = fwd(torch.from_numpy(preprocess(im)[None]))[0].numpy()
+        X[i % index_rows] = v / max(float(np.linalg.norm(v)), 1e-12)
+
+    one(0)  # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or done == 0:
+        one(done)
+        done += 1
+    el = time.perf_counter() - t0
+    rate = done / el
+    return {"value": rate, "unit": "images/s", "cores": threads, "kind": "reference-lib", "cpu": cpu_model_name(),
+            "extrapolated_hours": total_images / rate / 3600.0, "extrapolated_images": total_images,
+            "sample": f"{done} synthetic 224x224 q90 JPEGs one at a time: PIL decode + ViTImageProcessor arithmetic "
+                      f"(numpy restatement, bit-exact) + torch fp32 ViT-MSN-base forward at batch 1 + upsert of the "
+                      f"L2-normalised vector into a numpy index, {el:.1f}s; extrapolated linearly to "
+                      f"{total_images:,} images (BASELINE config 5)"}
+
+
 def cpu_search_baseline(n_rows=1_000_000, dim=512, budget_s=6.0):
     from threadpoolctl import threadpool_info
 
@@ -986,6 +1026,8 @@ def main():
         log("bench: stage: CPU baselines")
         try:
             result["cpu_baseline"] = cpu_embed_baseline()
+            if result.get("ingest") is not None:
+                result["ingest"]["cpu_baseline"] = cpu_ingest_baseline(10_000_000)
             if "search" in result:
                 result["search"]["cpu_baseline"] = cpu_search_baseline()
                 if "batched" in result["search"]:

@@ -131,6 +131,7 @@ SIGNATURES = {
     "rc_model_set_parts": (C.c_int, [_vp, _i32]),
     "rc_model_set_last_layer": (C.c_int, [_vp, _i32]),
     "rc_model_set_ln_fold": (C.c_int, [_vp, _i32]),
+    "rc_model_set_graphs": (C.c_int, [_vp, _i32]),
     "rc_model_timing": (C.c_int, [_vp, _i32]),
     "rc_model_timing_read": (C.c_int, [_vp, _i32, _pd, _pi64, _pd]),
     "rc_model_timing_reset": (C.c_int, [_vp]),

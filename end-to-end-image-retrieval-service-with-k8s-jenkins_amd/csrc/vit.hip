@@ -95,6 +95,23 @@ struct rc_model {
     int split_min = 32;            // fewest images per part
     hipStream_t sp[4] = {};        // streams of parts 1..3 (part 0 runs on the caller's stream)
     hipEvent_t ev_fork = nullptr, ev_join[4] = {};
+    // Batch-1 launch chains replayed as HIP graphs (rc_model_set_graphs): one instantiated graph per
+    // (images, raw, normed) buffer triple, least recently used evicted past kMaxGraphs.  The graph
+    // bakes every pointer and setting into its kernel arguments, so every setter clears the cache.
+    struct EmbedGraph {
+        const uint8_t *images;
+        float *raw, *normed;
+        hipGraphExec_t exec;
+        uint64_t last;
+    };
+    static constexpr int kMaxGraphs = 8;
+    bool use_graphs = true;
+    std::vector<EmbedGraph> graphs;
+    uint64_t graph_tick = 0;
+    void clear_graphs() {
+        for (auto &g : graphs) (void)hipGraphExecDestroy(g.exec);
+        graphs.clear();
+    }
 
     void *alloc(size_t bytes) {
         void *p = dmalloc(bytes);
@@ -102,6 +119,7 @@ struct rc_model {
         return p;
     }
     ~rc_model() {
+        clear_graphs();
         for (auto &t : timers) t.destroy();
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (auto &e : ev_join)
@@ -596,6 +614,52 @@ void forward(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
     }
 }
 
+// One image already at the model's input size: the ~70-kernel chain of forward() captured once
+// per buffer triple on a model-owned stream (capture is refused on the legacy default stream, which
+// the caller's may be), then replayed on the caller's stream with one hipGraphLaunch — the host
+// issues one launch per request instead of ~70 (the reference's /embed is batch 1 by
+// construction, embedding/main.py:88-124).  The same kernels and arguments: the same bits.
+bool graph_eligible(const rc_model *m, int n, int h, int w) {
+    if (!m->use_graphs || n != 1 || h != m->cfg.image_size || w != m->cfg.image_size) return false;
+    for (const auto &t : m->timers)
+        if (t.enabled) return false;  // event timing needs the stream form
+    return true;
+}
+
+void forward_graph(rc_model *m, const uint8_t *images, float *raw, float *normed, hipStream_t s) {
+    rc_model::EmbedGraph *e = nullptr;
+    for (auto &g : m->graphs)
+        if (g.images == images && g.raw == raw && g.normed == normed) e = &g;
+    if (e == nullptr) {
+        if ((int)m->graphs.size() >= rc_model::kMaxGraphs) {
+            auto old = std::min_element(m->graphs.begin(), m->graphs.end(),
+                                        [](const auto &a, const auto &b) { return a.last < b.last; });
+            (void)hipGraphExecDestroy(old->exec);
+            m->graphs.erase(old);
+        }
+        hipStream_t cs = m->sp[1];
+        const int S = m->cfg.image_size;
+        RC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        hipGraph_t g = nullptr;
+        try {
+            forward(m, images, 1, S, S, raw, normed, cs);
+        } catch (...) {
+            (void)hipStreamEndCapture(cs, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        RC_HIP(hipStreamEndCapture(cs, &g));
+        hipGraphExec_t ex = nullptr;
+        const hipError_t err = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        RC_HIP(err);
+        m->graphs.push_back({images, raw, normed, ex, 0});
+        e = &m->graphs.back();
+    }
+    e->last = ++m->graph_tick;
+    RC_HIP(hipGraphLaunch(e->exec, s));
+}
+
 }  // namespace
 
 extern "C" {
@@ -673,6 +737,7 @@ int rc_model_set_weight(rc_model *m, const char *name, const float *host_data, i
     return guard([&] {
         RC_REQUIRE(m && name && host_data, RC_ERR_INVALID, "null argument");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         const std::string key = canonical_name(name);
         auto it = m->shapes.find(key);
         RC_REQUIRE(it != m->shapes.end(), RC_ERR_INVALID, std::string("unknown weight name: ") + name);
@@ -689,6 +754,7 @@ int rc_model_set_preprocess(rc_model *m, int resample, double rescale_factor, co
         RC_REQUIRE(resample == RC_RESAMPLE_BICUBIC || resample == RC_RESAMPLE_BILINEAR, RC_ERR_UNSUPPORTED,
                    "resample must be BICUBIC (3) or BILINEAR (2)");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         DeviceScope ds(m->device);
         const int old_resample = m->resample;
         const double old_rescale = m->rescale;
@@ -719,6 +785,7 @@ int rc_model_finalize(rc_model *m) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         DeviceScope ds(m->device);
         for (auto &kv : m->shapes)
             RC_REQUIRE(m->host.count(kv.first), RC_ERR_STATE, "weight not set: " + kv.first);
@@ -787,7 +854,20 @@ int rc_embed(rc_model *m, const uint8_t *images, int n, int h, int w, float *raw
         std::lock_guard<std::mutex> lk(m->mu);
         RC_REQUIRE(m->ready, RC_ERR_STATE, "model weights not finalized");
         DeviceScope ds(m->device);
-        forward(m, images, n, h, w, raw_out, normed_out, (hipStream_t)stream);
+        if (graph_eligible(m, n, h, w))
+            forward_graph(m, images, raw_out, normed_out, (hipStream_t)stream);
+        else
+            forward(m, images, n, h, w, raw_out, normed_out, (hipStream_t)stream);
+    });
+}
+
+int rc_model_set_graphs(rc_model *m, int on) {
+    return guard([&] {
+        RC_REQUIRE(m, RC_ERR_INVALID, "null model");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        m->clear_graphs();
+        m->use_graphs = on != 0;
     });
 }
 
@@ -841,6 +921,7 @@ int rc_model_set_parts(rc_model *m, int parts) {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         RC_REQUIRE(parts >= 1 && parts <= kMaxParts, RC_ERR_INVALID, "parts must be in [1, 4]");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         m->split = parts;
     });
 }
@@ -849,6 +930,7 @@ int rc_model_set_ln_fold(rc_model *m, int on) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         m->ln_fold = on != 0;
     });
 }
@@ -857,6 +939,7 @@ int rc_model_set_last_layer(rc_model *m, int cls_only) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         m->cls_only_last = cls_only != 0;
     });
 }
@@ -885,6 +968,7 @@ extern "C" int rc_diag_set_attention(rc_model *m, int form) {
     return guard([&] {
         RC_REQUIRE(m && (form == 2 || form == 3), RC_ERR_INVALID, "attention form must be 2 or 3");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         m->attn_form = form;
     });
 }
@@ -899,6 +983,7 @@ extern "C" int rc_diag_set_gemm_variant(rc_model *m, int variant) {
                    RC_ERR_INVALID, "GEMM variant: 0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 11-14 producer "
                                    "mixes, 100 + ABL");
         std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
         m->gemm_variant = variant;
     });
 }

@@ -160,7 +160,8 @@ def embed_many(blobs: List[bytes]) -> list[list[float]]:
         host = torch.empty((1, emb.hidden), dtype=torch.float32, pin_memory=True)
         emb.embed_images(images, out=(host, None))
         torch.cuda.current_stream(emb.device).synchronize()
-        a = host.numpy()
+        a = host.numpy().copy()  # 3 KB: the pinned block goes back to torch's pool now, not when
+        # the caller drops the embedding (ingest results, caches)
     else:
         raw, _ = _embed_decoded(images)
         a = raw.cpu().numpy()

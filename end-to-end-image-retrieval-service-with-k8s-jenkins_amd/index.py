@@ -231,8 +231,9 @@ class Record(dict):
     (``retriever/utils.py:62-65``), so building 5 x 768 Python floats per request is work no
     caller of that path sees.  Every read path of the dict — ``[]``, ``get``, ``items``,
     ``values``, iteration with ``dict(...)`` / ``{**m}``, ``==``, ``copy``, ``repr``, pickling,
-    ``json.dumps`` (which calls ``items()`` on a dict subclass) — first turns the row into the
-    list of Python floats a plain dict would hold, once."""
+    ``json.dumps`` (which calls ``items()`` on a dict subclass), ``|`` — first turns the row into
+    the list of Python floats a plain dict would hold, once; writing or deleting ``"values"``
+    drops the pending row, and ``update`` / ``|=`` load it first."""
 
     __slots__ = ("_row",)
 
@@ -284,6 +285,34 @@ class Record(dict):
     def setdefault(self, key, default=None):
         self._load()
         return dict.setdefault(self, key, default)
+
+    # writes: a new "values" (or its removal) supersedes the pending row, so the row must not
+    # come back on the next read; any other key leaves it pending
+    def __setitem__(self, key, value):
+        if key == "values":
+            self._row = None
+        dict.__setitem__(self, key, value)
+
+    def __delitem__(self, key):
+        if key == "values":
+            self._row = None
+        dict.__delitem__(self, key)
+
+    def update(self, *a, **kw):
+        self._load()
+        dict.update(self, *a, **kw)
+
+    def __or__(self, other):
+        self._load()
+        return dict(dict.items(self)) | dict(other)
+
+    def __ror__(self, other):
+        self._load()
+        return dict(other) | dict(dict.items(self))
+
+    def __ior__(self, other):
+        self.update(other)
+        return self
 
     def __eq__(self, other):
         self._load()
@@ -546,7 +575,10 @@ class ShardSet:
             bufs = (sc, rw, val, ptrs)
             self._qbufs[key] = bufs
         sc, rw, val, ptrs = bufs
-        check(self._query_fn(self._h, q.ctypes.data, nq, n_rows, k, ptrs[0], ptrs[1], ptrs[2], ptrs[3]))
+        h = self._h
+        if h is None:
+            raise RuntimeError("index is closed")
+        check(self._query_fn(h, q.ctypes.data, nq, n_rows, k, ptrs[0], ptrs[1], ptrs[2], ptrs[3]))
         return sc, rw, val
 
     def fetch_rows(self, rows, stored: bool = False) -> torch.Tensor:

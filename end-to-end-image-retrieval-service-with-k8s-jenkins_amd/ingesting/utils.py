@@ -76,3 +76,11 @@ def embed_locally(image_bytes: bytes) -> list:
     from ..embedding.main import embed_bytes
 
     return embed_bytes(image_bytes)
+
+
+# embed_bytes validates the upload as the reference's routes do before embedding (embedding/main.py:
+# decode_many: UnidentifiedImageError -> 400 "Uploaded file is not a valid image." before the model;
+# a stream the GPU decoder rejects goes to PIL, whose other errors propagate as 500), so
+# /search_image need not decode it on the host first (retriever/main.py:111-117 does, because its
+# embed is a remote call)
+embed_locally.validates_image = True

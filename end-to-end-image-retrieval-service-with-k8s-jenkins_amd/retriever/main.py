@@ -7,7 +7,8 @@ Contract kept (``retriever/main.py:94-169``):
                       ([] when the index has no match); 400 "Uploaded file is not a valid
                       image."; 422 without ``file``
 
-Flow as in the reference: validation decode (``:111-117``) → ``get_feature_vector``
+Flow as in the reference: validation decode (``:111-117``; folded into the in-process embed,
+which validates with the same 400 body before the model runs) → ``get_feature_vector``
 (``:122``; in process by default, see ingesting.main) → ``search(index, feature,
 top_k=Config.TOP_K)`` (``:128``, the HIP exact top-k) → ``index.fetch(ids)``
 (``:142``) → one URL per match from its ``gcs_path`` metadata (``:148-168``; the
@@ -62,11 +63,15 @@ async def search_image(request: Request):
     if f is None:
         raise RequestValidationError([{"type": "missing", "loc": ("body", "file"), "msg": "Field required",
                                        "input": None}])
-    try:
-        Image.open(BytesIO(f.data)).convert("RGB")
-    except UnidentifiedImageError:
-        raise HTTPException(status_code=400, detail="Uploaded file is not a valid image.")
-    feature = _feature_fn(request)(f.data)
+    feature_fn = _feature_fn(request)
+    if not getattr(feature_fn, "validates_image", False):
+        try:
+            Image.open(BytesIO(f.data)).convert("RGB")
+        except UnidentifiedImageError:
+            raise HTTPException(status_code=400, detail="Uploaded file is not a valid image.")
+    # else: the in-process embed validates the upload itself, with this route's 400 body, before
+    # the model runs — a GPU-decodable JPEG is decoded once (on the GPU) instead of twice
+    feature = feature_fn(f.data)
     ix = index()
     match_ids = search(ix, feature, top_k=Config.TOP_K)
     if not match_ids:

@@ -364,6 +364,11 @@ class VitMsnEmbedder:
         """Run the last encoder layer on the CLS rows only (default) or on every row."""
         check(self.lib.rc_model_set_last_layer(self._h, int(bool(cls_only))))
 
+    def set_graphs(self, on: bool) -> None:
+        """Replay a one-image embed's launch chain as a captured HIP graph (default) or launch
+        every kernel from the host (the same bits)."""
+        check(self.lib.rc_model_set_graphs(self._h, int(bool(on))))
+
     def set_gemm_variant(self, variant: int) -> None:
         """Diagnostic builds only (tools/build_diag.sh, RC_LIB_PATH): the A/B kernel of the
         full-batch projections (0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 100 + ABL).
@@ -571,6 +576,10 @@ class EmbedderPool:
     def set_last_layer(self, cls_only: bool) -> None:
         for m in self.members:
             m.set_last_layer(cls_only)
+
+    def set_graphs(self, on: bool) -> None:
+        for m in self.members:
+            m.set_graphs(on)
 
 
 def gflop_per_image(cfg: dict = VIT_MSN_BASE, cls_only_last: bool = False) -> float:

@@ -287,6 +287,13 @@ int rc_model_set_last_layer(rc_model *m, int cls_only);
  * parity tests). */
 int rc_model_set_ln_fold(rc_model *m, int on);
 
+/* Batch-1 HIP graphs (default 1): an rc_embed of one image at the model's input size
+ * (the reference's /embed request, embedding/main.py:88-124) replays a HIP graph of its
+ * launch chain, captured on first use per (images, raw_out, normed_out) buffer triple
+ * (at most 8 kept, least recently used evicted): one host launch per request instead of
+ * ~70.  Same kernels, same bits.  Every setter drops the captured graphs.  0 = stream form. */
+int rc_model_set_graphs(rc_model *m, int on);
+
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
  * kernel ids: 0 = all GEMMs, 1 = fc1 GEMM, 2 = attention, 3 = layernorm,
  * 4 = preprocess, 5 = QKV GEMM, 6 = O-proj GEMM, 7 = fc2 GEMM (5-7 and 1: the

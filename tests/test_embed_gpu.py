@@ -320,3 +320,46 @@ def test_image_aligned_tiles_batch_invariant(vitmod, weights12, cuda):
     for j, i in enumerate((0, 1, 150, 299)):
         assert torch.equal(a[i:i + 1], ones[j]), i
     m.close()
+
+
+def test_batch1_graph_replay_matches_stream_form(vitmod, weights12, cuda):
+    """A one-image embed replays a captured HIP graph (rc_model_set_graphs, default on): the same
+    bits as the stream form, for new contents in the same buffers (the graph reads them at replay),
+    for a second buffer triple (a second graph), into pinned host memory, and after a setter (which
+    drops the captured graphs: the replay follows the new setting)."""
+    import torch
+
+    rng = np.random.default_rng(31)
+    imgs = torch.from_numpy(rng.integers(0, 256, (3, 224, 224, 3), dtype=np.uint8)).to(cuda)
+    m = vitmod.VitMsnEmbedder(weights12, device=0, max_batch=4)
+    x = torch.empty((1, 224, 224, 3), dtype=torch.uint8, device=cuda)
+    raw, nrm = torch.empty((1, 768), device=cuda), torch.empty((1, 768), device=cuda)
+    ref = {}
+    m.set_graphs(False)
+    for i in range(3):
+        ref[i] = [t.clone() for t in m.embed(imgs[i:i + 1])]
+    m.set_last_layer(False)
+    full_ref = m.embed(imgs[0:1])[0].clone()
+    m.set_last_layer(True)
+    m.set_graphs(True)
+    for rep in range(2):
+        for i in range(3):
+            x.copy_(imgs[i:i + 1])
+            m.embed(x, out=(raw, nrm))
+            torch.cuda.synchronize()
+            assert torch.equal(raw, ref[i][0]) and torch.equal(nrm, ref[i][1]), (rep, i)
+    raw2 = torch.empty((1, 768), device=cuda)
+    m.embed(imgs[1:2], out=(raw2, None))
+    torch.cuda.synchronize()
+    assert torch.equal(raw2, ref[1][0])
+    host = torch.empty((1, 768), dtype=torch.float32, pin_memory=True)
+    x.copy_(imgs[2:3])
+    m.embed(x, out=(host, None))
+    torch.cuda.synchronize()
+    assert torch.equal(host, ref[2][0].cpu())
+    m.set_last_layer(False)
+    x.copy_(imgs[0:1])
+    m.embed(x, out=(raw, nrm))
+    torch.cuda.synchronize()
+    assert torch.equal(raw, full_ref)
+    m.close()

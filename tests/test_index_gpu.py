@@ -208,3 +208,30 @@ def test_query_host_values_follow_each_query(idxmod, cuda):
         for i, w in zip(ids, want):
             assert np.array_equal(np.asarray(got[i]["values"], np.float32), w)
     ix.close()
+
+
+@pytest.mark.parametrize("n,k,cluster", [(100_000, 100, True), (32_768, 100, False), (100_000, 256, True)])
+def test_merge_heads_fallback_paths(idxmod, cuda, n, k, cluster):
+    """merge_heads_kernel's two rarely-taken paths, checked against the oracle: (a) the true top-k
+    packed into one scan block's contiguous rows (near-duplicates ingested back to back), so the
+    heads' threshold admits more than CAP candidates and the block falls back to the full merge;
+    (b) fewer lists than k (64 lists of 512 rows, k = 100): the heads' k-th key is EMPTY, every key
+    qualifies, and the full merge runs again."""
+    import torch
+
+    rng = np.random.default_rng(n + k)
+    dim = 512
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    Q = rng.standard_normal((2, dim)).astype(np.float32)
+    if cluster:
+        r0 = 1024  # rows 1024 .. 1024 + k - 1: all inside the third 512-row scan block
+        X[r0:r0 + k] = Q[0] + 0.05 * rng.standard_normal((k, dim)).astype(np.float32)
+    dev = idxmod.DeviceIndex(dim, capacity=n, device=cuda)
+    dev.upsert_rows(torch.from_numpy(X), torch.arange(n, dtype=torch.int64))
+    s, r = dev.search(torch.from_numpy(Q), k, n)
+    torch.cuda.synchronize()
+    Xs = dev.stored_rows(n).cpu().numpy()
+    _check(dev, Xs, Q, k, s, r)
+    if cluster:
+        assert sorted(r.cpu().numpy()[0].tolist()) == list(range(1024, 1024 + k))
+    dev.close()

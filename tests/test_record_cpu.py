@@ -90,3 +90,29 @@ def test_f32list_carries_its_row_until_mutated():
     w = ix.F32List(row.tolist(), row)
     w += [1.0]
     assert w.f32 is None
+
+
+def test_record_writes_drop_or_load_the_pending_row():
+    """Writing or deleting "values" supersedes the pending row (it must not come back on the next
+    read); update / |= / | see the loaded list, as on a plain dict."""
+    r, plain = _rec()
+    r["values"] = [1.0]
+    assert r["values"] == [1.0] and r._row is None
+    r, _ = _rec()
+    r.update(values=[2.0])
+    assert r["values"] == [2.0]
+    r, _ = _rec()
+    r.update({"score": 0.5})
+    assert r["values"] == plain["values"] and r["score"] == 0.5
+    r, _ = _rec()
+    del r["values"]
+    assert "values" not in r and r.get("values") is None and r == {k: v for k, v in plain.items() if k != "values"}
+    r, _ = _rec()
+    assert (r | {"score": 0.1})["values"] == plain["values"] and type(r | {}) is dict
+    assert ({"x": 1} | r)["values"] == plain["values"]
+    r, _ = _rec()
+    r |= {"values": [3.0]}
+    assert r["values"] == [3.0] and isinstance(r, import_pkg("index").Record)
+    r, _ = _rec()
+    r["metadata"] = {"gcs_path": "b"}
+    assert r["values"] == plain["values"]

@@ -142,3 +142,22 @@ def test_embed_route_by_value_seed1907_checkpoint(svc, fixture_jpeg, cuda, tmp_p
         assert got.shape == (768,) and 1.0 - cos < 1e-3, 1.0 - cos
     finally:
         emb.reset_embedder()
+
+
+@pytest.mark.gpu
+def test_search_image_truncated_jpeg_is_a_500(fixture_jpeg, cuda, monkeypatch):
+    """/search_image no longer decodes the upload on the host before the in-process embed (which
+    validates it itself): a truncated baseline JPEG passes the GPU decoder's header probe, the GPU
+    decoder rejects the damaged scan, PIL decides — and PIL's OSError propagates as a 500, as the
+    reference's validation decode (retriever/main.py:111-117) lets it; a non-image stays a 400."""
+    cfg = import_pkg("config").Config
+    monkeypatch.setattr(cfg, "INDEX_NAME", "truncated-jpeg-search")
+    jpeg = import_pkg("jpeg")
+    bad = fixture_jpeg[: len(fixture_jpeg) // 2]
+    assert jpeg.is_gpu_decodable(bad)
+    client = TestClient(import_pkg("service").app, raise_server_exceptions=False)
+    r = client.post("/search_image", files={"file": ("t.jpeg", bad, "image/jpeg")})
+    assert r.status_code == 500
+    r = client.post("/search_image", files={"file": ("a.jpg", b"This is not an image.", "image/jpeg")})
+    assert r.status_code == 400 and r.json()["detail"] == "Uploaded file is not a valid image."
+    import_pkg("ingesting.utils")._indexes.pop("truncated-jpeg-search", None)

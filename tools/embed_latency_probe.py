@@ -38,7 +38,14 @@ if "--trace-only" in sys.argv:  # for rocprofv3 --stats: 10 warm + 100 embed_byt
     r = lat(lambda: emb.embed_bytes(data), reps=100, warm=10)
     print(json.dumps({"embed_bytes": r, "calls": 110}), flush=True)
     sys.exit(0)
-out = {"embed_bytes": lat(lambda: emb.embed_bytes(data))}
+out = {}
+if hasattr(m, "set_graphs"):  # graph replay of the batch-1 chain vs the stream form, interleaved
+    for rnd in range(3):
+        for on in (False, True):
+            m.set_graphs(on)
+            out.setdefault(f"embed_bytes_graphs{int(on)}", []).append(lat(lambda: emb.embed_bytes(data))["p50_ms"])
+    m.set_graphs(True)
+out["embed_bytes"] = lat(lambda: emb.embed_bytes(data))
 dec = m._decoder()
 out["huffman_coefficients_host"] = lat(lambda: J.decode_coefficients(data))
 out["gpu_decode_resized"] = lat(lambda: (dec.decode_resized([data], 224, 3), torch.cuda.synchronize()))
