@@ -375,15 +375,19 @@ def latency_lines(pkg: str, reps: int = 40, cpu: bool = True):
     from fastapi.testclient import TestClient
 
     log("bench: latency /search_image")
-    client = TestClient(retmain.app)
     old_index = retmain.index
     retmain.index = lambda: ix
     try:
-        def post():
-            r = client.post("/search_image", files={"file": ("test_image.jpeg", data, "image/jpeg")})
-            assert r.status_code == 200 and len(r.json()) == 5
-        out["search_image"] = dict(_lat(post, reps), what="POST /search_image through the FastAPI app (TestClient): "
-                                   "validation decode, GPU embed, exact top-5, fetch, 5 URLs")
+        # one TestClient session (its event-loop thread kept across requests, as a served app keeps
+        # its loop): without the context manager TestClient starts a thread and an event loop per
+        # request, ~0.8 ms that no deployment pays (tools/search_image_breakdown.py)
+        with TestClient(retmain.app) as client:
+            def post():
+                r = client.post("/search_image", files={"file": ("test_image.jpeg", data, "image/jpeg")})
+                assert r.status_code == 200 and len(r.json()) == 5
+            out["search_image"] = dict(_lat(post, reps), what="POST /search_image through the FastAPI app (one "
+                                       "TestClient session): multipart parse, GPU decode + embed (validating the "
+                                       "upload), exact top-5, fetch, 5 URLs")
     finally:
         retmain.index = old_index
     if cpu:

@@ -579,6 +579,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     RC_STAMP(sb, RC_NOW());
     RC_STAMP(sb + 4, (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) | ((uint64_t)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32));
     RC_STAMP(sb + 5, (uint64_t)tm | ((uint64_t)tn << 32));
+    if constexpr ((ABL & (128 | 256)) != 0) {
+        // diagnostic: staggered start — the first round's workgroups on every other CU of an XCD
+        // (block b runs on XCD b % 8, consecutive b / 8 on neighbouring CUs) wait ~half a tile, so
+        // later rounds' epilogue store bursts fall beside other CUs' K loops
+        constexpr uint64_t D = (ABL & 128) ? 1000 : 500;  // s_memrealtime ticks (100 MHz)
+        if (blockIdx.x < 256 && ((blockIdx.x >> 3) & 1)) {
+            const uint64_t t0 = RC_NOW();
+            while (RC_NOW() - t0 < D) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     float4 biasr[2][2];
     pp_bias_regs<EPI>(a, n0, biasr, threadIdx.x);
     pp_kloop<EPI, ABL, BM>(a, smem, m0, n0, 0, NKT > 0 ? NKT : a.K / PP_BK, acc, threadIdx.x, sb + 1);
@@ -1576,7 +1586,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case 100 + 0: case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
-        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: {
+        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: {
             a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256;
             switch (variant - 100) {
@@ -1593,6 +1603,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 case 32: launch_pp<EPI, 32, PP_BM>(a, ntm, s); break;
                 case 64: launch_pp<EPI, 64, PP_BM>(a, ntm, s); break;
                 case 96: launch_pp<EPI, 96, PP_BM>(a, ntm, s); break;
+                case 50: launch_pp<EPI, 128, PP_BM>(a, ntm, s); break;  // staggered start, ~10 us
+                case 51: launch_pp<EPI, 256, PP_BM>(a, ntm, s); break;  // staggered start, ~5 us
             }
             break;
         }

@@ -2,8 +2,10 @@
 whole request through the FastAPI app (TestClient, in process, as bench.py's latency line) and of
 each step timed alone on the same fixture JPEG over config 1's 10k x 768 index:
 
-  testclient_floor  a POST of the same multipart body to a route that only reads it (TestClient +
-                    Starlette + the request/response plumbing every route pays)
+  request           the whole POST through one TestClient session (its event-loop thread kept)
+  request_new_portal the same without the session: TestClient starts a thread + event loop per request
+  testclient_floor  a POST of the same multipart body to a route that only reads it (one session:
+                    TestClient + Starlette + the request/response plumbing every route pays)
   multipart_parse   parse_form of that body
   host_validation   PIL open + convert (the reference's validation decode; the route now skips it
                     when the in-process embed validates, see retriever/main.py)
@@ -61,13 +63,31 @@ def main():
                      [{"gcs_path": f"images/r{i}.jpg"} for i in range(len(X))])
     out = {}
     client = TestClient(retmain.app)
+    if "--profile" in sys.argv:  # where the request's host time goes, by function (cProfile)
+        import cProfile
+        import pstats
+
+        retmain.index = lambda: ix
+        client.__enter__()  # one session, as the bench line
+        post_ = lambda: client.post("/search_image", files={"file": ("test_image.jpeg", data, "image/jpeg")})  # noqa: E731
+        for _ in range(10):
+            post_()
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(100):
+            post_()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
+        return
     old_index = retmain.index
     retmain.index = lambda: ix
     try:
-        def post():
-            r = client.post("/search_image", files={"file": ("test_image.jpeg", data, "image/jpeg")})
+        def post(c):
+            r = c.post("/search_image", files={"file": ("test_image.jpeg", data, "image/jpeg")})
             assert r.status_code == 200 and len(r.json()) == 5
-        out["request"] = p50(post)
+        with TestClient(retmain.app) as session:
+            out["request"] = p50(lambda: post(session))
+        out["request_new_portal"] = p50(lambda: post(client))
     finally:
         retmain.index = old_index
 
@@ -80,8 +100,8 @@ def main():
         seen["ctype"] = request.headers.get("content-type", "")
         return []
 
-    fc = TestClient(floor_app)
-    out["testclient_floor"] = p50(lambda: fc.post("/echo", files={"file": ("test_image.jpeg", data, "image/jpeg")}))
+    with TestClient(floor_app) as fc:
+        out["testclient_floor"] = p50(lambda: fc.post("/echo", files={"file": ("test_image.jpeg", data, "image/jpeg")}))
     body, ctype = seen["body"], seen["ctype"]
     out["multipart_parse"] = p50(lambda: mp.parse_form(body, ctype))
     out["host_validation"] = p50(lambda: Image.open(BytesIO(data)).convert("RGB"))
