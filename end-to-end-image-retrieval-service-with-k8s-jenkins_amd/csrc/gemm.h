@@ -610,17 +610,23 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // Epilogue of a 128 x 256 tile held as acc[mi][ni] by 4 waves (wave w: columns
 // [64w, 64w + 64)): acc[mi][ni][j] = C[m0 + mi*16 + li][n0 + w*64 + ni*16 + 4g + j].
 // The bf16 epilogues stage through `smem` (>= 64 KB; the caller's main loop must be done
-// with it); the f32 ones store from the accumulators.
+// with it); the f32 ones store from the accumulators.  LayerNorm-fold consumers (EPI_*_LN): the
+// tile rows' (rstd, -rstd*mu) at smem + ln_off, as gemm_pp_kernel keeps them, and the same
+// rstd·(acc − μ·c) + b′ arithmetic (the same bits).
 template <int EPI, int MI = 8>
-__device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][4], uint8_t *smem, int m0, int n0) {
+__device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][4], uint8_t *smem, int m0, int n0,
+                                            int ln_off = 0) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
-    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+    if constexpr (epi_bf16_out(EPI)) {
         static_assert(MI == 8, "bf16 epilogues stage a 128-row tile");
-        float4 bias[4];
+        float4 bias[4], lc[4];
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
+        for (int ni = 0; ni < 4; ++ni) {
+            bias[ni] = *reinterpret_cast<const float4 *>(a.bias + n0 + wave * 64 + ni * 16 + 4 * g);
+            if constexpr (epi_ln(EPI)) lc[ni] = *reinterpret_cast<const float4 *>(a.ln_c + n0 + wave * 64 + ni * 16 + 4 * g);
+        }
         __syncthreads();  // every wave's last fragment reads are done: the ring is free
         // 128 x 256 bf16 tile staged in LDS (512-B rows, 16-B chunk XOR (row & 31)),
         // stored as whole 512-B row segments, 16 B per lane.
@@ -631,8 +637,17 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][
             for (int mi = 0; mi < 8; ++mi) {
                 const int rl = mi * 16 + li;
                 const f32x4 v4 = acc[mi][ni];
-                float v0 = v4[0] + bias[ni].x, v1 = v4[1] + bias[ni].y, v2 = v4[2] + bias[ni].z, v3 = v4[3] + bias[ni].w;
-                if constexpr (EPI == EPI_GELU_BF16) {
+                float v0, v1, v2, v3;
+                if constexpr (epi_ln(EPI)) {  // rstd·(acc − μ·c) + b′
+                    const float2 r = *reinterpret_cast<const float2 *>(smem + ln_off + rl * 8);
+                    v0 = fmaf(r.x, v4[0], fmaf(r.y, lc[ni].x, bias[ni].x));
+                    v1 = fmaf(r.x, v4[1], fmaf(r.y, lc[ni].y, bias[ni].y));
+                    v2 = fmaf(r.x, v4[2], fmaf(r.y, lc[ni].z, bias[ni].z));
+                    v3 = fmaf(r.x, v4[3], fmaf(r.y, lc[ni].w, bias[ni].w));
+                } else {
+                    v0 = v4[0] + bias[ni].x, v1 = v4[1] + bias[ni].y, v2 = v4[2] + bias[ni].z, v3 = v4[3] + bias[ni].w;
+                }
+                if constexpr (epi_gelu(EPI)) {
                     const f32x2 lo = gelu_fast2(f32x2{v0, v1}), hi = gelu_fast2(f32x2{v2, v3});
                     v0 = lo.x;
                     v1 = lo.y;
@@ -726,7 +741,9 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
     constexpr int A_BYTES = BM * BK * 2, SLOT = A_BYTES + BN * BK * 2;  // 8 (10) KB + 16 KB
     constexpr int PIECES = SLOT / 1024;                                  // 24 (26) pieces: A then W
     constexpr int PPW = (PIECES + 3) / 4, PPW_LO = PIECES / 4;           // pieces of waves < PIECES % 4 / the rest
-    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * SLOT];  // 72 (78) KB
+    constexpr int LN_OFF = NSLOT * SLOT, LN_LDS = epi_ln(EPI) ? BM * 8 : 0;  // LN-fold row scales behind the ring
+    static_assert(!epi_ln(EPI) || LN_OFF >= 64 * 1024, "the staged bf16 tile must not reach the row scales");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * SLOT + LN_LDS];  // 72 (78) KB (+ 1 KB)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -782,6 +799,11 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
     const int nk = K / BK;
     stage(0, 0);
     if (nk > 1) stage(1, BK);
+    if constexpr (epi_ln(EPI)) {  // this tile's row scales, as gemm_pp_kernel's prologue (visible after the loop's barriers)
+        if (tid < BM)
+            *reinterpret_cast<float2 *>(smem + LN_OFF + tid * 8) =
+                ln_row_scale(a.ln_stats + (int64_t)min(m0 + tid, a.M - 1) * LN_STRIDE, a.ln_eps);
+    }
     for (int kt = 0; kt < nk; ++kt) {
         // a raw s_barrier: __syncthreads() would add a full vmcnt(0) drain (its
         // release fence), emptying the DMA pipeline every K-step.  The next slot's pieces of this
@@ -826,7 +848,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
             for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
         return;
     }
-    w2_epilogue<EPI, MI>(a, acc, smem, m0, n0);
+    w2_epilogue<EPI, MI>(a, acc, smem, m0, n0, LN_OFF);
 }
 
 // ------------------------------------------- implicit-GEMM patch embedding ----
@@ -1505,14 +1527,20 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
     if constexpr (epi_ln(EPI)) {
         bool ln_ok = pick == GEMM_PINGPONG || pick == GEMM_SKINNY;
 #if defined(RC_GEMM_ABLATION)
-        ln_ok = ln_ok || (pick >= 100 && pick < 200);  // gemm_pp_kernel<EPI, ABL>
+        ln_ok = ln_ok || (pick >= 100 && pick < 200) || pick == GEMM_W2;  // gemm_pp_kernel<EPI, ABL>, round-6 W2 A/B
 #endif
         RC_REQUIRE(ln_ok && a.ln_c && a.ln_stats, RC_ERR_UNSUPPORTED,
                    "LayerNorm-fold consumers run on the ping-pong or skinny kernel");
     }
     switch (pick) {
         case GEMM_W2: {
-            if constexpr (!epi_ln(EPI)) {
+#if !defined(RC_GEMM_ABLATION)
+            // LayerNorm-fold consumers on this kernel: diagnostic builds only (round 6 in-model A/B,
+            // bit-identical: fc1 302 vs 273 us, QKV 206 vs 183 on the ping-pong kernel)
+            if constexpr (epi_ln(EPI)) throw Error(RC_ERR_UNSUPPORTED, "LayerNorm-fold consumers: ping-pong or skinny kernel");
+            else
+#endif
+            {
                 RC_REQUIRE(a.N % 256 == 0, RC_ERR_UNSUPPORTED, "GEMM N must be a multiple of 256");
                 RC_REQUIRE(a.K % 32 == 0, RC_ERR_UNSUPPORTED, "GEMM K must be a multiple of 32");
                 const int ntn = a.N / 256;
