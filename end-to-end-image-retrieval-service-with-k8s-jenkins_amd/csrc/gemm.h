@@ -1135,18 +1135,21 @@ __device__ __forceinline__ int skinny_block(int b, int nwg) {
 
 // One wave per block: the loads are address-bound (PMC: the texture addresser busy for the
 // whole launch on the CUs holding blocks), so a tile per CU where 4-wave blocks put four.
-template <int EPI, int NI, int KT>
-__global__ __launch_bounds__(64) void gemm_skinny_kernel(GemmArgs a) {
+// WPB > 1 (diagnostic builds): WPB consecutive tiles per block, one wave and one DMA ring each —
+// a one-image fc1 is 1 248 one-wave workgroups (the same bits either way).
+template <int EPI, int NI, int KT, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB) void gemm_skinny_kernel(GemmArgs a) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int wave = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
     const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
-    const int w = skinny_block(blockIdx.x, gridDim.x);
+    const int w = skinny_block(blockIdx.x, gridDim.x) * WPB + wave;
     if (w >= nct * nrt) return;
     const int ct = w / nrt, rt = w % nrt;
     const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
     f32x4 acc[NI];
     if constexpr (KT > 0) {
-        __shared__ __attribute__((aligned(16))) uint8_t ring[SKINNY_DMA_STAGES * skinny_dma_stage_bytes<NI>()];
-        skinny_chain_dma<NI, KT / 64>(a.A, rt * 16, a.M, a.W, n0, K, ring, acc);
+        __shared__ __attribute__((aligned(16))) uint8_t ring[WPB][SKINNY_DMA_STAGES * skinny_dma_stage_bytes<NI>()];
+        skinny_chain_dma<NI, KT / 64>(a.A, rt * 16, a.M, a.W, n0, K, ring[wave], acc);
     } else {
         const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
         const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
@@ -1350,6 +1353,10 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool l
 // 256, interleaved A/B in tools/gemm_calib.py), row-major otherwise (fc2 prefers
 // it by 2 %).
 inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
+
+#if defined(RC_GEMM_ABLATION)
+inline int g_skinny_wpb = 1;  // diagnostic builds: tiles (waves) per skinny-GEMM block (rc_diag_set_skinny_wpb)
+#endif
 
 // The patch embedding of a small batch (M <= 256 patch rows, the bf16 stream: one image is
 // 196 rows, and patch_gemm_kernel's 128 x 256 tiles put it on 6 workgroups, 33 us): the skinny
@@ -1572,6 +1579,20 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 }
             }
             const dim3 gr(((a.M + 15) / 16) * (a.N / 32));  // one wave (tile) per block
+#if defined(RC_GEMM_ABLATION)
+            if (g_skinny_wpb > 1 && (a.K == 768 || a.K == 3072)) {  // diagnostic: WPB tiles per block
+                const unsigned nb = (unsigned)(((a.M + 15) / 16) * (a.N / 32) + g_skinny_wpb - 1) / g_skinny_wpb;
+                if (g_skinny_wpb == 2 && a.K == 768)
+                    hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768, 2>), dim3(nb), dim3(128), 0, s, a);
+                else if (g_skinny_wpb == 2)
+                    hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072, 2>), dim3(nb), dim3(128), 0, s, a);
+                else if (a.K == 768)
+                    hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768, 4>), dim3(nb), dim3(256), 0, s, a);
+                else
+                    hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072, 4>), dim3(nb), dim3(256), 0, s, a);
+                break;
+            }
+#endif
             if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768>), gr, dim3(64), 0, s, a);
             else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072>), gr, dim3(64), 0, s, a);
             else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 0>), gr, dim3(64), 0, s, a);

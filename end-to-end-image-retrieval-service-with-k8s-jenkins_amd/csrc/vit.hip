@@ -966,6 +966,16 @@ extern "C" int rc_diag_set_stamps(void *dev) {
     return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rc_stamps), &dev, sizeof(dev))); });
 }
 
+// diagnostic builds: tiles (one wave each) per block of the skinny GEMM (1, the product's; 2; 4)
+extern "C" int rc_diag_set_skinny_wpb(rc_model *m, int wpb) {
+    return guard([&] {
+        RC_REQUIRE(m && (wpb == 1 || wpb == 2 || wpb == 4), RC_ERR_INVALID, "skinny waves per block: 1, 2 or 4");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
+        g_skinny_wpb = wpb;
+    });
+}
+
 // diagnostic builds: attention_v2_kernel (2, the product's) or attention_v3_kernel (3, lost the
 // A/B) for the full-token layers (the same bits)
 extern "C" int rc_diag_set_attention(rc_model *m, int form) {
