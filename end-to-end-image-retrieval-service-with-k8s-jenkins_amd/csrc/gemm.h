@@ -194,8 +194,8 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
     // swapped with v_permlane16_swap so each lane stores 16 B (8 consecutive columns);
     // lane (g, li) of rows 16-block holds columns 4g..4g+3 of both 16-column halves ni, the
     // swap of rows 1<->0 and 3<->2 between the ni halves makes them 8 contiguous columns.
-    // (Also ABL 64 for the other bf16 epilogues in diagnostic builds.)
-    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN || (epi_bf16_out(EPI) && (ABL & 64) != 0 && !epi_ln(EPI));
+    // (Also ABL 64 for the other bf16 epilogues, QKV's LN consumer included, in diagnostic builds.)
+    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN || (epi_bf16_out(EPI) && (ABL & 64) != 0);
     if constexpr (DIRECT) {
         float4 bq[2][2], cq[2][2];
 #pragma unroll
