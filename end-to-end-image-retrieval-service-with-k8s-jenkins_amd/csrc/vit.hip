@@ -546,6 +546,12 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
             const int nb = std::min(items, 2 * m->ncu);
             hipLaunchKernelGGL(attention_v3_kernel<197>, dim3(nb), dim3(256), 0, s, qkv, attn, T, c.heads, items,
                                scale * 1.4426950408889634f);
+        } else if (m->attn_form == 4 && T == 197) {  // v2, co-resident blocks staggered by ~6 us
+            hipLaunchKernelGGL((attention_v2_kernel<197, 600>), dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f, qsplit);
+        } else if (m->attn_form == 5 && T == 197) {  // ~3 us
+            hipLaunchKernelGGL((attention_v2_kernel<197, 300>), dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f, qsplit);
         } else
 #endif
         if (T == 197) {
@@ -980,7 +986,7 @@ extern "C" int rc_diag_set_skinny_wpb(rc_model *m, int wpb) {
 // A/B) for the full-token layers (the same bits)
 extern "C" int rc_diag_set_attention(rc_model *m, int form) {
     return guard([&] {
-        RC_REQUIRE(m && (form == 2 || form == 3), RC_ERR_INVALID, "attention form must be 2 or 3");
+        RC_REQUIRE(m && form >= 2 && form <= 5, RC_ERR_INVALID, "attention form must be 2 (v2), 3 (v3), 4 / 5 (v2 staggered)");
         std::lock_guard<std::mutex> lk(m->mu);
         m->clear_graphs();
         m->attn_form = form;

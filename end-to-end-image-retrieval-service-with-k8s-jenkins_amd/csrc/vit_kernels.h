@@ -443,9 +443,19 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
 // qsplit > 1 (small batches: a lone image is 12 (image, head) items for 256 CUs): block b is
 // part b % qsplit of item b / qsplit and takes query tiles qs·4 + wave, stepping 4·qsplit — each
 // part stages the head's K and V (L2 hits after the first) and runs the same per-tile arithmetic.
-template <int TOK>
+// STAG > 0 (diagnostic builds): the first round's second and third blocks of each CU (blockIdx
+// 256..767 under the dispatcher's round-robin placement) start STAG and 2·STAG s_memrealtime
+// ticks (10 ns) late, so that co-resident blocks are out of phase (one's K/V DMA under the others'
+// math) for the rest of the launch.
+template <int TOK, int STAG = 0>
 __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
                                                           int tokens_rt, int heads, float scale_log2e, int qsplit) {
+    if constexpr (STAG > 0) {
+        if (blockIdx.x >= 256 && blockIdx.x < 768) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), d = (uint64_t)STAG * (blockIdx.x >> 8);
+            while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     constexpr int W = 4, HALF = W / 2, HD = 64, PPW = ATT2_TILES * 2 / HALF;  // 13 DMA pieces per wave
     const int tokens = TOK > 0 ? TOK : tokens_rt;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * ATT2_ROWS * 128];

@@ -27,7 +27,7 @@ g = torch.Generator(device=dev).manual_seed(1)
 imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
 raw = torch.empty((B, 768), device=dev)
 nrm = torch.empty((B, 768), device=dev)
-forms = [2, 3]
+forms = [int(f) for f in os.environ.get("FORMS", "2,3").split(",")]
 res = {f: {"step_ms": [], "attn_us": []} for f in forms}
 ref = None
 for r in range(rounds):
