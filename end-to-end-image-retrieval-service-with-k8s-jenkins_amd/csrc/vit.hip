@@ -972,6 +972,25 @@ extern "C" int rc_diag_set_stamps(void *dev) {
     return guard([&] { RC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rc_stamps), &dev, sizeof(dev))); });
 }
 
+// diagnostic builds: the priority of the part streams 1..3 (part 0 runs on the caller's stream):
+// -1 = higher than the default, 1 = lower, 0 = default (the product's)
+extern "C" int rc_diag_set_part_priority(rc_model *m, int prio) {
+    return guard([&] {
+        RC_REQUIRE(m && prio >= -1 && prio <= 1, RC_ERR_INVALID, "part priority: -1, 0 or 1");
+        std::lock_guard<std::mutex> lk(m->mu);
+        DeviceScope ds(m->device);
+        m->clear_graphs();
+        int lo = 0, hi = 0;
+        RC_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        const int pr = prio < 0 ? hi : (prio > 0 ? lo : 0);
+        RC_HIP(hipDeviceSynchronize());
+        for (int p = 1; p < kMaxParts; ++p) {
+            RC_HIP(hipStreamDestroy(m->sp[p]));
+            RC_HIP(hipStreamCreateWithPriority(&m->sp[p], hipStreamNonBlocking, pr));
+        }
+    });
+}
+
 // diagnostic builds: tiles (one wave each) per block of the skinny GEMM (1, the product's; 2; 4)
 extern "C" int rc_diag_set_skinny_wpb(rc_model *m, int wpb) {
     return guard([&] {

@@ -357,6 +357,15 @@ def test_batch1_graph_replay_matches_stream_form(vitmod, weights12, cuda):
     m.embed(x, out=(host, None))
     torch.cuda.synchronize()
     assert torch.equal(host, ref[2][0].cpu())
+    # more buffer triples than the cache keeps (8): the least recently used graphs are evicted and
+    # re-captured on their next use, the results unchanged
+    outs = [torch.empty((1, 768), device=cuda) for _ in range(11)]
+    for rep in range(2):
+        for i, o in enumerate(outs):
+            m.embed(imgs[i % 3:i % 3 + 1], out=(o, None))
+        torch.cuda.synchronize()
+        for i, o in enumerate(outs):
+            assert torch.equal(o, ref[i % 3][0]), (rep, i)
     m.set_last_layer(False)
     x.copy_(imgs[0:1])
     m.embed(x, out=(raw, nrm))
