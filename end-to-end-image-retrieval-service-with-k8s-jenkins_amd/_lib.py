@@ -152,6 +152,7 @@ DIAG_SIGNATURES = {
     "rc_diag_set_attention": (C.c_int, [_vp, _i32]),
     "rc_diag_set_skinny_wpb": (C.c_int, [_vp, _i32]),
     "rc_diag_set_part_priority": (C.c_int, [_vp, _i32]),
+    "rc_diag_set_group_m": (C.c_int, [_vp, _i32]),
     "rc_diag_set_band_skip": (C.c_int, [_i32]),
     "rc_diag_set_filter_split": (C.c_int, [_i32]),
 }

@@ -63,7 +63,7 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
     return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
-// 16-B store with the non-temporal (streaming) hint (diagnostic ablations)
+// 16-B store with the non-temporal (streaming) hint
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <typename T>
 __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
@@ -195,7 +195,8 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
     // lane (g, li) of rows 16-block holds columns 4g..4g+3 of both 16-column halves ni, the
     // swap of rows 1<->0 and 3<->2 between the ni halves makes them 8 contiguous columns.
     // (Also ABL 64 for the other bf16 epilogues, QKV's LN consumer included, in diagnostic builds.)
-    constexpr bool DIRECT = EPI == EPI_GELU_BF16_LN || (epi_bf16_out(EPI) && (ABL & 64) != 0);
+    // (ABL 512, diagnostic: fc1 through the LDS-staged path with its nontemporal 512-B row stores)
+    constexpr bool DIRECT = (EPI == EPI_GELU_BF16_LN && (ABL & 512) == 0) || (epi_bf16_out(EPI) && (ABL & 64) != 0);
     if constexpr (DIRECT) {
         float4 bq[2][2], cq[2][2];
 #pragma unroll
@@ -321,8 +322,11 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
                 asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
             } else if (m0 + rl < mlim) {
                 uint4 *dst = reinterpret_cast<uint4 *>(a.out_bf16 + (int64_t)(m0 + rl) * (a.ldc ? a.ldc : a.N) + n0 + ch * 8);
-                if constexpr ((ABL & 32) != 0) nt_store16(dst, v);  // diagnostic: streaming store
-                else *dst = v;
+                // nontemporal: whole 512-B row segments stream out without allocating in L2, where
+                // they would evict the A / W panels the next tiles read (QKV at batch 256: reads
+                // 376 -> 348 MB, 181.5 -> 175.6 us per launch; round 6, r06q).  (fc1's direct
+                // 64-B row pieces are not: nontemporal there raised its writes 311 -> 430 MB.)
+                nt_store16(dst, v);
             }
         }
         return;
@@ -1352,10 +1356,12 @@ inline int gemm_pick(const GemmArgs &a, int variant, bool patch_epilogue, bool l
 // a row has >= 6 column tiles (QKV: 176 -> 170 us, fc1: 285 -> 274 us at batch
 // 256, interleaved A/B in tools/gemm_calib.py), row-major otherwise (fc2 prefers
 // it by 2 %).
-inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
-
 #if defined(RC_GEMM_ABLATION)
-inline int g_skinny_wpb = 1;  // diagnostic builds: tiles (waves) per skinny-GEMM block (rc_diag_set_skinny_wpb)
+inline int g_skinny_wpb = 1;    // diagnostic builds: tiles (waves) per skinny-GEMM block (rc_diag_set_skinny_wpb)
+inline int g_group_m_wide = 8;  // diagnostic builds: group_m of the wide ping-pong GEMMs (rc_diag_set_group_m)
+inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? g_group_m_wide : 0; }
+#else
+inline int gemm_group_m(const GemmArgs &a) { return a.N / 256 >= 6 ? 8 : 0; }
 #endif
 
 // The patch embedding of a small batch (M <= 256 patch rows, the bf16 stream: one image is
@@ -1635,7 +1641,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case 100 + 0: case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
-        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: {
+        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: case 152: {
             a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256;
             switch (variant - 100) {
@@ -1654,6 +1660,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 case 96: launch_pp<EPI, 96, PP_BM>(a, ntm, s); break;
                 case 50: launch_pp<EPI, 128, PP_BM>(a, ntm, s); break;  // staggered start, ~10 us
                 case 51: launch_pp<EPI, 256, PP_BM>(a, ntm, s); break;  // staggered start, ~5 us
+                case 52: launch_pp<EPI, 512, PP_BM>(a, ntm, s); break;  // fc1 LDS-staged, nontemporal stores
             }
             break;
         }

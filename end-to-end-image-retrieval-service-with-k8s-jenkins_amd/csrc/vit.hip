@@ -991,6 +991,17 @@ extern "C" int rc_diag_set_part_priority(rc_model *m, int prio) {
     });
 }
 
+// diagnostic builds: the ping-pong tile order of the wide GEMMs (QKV, fc1): groups of g row tiles
+// walked column-major (8, the product's; 0 = row-major)
+extern "C" int rc_diag_set_group_m(rc_model *m, int g) {
+    return guard([&] {
+        RC_REQUIRE(m && g >= 0 && g <= 64, RC_ERR_INVALID, "group_m in [0, 64]");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->clear_graphs();
+        g_group_m_wide = g;
+    });
+}
+
 // diagnostic builds: tiles (one wave each) per block of the skinny GEMM (1, the product's; 2; 4)
 extern "C" int rc_diag_set_skinny_wpb(rc_model *m, int wpb) {
     return guard([&] {
