@@ -84,7 +84,8 @@ __device__ __forceinline__ void nt_store16(T *dst, const T &v) {
 // residual stream is bf16 in a.ln_x (the statistics from the rounded values); otherwise f32
 // a.out_f32, plus the bf16 copy in a.ln_x and the partials when a.ln_x is set.  All lanes run the swaps; rows
 // >= mlim (M, or the end of an image-aligned tile's image) load a clamped row and store nothing.
-template <int EPI, int NR>
+// ABL (diagnostic builds): 1024 = the residual read nontemporal, 2048 = the stores nontemporal
+template <int EPI, int NR, int ABL = 0>
 __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4 (&A)[NR][2][2], const int (&rows)[NR],
                                                   int colw, int g, const float4 (&bq)[2][2], int mlim) {
     constexpr bool BS = epi_bf16_stream(EPI);
@@ -102,7 +103,10 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
             if constexpr (epi_resid(EPI)) {
                 const int64_t off = (int64_t)rr * a.N + col;
                 if constexpr (BS) {
-                    sh[r][c] = *reinterpret_cast<const uint4 *>(a.ln_x + off);
+                    if constexpr ((ABL & 1024) != 0)
+                        sh[r][c] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.ln_x + off)));
+                    else
+                        sh[r][c] = *reinterpret_cast<const uint4 *>(a.ln_x + off);
                 } else {
                     sf[r][c][0] = *reinterpret_cast<const float4 *>(a.out_f32 + off);
                     sf[r][c][1] = *reinterpret_cast<const float4 *>(a.out_f32 + off + 4);
@@ -152,7 +156,11 @@ __device__ __forceinline__ void f32_rows_epilogue(const GemmArgs &a, const f32x4
             const int64_t off = orow * a.N + colw + 32 * c + cl;
             if constexpr (BS) {
                 const uint4 h = bf16x8_pack(x);
-                if (ok) *reinterpret_cast<uint4 *>(a.ln_x + off) = h;
+                if constexpr ((ABL & 2048) != 0) {
+                    if (ok) nt_store16(reinterpret_cast<uint4 *>(a.ln_x + off), h);
+                } else {
+                    if (ok) *reinterpret_cast<uint4 *>(a.ln_x + off) = h;
+                }
                 float xv[8];
                 bf16x8_unpack(h, xv);
 #pragma unroll
@@ -195,7 +203,9 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
     // lane (g, li) of rows 16-block holds columns 4g..4g+3 of both 16-column halves ni, the
     // swap of rows 1<->0 and 3<->2 between the ni halves makes them 8 contiguous columns.
     // (Also ABL 64 for the other bf16 epilogues, QKV's LN consumer included, in diagnostic builds.)
-    // (ABL 512, diagnostic: fc1 through the LDS-staged path with its nontemporal 512-B row stores)
+    // Round 6 measured fc1 through the LDS-staged path with its nontemporal 512-B row stores
+    // (ABL 512): fc1 itself +1.5…6 us per launch, the fc2 after it −8 us, step +0.3 % (r06s, r06t)
+    // — within the run-to-run spread, so fc1 keeps this form.
     constexpr bool DIRECT = (EPI == EPI_GELU_BF16_LN && (ABL & 512) == 0) || (epi_bf16_out(EPI) && (ABL & 64) != 0);
     if constexpr (DIRECT) {
         float4 bq[2][2], cq[2][2];
@@ -356,7 +366,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs &a, f32x4 (&acc)[2][2
 #pragma unroll
                     for (int h = 0; h < 2; ++h) A[r][c][h] = acc[mq][c][mi][h];
             }
-            f32_rows_epilogue<EPI, NR>(a, A, rows, n0 + wc * 64, g, bq, mlim);
+            f32_rows_epilogue<EPI, NR, ABL>(a, A, rows, n0 + wc * 64, g, bq, mlim);
         }
 }
 
@@ -617,7 +627,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // with it); the f32 ones store from the accumulators.  LayerNorm-fold consumers (EPI_*_LN): the
 // tile rows' (rstd, -rstd*mu) at smem + ln_off, as gemm_pp_kernel keeps them, and the same
 // rstd·(acc − μ·c) + b′ arithmetic (the same bits).
-template <int EPI, int MI = 8>
+template <int EPI, int MI = 8, int ABL = 0>
 __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][4], uint8_t *smem, int m0, int n0,
                                             int ln_off = 0) {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -697,7 +707,7 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][
 #pragma unroll
                 for (int h = 0; h < 2; ++h) A[r][c][h] = acc[h4 * 4 + r][2 * c + h];
         }
-        f32_rows_epilogue<EPI, 4>(a, A, rows, n0 + wave * 64, g, bq, a.M);
+        f32_rows_epilogue<EPI, 4, ABL>(a, A, rows, n0 + wave * 64, g, bq, a.M);
     }
 #pragma unroll
     for (int m2 = 4 * N4; m2 < MI; m2 += 2) {
@@ -711,7 +721,7 @@ __device__ __forceinline__ void w2_epilogue(const GemmArgs &a, f32x4 (&acc)[MI][
 #pragma unroll
                 for (int h = 0; h < 2; ++h) A[r][c][h] = acc[m2 + r][2 * c + h];
         }
-        f32_rows_epilogue<EPI, 2>(a, A, rows, n0 + wave * 64, g, bq, a.M);
+        f32_rows_epilogue<EPI, 2, ABL>(a, A, rows, n0 + wave * 64, g, bq, a.M);
     }
 }
 
@@ -852,7 +862,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
             for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
         return;
     }
-    w2_epilogue<EPI, MI>(a, acc, smem, m0, n0, LN_OFF);
+    w2_epilogue<EPI, MI, ABL>(a, acc, smem, m0, n0, LN_OFF);
 }
 
 // ------------------------------------------- implicit-GEMM patch embedding ----
@@ -1624,6 +1634,15 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
+        case 301: case 302: case 303: {  // residual epilogue nontemporal reads / stores / both, 160-row W2 tiles
+            if constexpr (epi_resid(EPI)) {
+                const dim3 gr((a.M + 159) / 160 * (a.N / 256)), bl(256);
+                if (variant == 301) hipLaunchKernelGGL((gemm_w2_kernel<EPI, 1024, 160>), gr, bl, 0, s, a);
+                else if (variant == 302) hipLaunchKernelGGL((gemm_w2_kernel<EPI, 2048, 160>), gr, bl, 0, s, a);
+                else hipLaunchKernelGGL((gemm_w2_kernel<EPI, 3072, 160>), gr, bl, 0, s, a);
+            }
+            break;
+        }
         case 300: {  // the two-workgroup kernel on 128-row tiles whatever M (A/B of the 160-row pick)
             if constexpr (!epi_ln(EPI))
                 hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3((a.M + 127) / 128 * (a.N / 256)), dim3(256), 0, s, a);
@@ -1641,7 +1660,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case 100 + 0: case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
-        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: case 152: {
+        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: case 152: case 153: case 154: case 155: {
             a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256;
             switch (variant - 100) {
@@ -1661,6 +1680,9 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 case 50: launch_pp<EPI, 128, PP_BM>(a, ntm, s); break;  // staggered start, ~10 us
                 case 51: launch_pp<EPI, 256, PP_BM>(a, ntm, s); break;  // staggered start, ~5 us
                 case 52: launch_pp<EPI, 512, PP_BM>(a, ntm, s); break;  // fc1 LDS-staged, nontemporal stores
+                case 53: launch_pp<EPI, 1024, PP_BM>(a, ntm, s); break;  // residual read nontemporal
+                case 54: launch_pp<EPI, 2048, PP_BM>(a, ntm, s); break;  // residual stores nontemporal
+                case 55: launch_pp<EPI, 3072, PP_BM>(a, ntm, s); break;  // both
             }
             break;
         }
