@@ -553,6 +553,9 @@ void encode(rc_model *m, const uint8_t *images, int i0, int n, float *raw, float
         } else if (m->attn_form == 4 && T == 197) {  // v2, co-resident blocks staggered by ~6 us
             hipLaunchKernelGGL((attention_v2_kernel<197, 600>), dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f, qsplit);
+        } else if (m->attn_form == 6 && T == 197) {  // v2 with the default-policy K/V DMA (rounds 1-5)
+            hipLaunchKernelGGL((attention_v2_kernel<197, 0, 0>), dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
+                               scale * 1.4426950408889634f, qsplit);
         } else if (m->attn_form == 5 && T == 197) {  // ~3 us
             hipLaunchKernelGGL((attention_v2_kernel<197, 300>), dim3(items * qsplit), dim3(256), 0, s, qkv, attn, T, c.heads,
                                scale * 1.4426950408889634f, qsplit);
@@ -1020,7 +1023,8 @@ extern "C" int rc_diag_set_skinny_wpb(rc_model *m, int wpb) {
 // A/B) for the full-token layers (the same bits)
 extern "C" int rc_diag_set_attention(rc_model *m, int form) {
     return guard([&] {
-        RC_REQUIRE(m && form >= 2 && form <= 5, RC_ERR_INVALID, "attention form must be 2 (v2), 3 (v3), 4 / 5 (v2 staggered)");
+        RC_REQUIRE(m && form >= 2 && form <= 6, RC_ERR_INVALID,
+                   "attention form must be 2 (v2), 3 (v3), 4 / 5 (v2 staggered), 6 (v2, default-policy K/V DMA)");
         std::lock_guard<std::mutex> lk(m->mu);
         m->clear_graphs();
         m->attn_form = form;

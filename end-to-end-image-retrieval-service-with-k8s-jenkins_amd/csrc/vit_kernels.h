@@ -447,7 +447,11 @@ __device__ __forceinline__ void att_pv_store(const uint8_t *Vs, const f32x4 (&st
 // 256..767 under the dispatcher's round-robin placement) start STAG and 2·STAG s_memrealtime
 // ticks (10 ns) late, so that co-resident blocks are out of phase (one's K/V DMA under the others'
 // math) for the rest of the launch.
-template <int TOK, int STAG = 0>
+// AUX: the cache-policy bits of the K/V LDS-DMA — 2 = nontemporal: every K/V row is read by exactly
+// one block (round 6 in-model A/B, bit-identical: 72.8 -> 71.5 us per launch, step 9.19 -> 9.14 ms
+// at parts = 2, profiles/r06/r06u_attention_nt_dma_ab_p{1,2}.log); 0 = the default policy (rounds
+// 1-5, diagnostic builds)
+template <int TOK, int STAG = 0, int AUX = 2>
 __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__restrict__ qkv, uint16_t *__restrict__ out,
                                                           int tokens_rt, int heads, float scale_log2e, int qsplit) {
     if constexpr (STAG > 0) {
@@ -475,7 +479,7 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
     auto load_q = [&](int qt, bf16x8 (&qv)[2]) {
         const int q = qt * 16 + li;
         const uint16_t *qp = base + (int64_t)(q < tokens ? q : tokens - 1) * H3 + g * 8;
-        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:64"
+        asm volatile("global_load_dwordx4 %0, %2, off nt\n\tglobal_load_dwordx4 %1, %2, off offset:64 nt"
                      : "=&v"(qv[0]), "=&v"(qv[1])
                      : "v"(qp)
                      : "memory");
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(256, 3) void attention_v2_kernel(const uint16_t *__
         const int c = isv ? (pc ^ (((r >> 1) & 3) << 1)) : (pc ^ ((r >> 1) & 7));
         const int rr = r < tokens ? r : tokens - 1;
         const uint16_t *src = base + (int64_t)rr * H3 + (isv ? 2 * H : H) + c * 8;
-        __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(lds + piece * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(lds + piece * 1024), 16, 0, AUX);
     }
     auto bar = [] {
         asm volatile("" ::: "memory");
