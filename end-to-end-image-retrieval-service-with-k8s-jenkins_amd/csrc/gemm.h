@@ -465,7 +465,15 @@ __device__ __forceinline__ void pp_kloop(const GemmArgs &a, uint8_t *smem, int m
             const int r = (is_a ? piece : piece - 32) * 8 + (lane >> 3);
             const int c = (lane & 7) ^ ((r >> 1) & 7);
             const uint16_t *src = (is_a ? Ag : Wg) + (int64_t)r * K + k0 + c * 8;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+            // The residual producers' A operand (fc2: fc1's 310 MB output, each row panel read by its
+            // three column tiles at about the same time) is staged nontemporal (aux 2), so it does not
+            // displace W and the residual rows in L2 (round 6 in-model A/B: fc2 277.6 -> 264.9 us,
+            // r06x); QKV / fc1 re-read their A panels over several rounds and keep the default
+            // (ABL 4096, diagnostic: nontemporal for every GEMM: QKV 186 -> 200, fc1 294 -> 310 us)
+            if (is_a && (epi_resid(EPI) || (ABL & 4096) != 0))
+                __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 2);
+            else
+                __builtin_amdgcn_global_load_lds((const void *)src, (lds_void_t *)(base + piece * 1024), 16, 0, 0);
         }
     };
     auto bar = [] {
@@ -798,7 +806,10 @@ __global__ __launch_bounds__(256, 2) void gemm_w2_kernel(GemmArgs a) {
         for (int i = 0; i < PPW; ++i) {
             const int piece = wave + 4 * i;  // wave-uniform
             if (piece >= PIECES) continue;
-            __builtin_amdgcn_global_load_lds((const void *)(srcp[i] + k0), (lds_void_t *)(base + piece * 1024), 16, 0, 0);
+            if ((ABL & 4096) != 0 && piece < MI)  // diagnostic: the A operand's DMA nontemporal
+                __builtin_amdgcn_global_load_lds((const void *)(srcp[i] + k0), (lds_void_t *)(base + piece * 1024), 16, 0, 2);
+            else
+                __builtin_amdgcn_global_load_lds((const void *)(srcp[i] + k0), (lds_void_t *)(base + piece * 1024), 16, 0, 0);
         }
     };
     // fragment of rows r0 + li (r0 % 16 == 0), k chunk g: 16 B at row*64 + (g ^ h(li))*16
@@ -1643,6 +1654,11 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             }
             break;
         }
+        case 304: {  // residual producer on 160-row W2 tiles, A operand's DMA nontemporal
+            if constexpr (epi_resid(EPI))
+                hipLaunchKernelGGL((gemm_w2_kernel<EPI, 4096, 160>), dim3((a.M + 159) / 160 * (a.N / 256)), dim3(256), 0, s, a);
+            break;
+        }
         case 300: {  // the two-workgroup kernel on 128-row tiles whatever M (A/B of the 160-row pick)
             if constexpr (!epi_ln(EPI))
                 hipLaunchKernelGGL((gemm_w2_kernel<EPI>), dim3((a.M + 127) / 128 * (a.N / 256)), dim3(256), 0, s, a);
@@ -1660,7 +1676,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
             break;
         }
         case 100 + 0: case 100 + 1: case 100 + 2: case 100 + 3: case 100 + 4: case 100 + 5: case 100 + 6:
-        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: case 152: case 153: case 154: case 155: {
+        case 100 + 8: case 100 + 16: case 100 + 24: case 100 + 32: case 100 + 64: case 100 + 96: case 150: case 151: case 152: case 153: case 154: case 155: case 156: {
             a.group_m = gemm_group_m(a);  // the product tile order
             const int ntm = (a.M + 255) / 256;
             switch (variant - 100) {
@@ -1683,6 +1699,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 case 53: launch_pp<EPI, 1024, PP_BM>(a, ntm, s); break;  // residual read nontemporal
                 case 54: launch_pp<EPI, 2048, PP_BM>(a, ntm, s); break;  // residual stores nontemporal
                 case 55: launch_pp<EPI, 3072, PP_BM>(a, ntm, s); break;  // both
+                case 56: launch_pp<EPI, 4096, PP_BM>(a, ntm, s); break;  // A operand's DMA nontemporal
             }
             break;
         }

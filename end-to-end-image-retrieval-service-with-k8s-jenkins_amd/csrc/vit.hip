@@ -377,6 +377,9 @@ int diag_variant(const GemmArgs &a, int variant, bool patch_epilogue, bool ln_ep
     // fc2 (ping-pong) 21-23
     if (producer && variant >= 18 && variant <= 20) return a.K <= 768 ? 300 + (variant - 17) : GEMM_AUTO;
     if (producer && variant >= 21 && variant <= 23) return a.K > 768 ? 153 + (variant - 21) : GEMM_AUTO;
+    // the A operand's DMA nontemporal: 24 fc2, 25 O-proj, 26 both
+    if (producer && (variant == 24 || variant == 26) && a.K > 768) return 156;
+    if (producer && (variant == 25 || variant == 26) && a.K <= 768) return 304;
     // LayerNorm-fold consumers of a full batch on the two-workgroup kernel: 15 fc1, 16 QKV, 17 both
     if (ln_epilogue && pick == GEMM_PINGPONG &&
         (variant == 17 || (variant == 15 && a.N == 3072) || (variant == 16 && a.N != 3072)))
@@ -1037,7 +1040,7 @@ extern "C" int rc_diag_set_gemm_variant(rc_model *m, int variant) {
     return guard([&] {
         RC_REQUIRE(m, RC_ERR_INVALID, "null model");
         RC_REQUIRE(variant == GEMM_AUTO || variant == GEMM_PINGPONG || variant == GEMM_W2 || variant == GEMM_PP_IMG ||
-                       (variant >= 11 && variant <= 23) || (variant >= 100 && variant < 200),
+                       (variant >= 11 && variant <= 26) || (variant >= 100 && variant < 200),
                    RC_ERR_INVALID, "GEMM variant: 0 auto, 4 ping-pong, 8 two-workgroup, 10 image-aligned, 11-14 producer "
                                    "mixes, 15-17 LN consumers on the two-workgroup kernel, 100 + ABL");
         std::lock_guard<std::mutex> lk(m->mu);
