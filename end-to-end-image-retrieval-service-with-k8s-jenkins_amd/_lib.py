@@ -155,6 +155,7 @@ DIAG_SIGNATURES = {
     "rc_diag_set_group_m": (C.c_int, [_vp, _i32]),
     "rc_diag_set_band_skip": (C.c_int, [_i32]),
     "rc_diag_set_filter_split": (C.c_int, [_i32]),
+    "rc_diag_set_filter_aux": (C.c_int, [_i32]),
 }
 
 _lock = threading.Lock()

@@ -553,7 +553,8 @@ __device__ __forceinline__ void lds_write_u32(uint32_t *p, uint32_t v) {
     asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)p), "v"(v) : "memory");
 }
 
-template <int NKT, int RT>
+// AUX: cache-policy bits of the row DMA (0; 2 = nontemporal: diagnostic builds' A/B)
+template <int NKT, int RT, int AUX = 0>
 __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
     typedef int i32x4_t __attribute__((ext_vector_type(4)));
     constexpr int QT = QS_QT, WAVES = 16 / QS_QT, RF = RT / 16, RH = RF / 4;
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(512, 1) void filter_i8_kernel(FilterArgs a) {
         for (int i = 0; i < PPW; ++i) {
             lds_void *dst = (lds_void *)(base + (wave + WAVES * i) * 1024);
             const uint32_t off = loff[i];
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, AUX);
         }
     };
     f32x4_t sxv[RH], exv[RH];  // rows 16 rf + li of the tile, rf = 4 h + e → sxv[h][e]
@@ -941,6 +942,7 @@ int batch_stage_ratio(int k, int cap, int inflation) {
 // dispatch over rows [c0, c1) split into nchunk row chunks.
 #if defined(RC_GEMM_ABLATION)
 int g_diag_filter_split_log2 = 31;
+int g_diag_filter_aux = 0;  // the int8 filter's row DMA cache policy (rc_diag_set_filter_aux)
 #endif
 template <typename T, typename F>
 void run_stages(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer *timer, int g, int64_t row_bytes, F &&filter) {
@@ -1025,6 +1027,12 @@ void run_batched_i8(const BatchPlan &p, BatchWs &ws, hipStream_t s, KernelTimer 
         fa.sq = ws.sq;
         fa.aq = ws.aq;
         const dim3 gr((unsigned)(nchunk * nqb)), bl(64 * 16 / QS_QT);
+#if defined(RC_GEMM_ABLATION)
+        if (nkt == 4 && g_diag_filter_aux == 2) {
+            hipLaunchKernelGGL((filter_i8_kernel<4, 128, 2>), gr, bl, 0, s, fa);
+            return;
+        }
+#endif
         if (nkt == 4) hipLaunchKernelGGL((filter_i8_kernel<4, 128>), gr, bl, 0, s, fa);
         else if (nkt == 6) hipLaunchKernelGGL((filter_i8_kernel<6, 64>), gr, bl, 0, s, fa);
         else hipLaunchKernelGGL((filter_i8_kernel<2, 128>), gr, bl, 0, s, fa);
@@ -1104,6 +1112,12 @@ void BatchWs::release() {
 
 #if defined(RC_GEMM_ABLATION)
 // diagnostic builds: log2 of the bytes of rows per filter sub-launch (31 = the product's 2 GB)
+extern "C" int rc_diag_set_filter_aux(int aux) {
+    return rc::guard([&] {
+        RC_REQUIRE(aux == 0 || aux == 2, RC_ERR_INVALID, "aux 0 or 2");
+        rc::g_diag_filter_aux = aux;
+    });
+}
 extern "C" int rc_diag_set_filter_split(int log2_bytes) {
     return rc::guard([&] {
         RC_REQUIRE(log2_bytes >= 24 && log2_bytes <= 40, RC_ERR_INVALID, "log2 bytes in [24, 40]");
