@@ -1065,14 +1065,20 @@ __device__ __forceinline__ void skinny_chain_t(const uint16_t *Ar, const uint16_
 // C++ loads hipcc would wait for the whole DMA ring first).  The MFMAs run in the same k order as
 // every other kernel: the same bits.
 constexpr int SKINNY_DMA_STAGES = 6;
+// A lone image's fc1 (1 248 one-wave blocks) keeps 5 stages: 30 KB of LDS per wave puts five waves
+// on a CU, every block in one round (six stages: four per CU, a second round of 224 blocks; batch-1
+// device time 436 -> 419 us, interleaved, profiles/r06/r06ae_skinny_ring_depth_b1_ab.log).  Deeper
+// rings for the two-wave LayerNorm producers (10 stages) and five for QKV measured no better.
+constexpr int SKINNY_FC1_STAGES = 5;
 template <int NI>
 constexpr int skinny_dma_stage_bytes() { return (16 + 16 * NI) * 128; }
 
-template <int NI, int NKB>
+template <int NI, int NKB, int SK = SKINNY_DMA_STAGES>
 __device__ __forceinline__ void skinny_chain_dma(const uint16_t *__restrict__ A, int row_a0, int M, const uint16_t *__restrict__ W,
                                                  int n0, int K, uint8_t *ring, f32x4 (&acc)[NI]) {
-    constexpr int SK = SKINNY_DMA_STAGES, SB = skinny_dma_stage_bytes<NI>(), NA = 2, NW = 2 * NI, NP = NA + NW;
+    constexpr int SB = skinny_dma_stage_bytes<NI>(), NA = 2, NW = 2 * NI, NP = NA + NW;
     static_assert(NKB >= SK, "the ring is primed with SK - 1 blocks");
+    static_assert((SK - 1) * NP <= 63 && SK <= 11, "the copies in flight fit the 6-bit vmcnt");
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
     // copy sources: instruction i (A: i < 2, W: i >= 2) moves rows 8(i mod ..) + lane / 8, chunk lane % 8
     const uint16_t *src[NP];
@@ -1107,7 +1113,12 @@ __device__ __forceinline__ void skinny_chain_dma(const uint16_t *__restrict__ A,
         // block kb landed: younger copies in flight are those of blocks kb + 1 .. min(kb + SK - 2, NKB - 1)
         constexpr int X = NP;
         const int younger = min(SK - 2, NKB - 1 - kb);
-        if (younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * X) : "memory");
+        if (younger >= 9) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(9 * X) : "memory");
+        else if (younger == 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * X) : "memory");
+        else if (younger == 7) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(7 * X) : "memory");
+        else if (younger == 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * X) : "memory");
+        else if (younger == 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * X) : "memory");
+        else if (younger == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * X) : "memory");
         else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * X) : "memory");
         else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * X) : "memory");
         else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
@@ -1162,7 +1173,7 @@ __device__ __forceinline__ int skinny_block(int b, int nwg) {
 // whole launch on the CUs holding blocks), so a tile per CU where 4-wave blocks put four.
 // WPB > 1 (diagnostic builds): WPB consecutive tiles per block, one wave and one DMA ring each —
 // a one-image fc1 is 1 248 one-wave workgroups (the same bits either way).
-template <int EPI, int NI, int KT, int WPB = 1>
+template <int EPI, int NI, int KT, int WPB = 1, int SK = SKINNY_DMA_STAGES>
 __global__ __launch_bounds__(64 * WPB) void gemm_skinny_kernel(GemmArgs a) {
     const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
     const int wave = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
@@ -1173,8 +1184,8 @@ __global__ __launch_bounds__(64 * WPB) void gemm_skinny_kernel(GemmArgs a) {
     const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
     f32x4 acc[NI];
     if constexpr (KT > 0) {
-        __shared__ __attribute__((aligned(16))) uint8_t ring[WPB][SKINNY_DMA_STAGES * skinny_dma_stage_bytes<NI>()];
-        skinny_chain_dma<NI, KT / 64>(a.A, rt * 16, a.M, a.W, n0, K, ring[wave], acc);
+        __shared__ __attribute__((aligned(16))) uint8_t ring[WPB][SK * skinny_dma_stage_bytes<NI>()];
+        skinny_chain_dma<NI, KT / 64, SK>(a.A, rt * 16, a.M, a.W, n0, K, ring[wave], acc);
     } else {
         const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
         const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
@@ -1620,7 +1631,7 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 break;
             }
 #endif
-            if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768>), gr, dim3(64), 0, s, a);
+            if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768, 1, epi_gelu(EPI) ? SKINNY_FC1_STAGES : SKINNY_DMA_STAGES>), gr, dim3(64), 0, s, a);
             else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072>), gr, dim3(64), 0, s, a);
             else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 0>), gr, dim3(64), 0, s, a);
             break;
