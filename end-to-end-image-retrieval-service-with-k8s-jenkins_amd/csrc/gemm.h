@@ -1065,10 +1065,10 @@ __device__ __forceinline__ void skinny_chain_t(const uint16_t *Ar, const uint16_
 // C++ loads hipcc would wait for the whole DMA ring first).  The MFMAs run in the same k order as
 // every other kernel: the same bits.
 constexpr int SKINNY_DMA_STAGES = 6;
-// A lone image's fc1 (1 248 one-wave blocks) keeps 5 stages: 30 KB of LDS per wave puts five waves
-// on a CU, every block in one round (six stages: four per CU, a second round of 224 blocks; batch-1
-// device time 436 -> 419 us, interleaved, profiles/r06/r06ae_skinny_ring_depth_b1_ab.log).  Deeper
-// rings for the two-wave LayerNorm producers (10 stages) and five for QKV measured no better.
+// fc1 on the one-wave kernel keeps 5 stages: 30 KB of LDS per wave puts five waves on a CU (measured
+// on a lone image's 1 248 fc1 tiles, before gemm_skinny_shared_kernel took them: six stages left a
+// second round of 224 blocks; device time 436 -> 419 us, profiles/r06/r06ae_skinny_ring_depth_b1_ab.log).
+// Deeper rings for the two-wave LayerNorm producers (10 stages) and five for QKV measured no better.
 constexpr int SKINNY_FC1_STAGES = 5;
 template <int NI>
 constexpr int skinny_dma_stage_bytes() { return (16 + 16 * NI) * 128; }
@@ -1169,29 +1169,10 @@ __device__ __forceinline__ int skinny_block(int b, int nwg) {
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
 }
 
-// One wave per block: the loads are address-bound (PMC: the texture addresser busy for the
-// whole launch on the CUs holding blocks), so a tile per CU where 4-wave blocks put four.
-// WPB > 1 (diagnostic builds): WPB consecutive tiles per block, one wave and one DMA ring each —
-// a one-image fc1 is 1 248 one-wave workgroups (the same bits either way).
-template <int EPI, int NI, int KT, int WPB = 1, int SK = SKINNY_DMA_STAGES>
-__global__ __launch_bounds__(64 * WPB) void gemm_skinny_kernel(GemmArgs a) {
-    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-    const int wave = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-    const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
-    const int w = skinny_block(blockIdx.x, gridDim.x) * WPB + wave;
-    if (w >= nct * nrt) return;
-    const int ct = w / nrt, rt = w % nrt;
-    const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
-    f32x4 acc[NI];
-    if constexpr (KT > 0) {
-        __shared__ __attribute__((aligned(16))) uint8_t ring[WPB][SK * skinny_dma_stage_bytes<NI>()];
-        skinny_chain_dma<NI, KT / 64, SK>(a.A, rt * 16, a.M, a.W, n0, K, ring[wave], acc);
-    } else {
-        const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
-        const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
-        skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
-    }
-    if (row >= a.M) return;
+// The skinny kernels' epilogue (not the LayerNorm producers): lane (g, li) holds row `row`, columns
+// n0 + 16 ni + 4g .. + 3 of acc[ni]
+template <int EPI, int NI>
+__device__ __forceinline__ void skinny_epilogue(const GemmArgs &a, const f32x4 (&acc)[NI], int row, int n0, int g) {
     float2 lrs;  // LayerNorm fold: this row's (rstd, -rstd*mu), as gemm_pp_kernel computes it
     if constexpr (epi_ln(EPI)) lrs = ln_row_scale(a.ln_stats + (int64_t)row * LN_STRIDE, a.ln_eps);
 #pragma unroll
@@ -1228,6 +1209,131 @@ __global__ __launch_bounds__(64 * WPB) void gemm_skinny_kernel(GemmArgs a) {
                 make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
         }
     }
+}
+
+// One wave per block: the loads are address-bound (PMC: the texture addresser busy for the
+// whole launch on the CUs holding blocks), so a tile per CU where 4-wave blocks put four.
+// WPB > 1 (diagnostic builds): WPB consecutive tiles per block, one wave and one DMA ring each —
+// a one-image fc1 is 1 248 one-wave workgroups (the same bits either way).
+template <int EPI, int NI, int KT, int WPB = 1, int SK = SKINNY_DMA_STAGES>
+__global__ __launch_bounds__(64 * WPB) void gemm_skinny_kernel(GemmArgs a) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int wave = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    const int nct = a.N / (16 * NI), nrt = (a.M + 15) / 16;
+    const int w = skinny_block(blockIdx.x, gridDim.x) * WPB + wave;
+    if (w >= nct * nrt) return;
+    const int ct = w / nrt, rt = w % nrt;
+    const int K = a.K, n0 = ct * 16 * NI, row = rt * 16 + li;
+    f32x4 acc[NI];
+    if constexpr (KT > 0) {
+        __shared__ __attribute__((aligned(16))) uint8_t ring[WPB][SK * skinny_dma_stage_bytes<NI>()];
+        skinny_chain_dma<NI, KT / 64, SK>(a.A, rt * 16, a.M, a.W, n0, K, ring[wave], acc);
+    } else {
+        const uint16_t *Ar = a.A + (int64_t)min(row, a.M - 1) * K + 8 * g;  // rows past M: clamped loads, no stores
+        const uint16_t *Wr = a.W + (int64_t)(n0 + li) * K + 8 * g;
+        skinny_chain<NI, KT>(Ar, Wr, K, K / 32, acc);
+    }
+    if (row >= a.M) return;
+    skinny_epilogue<EPI, NI>(a, acc, row, n0, g);
+}
+
+// Weights shared by SKR row tiles (QKV / fc1 of a lone image, K = 768 / 3072): a block of SKR waves
+// owns SKR consecutive 16-row tiles of one 32-column tile; per 64-deep K block each wave copies its
+// own 16 A rows and a quarter of the 32 W rows into one LDS stage, and every wave reads all 32 W rows
+// from it — W crosses L2 -> CU once per row group instead of once per row tile (a one-image fc1
+// moved 61 MB of W for 4.7 MB of unique weights).  Per stage: A at wave·2048 (16 rows), W at
+// SKR·2048 (32 rows), 128-B rows with skinny_chain_dma's swizzle.  One barrier per K block: a wave
+// has its own copies of block kb (counted vmcnt), the barrier says every wave's have landed and that
+// every wave has read block kb − 1, whose stage is then refilled.  Waves of a row group past M copy
+// clamped rows and skip the stores.  Each wave's MFMA chain is skinny_chain_dma's: the same bits.
+constexpr int SKR = 4;
+template <int NKB, int SK>
+__device__ __forceinline__ void skinny_chain_dma_shared(const uint16_t *__restrict__ A, int row_a0, int M, const uint16_t *__restrict__ W,
+                                                        int n0, int K, uint8_t *ring, int wave, f32x4 (&acc)[2]) {
+    constexpr int NI = 2, SB = (SKR * 16 + 32) * 128, NP = 3, WOFF = SKR * 2048;
+    static_assert(NKB >= SK && (SK - 1) * NP <= 63 && SK <= 11, "ring depth: primed with SK - 1 blocks, 6-bit vmcnt");
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    // copies: i = 0, 1: A rows 8i + lane / 8 of the wave's tile; i = 2: W row 8·wave + lane / 8
+    const uint16_t *src[NP];
+    uint32_t dst[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int r = i < 2 ? i * 8 + (lane >> 3) : wave * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        src[i] = (i < 2 ? A + (int64_t)min(row_a0 + r, M - 1) * K : W + (int64_t)(n0 + r) * K) + c * 8;
+        dst[i] = i < 2 ? (uint32_t)(wave * 2048 + i * 1024) : (uint32_t)(WOFF + wave * 1024);
+    }
+    auto issue = [&](int kb) __attribute__((always_inline)) {
+        uint8_t *st = ring + (kb % SK) * SB;
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + kb * 64), (lds_void_t *)(st + dst[i]), 16, 0, 0);
+    };
+    uint32_t fa[2], fw[2][NI];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const int c = (4 * s2 + g) ^ ((li >> 1) & 7);
+        fa[s2] = (uint32_t)(wave * 2048 + li * 128 + c * 16);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) fw[s2][ni] = (uint32_t)(WOFF + (16 * ni + li) * 128 + c * 16);
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < SK - 1; ++kb) issue(kb);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        constexpr int X = NP;
+        const int younger = min(SK - 2, NKB - 1 - kb);
+        if (younger >= 9) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(9 * X) : "memory");
+        else if (younger == 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * X) : "memory");
+        else if (younger == 7) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(7 * X) : "memory");
+        else if (younger == 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * X) : "memory");
+        else if (younger == 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * X) : "memory");
+        else if (younger == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * X) : "memory");
+        else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * X) : "memory");
+        else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * X) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const uint32_t st = (uint32_t)(uintptr_t)(ring + (kb % SK) * SB);
+        bf16x8 a[2], w[2][NI];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            asm volatile("ds_read_b128 %0, %1" : "=v"(a[s2]) : "v"(st + fa[s2]));
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) asm volatile("ds_read_b128 %0, %1" : "=v"(w[s2][ni]) : "v"(st + fw[s2][ni]));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1]));
+        // every wave passed this barrier after reading block kb - 1: its stage takes block kb + SK - 1
+        if (kb + SK - 1 < NKB) issue(kb + SK - 1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+                acc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[s2][ni], a[s2], acc[ni], 0, 0, 0);
+    }
+}
+
+// grid: (N / 32) · ceil(ceil(M / 16) / SKR) blocks of SKR waves, column-tile-major through skinny_block
+template <int EPI, int KT, int SK = SKINNY_DMA_STAGES>
+__global__ __launch_bounds__(64 * SKR) void gemm_skinny_shared_kernel(GemmArgs a) {
+    constexpr int NI = 2;
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nct = a.N / 32, nrt = (a.M + 15) / 16, nrg = (nrt + SKR - 1) / SKR;
+    const int b = skinny_block(blockIdx.x, gridDim.x);
+    if (b >= nct * nrg) return;  // block-uniform
+    const int ct = b / nrg, rt = (b % nrg) * SKR + wave;
+    const int n0 = ct * 32, row = rt * 16 + li;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[SK * (SKR * 16 + 32) * 128];
+    f32x4 acc[NI];
+    skinny_chain_dma_shared<KT / 64, SK>(a.A, rt * 16, a.M, a.W, n0, a.K, ring, wave, acc);
+    if (row >= a.M) return;
+    skinny_epilogue<EPI, NI>(a, acc, row, n0, g);
 }
 
 // The skinny GEMM as a LayerNorm-fold producer (residual epilogues with ln_x + ln_stats, N = 768:
@@ -1616,7 +1722,8 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                     break;
                 }
             }
-            const dim3 gr(((a.M + 15) / 16) * (a.N / 32));  // one wave (tile) per block
+            const int nrt = (a.M + 15) / 16;
+            const dim3 gr(nrt * (a.N / 32));  // one wave (tile) per block
 #if defined(RC_GEMM_ABLATION)
             if (g_skinny_wpb > 1 && (a.K == 768 || a.K == 3072)) {  // diagnostic: WPB tiles per block
                 const unsigned nb = (unsigned)(((a.M + 15) / 16) * (a.N / 32) + g_skinny_wpb - 1) / g_skinny_wpb;
@@ -1631,6 +1738,16 @@ void launch_gemm(const GemmArgs &a_in, int variant, hipStream_t s) {
                 break;
             }
 #endif
+            // more one-wave tiles than the one-wave kernel holds resident (4-5 per CU: a lone image's
+            // fc1, 1 248): row tiles share the weights, SKR per block (fc1 7.68 -> 7.16 us per launch in
+            // rocprofv3; QKV's 936 tiles stay one per block: 5.84 vs 6.16 us shared,
+            // profiles/r06/r06ai_skinny_shared_w_b1_ab.log)
+            if (nrt > 1 && nrt * (a.N / 32) > 1024 && (a.K == 768 || a.K == 3072)) {
+                const dim3 gs((unsigned)((a.N / 32) * ((nrt + SKR - 1) / SKR)));
+                if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_shared_kernel<EPI, 768>), gs, dim3(64 * SKR), 0, s, a);
+                else hipLaunchKernelGGL((gemm_skinny_shared_kernel<EPI, 3072>), gs, dim3(64 * SKR), 0, s, a);
+                break;
+            }
             if (a.K == 768) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 768, 1, epi_gelu(EPI) ? SKINNY_FC1_STAGES : SKINNY_DMA_STAGES>), gr, dim3(64), 0, s, a);
             else if (a.K == 3072) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 3072>), gr, dim3(64), 0, s, a);
             else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, 2, 0>), gr, dim3(64), 0, s, a);
