@@ -53,10 +53,14 @@ def test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
 
 
 @pytest.mark.parametrize("variant", [0, 9])
-@pytest.mark.parametrize("M,N,K", [(1, 768, 768), (85, 3072, 768), (86, 768, 3072), (256, 2304, 768), (17, 32, 64)])
+@pytest.mark.parametrize("M,N,K", [(1, 768, 768), (85, 3072, 768), (86, 768, 3072), (256, 2304, 768), (17, 32, 64),
+                                   (200, 3072, 768), (230, 2304, 3072)])
 @pytest.mark.parametrize("epi", [EPI_BF16, EPI_GELU, EPI_RESID])
 def test_skinny_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi):
-    """M <= 256 (the CLS rows of the last layer): auto picks the skinny kernel (variant 9)."""
+    """M <= 256 (the CLS rows of the last layer): auto picks the skinny kernel (variant 9).  More than
+    1024 16x32 tiles take the shared-weight form (four row tiles per block): (256, 2304, 768) with full
+    row groups, (200, 3072, 768) and (230, 2304, 3072) with a partial last group (1 and 3 of 4 row
+    tiles below M)."""
     test_gemm_matches_torch_fp32(cuda, variant, M, N, K, epi)
 
 
