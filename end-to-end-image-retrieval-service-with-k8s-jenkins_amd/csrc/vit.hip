@@ -108,9 +108,15 @@ struct rc_model {
     bool use_graphs = true;
     std::vector<EmbedGraph> graphs;
     uint64_t graph_tick = 0;
+    // misses in a row, and the last missed triple: once kMaxGraphs calls in a row missed (the
+    // caller's buffers churn), only a triple that misses twice in a row is captured
+    int graph_miss_streak = 0;
+    EmbedGraph last_miss{};
     void clear_graphs() {
         for (auto &g : graphs) (void)hipGraphExecDestroy(g.exec);
         graphs.clear();
+        graph_miss_streak = 0;
+        last_miss = EmbedGraph{};
     }
 
     void *alloc(size_t bytes) {
@@ -651,6 +657,13 @@ void forward_graph(rc_model *m, const uint8_t *images, float *raw, float *normed
     for (auto &g : m->graphs)
         if (g.images == images && g.raw == raw && g.normed == normed) e = &g;
     if (e == nullptr) {
+        const bool repeat = m->last_miss.images == images && m->last_miss.raw == raw && m->last_miss.normed == normed;
+        m->last_miss.images = images, m->last_miss.raw = raw, m->last_miss.normed = normed;
+        if (m->graph_miss_streak++ >= rc_model::kMaxGraphs && !repeat) {
+            // every call brings new buffers: a capture per call would cost more than it saves
+            forward(m, images, 1, m->cfg.image_size, m->cfg.image_size, raw, normed, s);
+            return;
+        }
         if ((int)m->graphs.size() >= rc_model::kMaxGraphs) {
             auto old = std::min_element(m->graphs.begin(), m->graphs.end(),
                                         [](const auto &a, const auto &b) { return a.last < b.last; });
@@ -675,6 +688,8 @@ void forward_graph(rc_model *m, const uint8_t *images, float *raw, float *normed
         RC_HIP(err);
         m->graphs.push_back({images, raw, normed, ex, 0});
         e = &m->graphs.back();
+    } else {
+        m->graph_miss_streak = 0;
     }
     e->last = ++m->graph_tick;
     RC_HIP(hipGraphLaunch(e->exec, s));

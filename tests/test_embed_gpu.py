@@ -326,7 +326,8 @@ def test_batch1_graph_replay_matches_stream_form(vitmod, weights12, cuda):
     """A one-image embed replays a captured HIP graph (rc_model_set_graphs, default on): the same
     bits as the stream form, for new contents in the same buffers (the graph reads them at replay),
     for a second buffer triple (a second graph), into pinned host memory, and after a setter (which
-    drops the captured graphs: the replay follows the new setting)."""
+    drops the captured graphs: the replay follows the new setting); with more triples than the
+    cache keeps, and when every call brings new buffers (churn: the stream form, no capture)."""
     import torch
 
     rng = np.random.default_rng(31)
@@ -366,6 +367,13 @@ def test_batch1_graph_replay_matches_stream_form(vitmod, weights12, cuda):
         torch.cuda.synchronize()
         for i, o in enumerate(outs):
             assert torch.equal(o, ref[i % 3][0]), (rep, i)
+    # 22 misses in a row put the cache in churn mode (new triples run the stream form); a triple
+    # used twice in a row is captured again and replayed from then on
+    for rep in range(3):
+        x.copy_(imgs[rep:rep + 1])
+        m.embed(x, out=(raw, nrm))
+        torch.cuda.synchronize()
+        assert torch.equal(raw, ref[rep][0]) and torch.equal(nrm, ref[rep][1]), rep
     m.set_last_layer(False)
     x.copy_(imgs[0:1])
     m.embed(x, out=(raw, nrm))
