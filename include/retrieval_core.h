@@ -290,8 +290,10 @@ int rc_model_set_ln_fold(rc_model *m, int on);
 /* Batch-1 HIP graphs (default 1): an rc_embed of one image at the model's input size
  * (the reference's /embed request, embedding/main.py:88-124) replays a HIP graph of its
  * launch chain, captured on first use per (images, raw_out, normed_out) buffer triple
- * (at most 8 kept, least recently used evicted): one host launch per request instead of
- * ~70.  Same kernels, same bits.  Every setter drops the captured graphs.  0 = stream form. */
+ * (at most 8 kept, least recently used evicted; after 8 misses in a row only a triple that
+ * misses twice in a row is captured, the others run the stream form): one host launch per
+ * request instead of ~70.  Same kernels, same bits.  Every setter drops the captured graphs.
+ * 0 = stream form. */
 int rc_model_set_graphs(rc_model *m, int on);
 
 /* Per-kernel timing with HIP events on the launch stream (bench/roofline).
